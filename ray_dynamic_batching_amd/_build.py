@@ -1,0 +1,140 @@
+"""In-tree build of the native extensions (no setuptools / hipify involved).
+
+* ``_rdb_ops``     -- gfx950 HIP kernels (MFMA GEMM / implicit-GEMM conv, norms,
+                      attention, softmax-top-k, gather) + the replica Engine.
+                      Built with ``hipcc --offload-arch=gfx950``.
+* ``_rdb_runtime`` -- host runtime (shm rings, router, load generator,
+                      consumer).  Pure C++, built with g++ so it works on
+                      CPU-only hosts.
+
+Both land next to this file so they travel with the repository snapshot.
+Usage: ``python -m ray_dynamic_batching_amd._build [--force] [--only ops|runtime]``.
+"""
+from __future__ import annotations
+
+import argparse
+import concurrent.futures as cf
+import os
+import shutil
+import subprocess
+import sys
+import sysconfig
+from pathlib import Path
+
+PKG = Path(__file__).resolve().parent
+OPS_SRC = PKG / "ops" / "csrc"
+RT_SRC = PKG / "runtime" / "csrc"
+BUILD = PKG.parent / "build" / "native"
+EXT = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
+ARCH = os.environ.get("RDB_OFFLOAD_ARCH", "gfx950")
+ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
+
+
+def _pybind_includes() -> list[str]:
+    import pybind11
+
+    return [f"-I{sysconfig.get_paths()['include']}", f"-I{pybind11.get_include()}"]
+
+
+def ops_target() -> Path:
+    return PKG / f"_rdb_ops{EXT}"
+
+
+def runtime_target() -> Path:
+    return PKG / f"_rdb_runtime{EXT}"
+
+
+def _ops_sources() -> list[Path]:
+    return sorted(OPS_SRC.glob("*.hip")) + sorted(OPS_SRC.glob("*.cpp"))
+
+
+def _deps(srcs: list[Path], extra_dirs: list[Path]) -> list[Path]:
+    deps = list(srcs)
+    for d in extra_dirs:
+        deps += list(d.glob("*.h"))
+    return deps
+
+
+def _stale(target: Path, deps: list[Path]) -> bool:
+    if not target.exists():
+        return True
+    t = target.stat().st_mtime
+    return any(p.stat().st_mtime > t for p in deps)
+
+
+def _run(cmd: list[str]) -> None:
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"build failed: {' '.join(cmd)}\n{r.stdout}")
+
+
+def hipcc() -> str:
+    p = shutil.which("hipcc") or os.path.join(ROCM, "bin", "hipcc")
+    if not os.path.exists(p):
+        raise RuntimeError("hipcc not found; set ROCM_PATH")
+    return p
+
+
+def build_ops(force: bool = False, jobs: int | None = None, verbose: bool = False) -> Path:
+    target = ops_target()
+    srcs = _ops_sources()
+    if not force and not _stale(target, _deps(srcs, [OPS_SRC, RT_SRC])):
+        return target
+    BUILD.mkdir(parents=True, exist_ok=True)
+    cc = hipcc()
+    common = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wno-unused-result",
+              f"-I{OPS_SRC}", f"-I{RT_SRC}"] + _pybind_includes()
+    objs = []
+    cmds = []
+    for s in srcs:
+        o = BUILD / (s.name + ".o")
+        objs.append(o)
+        lang = ["-x", "hip"] if s.suffix == ".hip" else []
+        cmds.append([cc] + common + lang + ["-c", str(s), "-o", str(o)])
+    jobs = jobs or min(8, os.cpu_count() or 4, 16)
+    with cf.ThreadPoolExecutor(jobs) as ex:
+        for c in cmds:
+            if verbose:
+                print(" ".join(c))
+        list(ex.map(_run, cmds))
+    tmp = target.with_suffix(".tmp.so")
+    _run([cc, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", str(tmp)] + [str(o) for o in objs]
+         + [f"-L{ROCM}/lib", "-lamdhip64"])
+    os.replace(tmp, target)
+    return target
+
+
+def build_runtime(force: bool = False) -> Path:
+    target = runtime_target()
+    srcs = [RT_SRC / "runtime.cpp"]
+    if not force and not _stale(target, _deps(srcs, [RT_SRC])):
+        return target
+    cxx = os.environ.get("CXX", "g++")
+    tmp = target.with_suffix(".tmp.so")
+    _run([cxx, "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", "-Wno-unused-function",
+          "-fvisibility=hidden", f"-I{RT_SRC}"] + _pybind_includes() + [str(s) for s in srcs]
+         + ["-o", str(tmp), "-lrt", "-pthread"])
+    os.replace(tmp, target)
+    return target
+
+
+def build_all(force: bool = False, verbose: bool = False) -> None:
+    build_runtime(force)
+    build_ops(force, verbose=verbose)
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("--only", choices=["ops", "runtime"])
+    ap.add_argument("-v", "--verbose", action="store_true")
+    a = ap.parse_args(argv)
+    if a.only in (None, "runtime"):
+        print("built", build_runtime(a.force))
+    if a.only in (None, "ops"):
+        print("built", build_ops(a.force, verbose=a.verbose))
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,386 @@
+"""Python wrappers of the gfx950 kernels, plus plain-PyTorch fp32 references.
+
+Every wrapper validates shapes / dtypes / strides / alignment on the host
+before launching (a mis-shaped launch on the GPU can take the whole node down),
+allocates its output with the torch caching allocator and launches on
+``torch.cuda.current_stream()`` -- so the calls are capturable into hipGraphs.
+
+The ``*_ref`` functions are the numerics references used by the tests and the
+eager baseline path of the models (``backend="torch"``).
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional, Tuple
+
+import torch
+import torch.nn.functional as F
+
+from ..utils.native import require_gpu_ops
+
+DTYPE_CODE = {torch.bfloat16: 0, torch.float16: 1, torch.float32: 2}
+ACT_CODE = {"none": 0, "gelu": 1, "relu": 2, "tanh": 3, "silu": 4, "gelu_tanh": 5, "swiglu": 6}
+
+
+def _ops():
+    return require_gpu_ops()
+
+
+def _stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _ptr(t: Optional[torch.Tensor]) -> int:
+    return 0 if t is None else t.data_ptr()
+
+
+def _check(cond: bool, msg: str) -> None:
+    if not cond:
+        raise ValueError(msg)
+
+
+def _aligned(t: torch.Tensor, n: int = 16) -> bool:
+    return t.data_ptr() % n == 0
+
+
+# ---------------------------------------------------------------------------
+# GEMM (+ fused bias / activation / residual epilogue)
+# ---------------------------------------------------------------------------
+def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, act: str = "none",
+           residual: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None,
+           out_dtype: Optional[torch.dtype] = None, alpha: float = 1.0, tile_cfg: int = -1) -> torch.Tensor:
+    """y = act(alpha * x @ w.T + bias + residual).  x: [..., K] or a 2-D row-strided
+    view; w: [N, K] contiguous.  act="swiglu" expects w rows interleaved (gate, up)
+    and returns N/2 columns."""
+    _check(x.is_cuda and w.is_cuda, "linear: tensors must be on the GPU")
+    _check(x.dtype in (torch.bfloat16, torch.float16) and w.dtype == x.dtype, "linear: bf16/f16 inputs of equal dtype")
+    _check(w.dim() == 2 and w.is_contiguous(), "linear: w must be a contiguous [N, K] matrix")
+    N, K = w.shape
+    _check(x.shape[-1] == K, f"linear: K mismatch {tuple(x.shape)} vs {tuple(w.shape)}")
+    _check(K % 8 == 0, "linear: K must be a multiple of 8")
+    if x.dim() == 2 and x.stride(1) == 1:
+        x2, lead = x, (x.shape[0],)
+    else:
+        _check(x.is_contiguous(), "linear: x must be contiguous (or a 2-D row-strided view)")
+        lead = tuple(x.shape[:-1])
+        x2 = x.reshape(-1, K)
+    M = x2.shape[0]
+    lda = x2.stride(0)
+    _check(lda % 8 == 0 and _aligned(x2) and _aligned(w), "linear: rows must be 16-byte aligned")
+    n_out = N // 2 if act == "swiglu" else N
+    od = out_dtype or x.dtype
+    if out is None:
+        out = torch.empty(*lead, n_out, device=x.device, dtype=od)
+    _check(out.is_contiguous() and out.shape[-1] == n_out and out.numel() == M * n_out, "linear: bad out")
+    if bias is not None:
+        _check(bias.is_contiguous() and bias.numel() == N and bias.dtype == x.dtype, "linear: bad bias")
+    ldr = 0
+    if residual is not None:
+        _check(residual.dtype == x.dtype and residual.shape[-1] == n_out and residual.is_contiguous()
+               and residual.numel() == M * n_out, "linear: bad residual")
+        ldr = n_out
+    _ops().gemm_tn(DTYPE_CODE[x.dtype], DTYPE_CODE[od], x2.data_ptr(), lda, w.data_ptr(), K, out.data_ptr(),
+                   n_out, _ptr(bias), _ptr(residual), ldr, M, N, K, float(alpha), ACT_CODE[act], _stream(),
+                   int(tile_cfg))
+    return out
+
+
+def _act_ref(y: torch.Tensor, act: str) -> torch.Tensor:
+    if act == "gelu":
+        return F.gelu(y)
+    if act == "gelu_tanh":
+        return F.gelu(y, approximate="tanh")
+    if act == "relu":
+        return F.relu(y)
+    if act == "tanh":
+        return torch.tanh(y)
+    if act == "silu":
+        return F.silu(y)
+    return y
+
+
+def linear_ref(x, w, bias=None, act="none", residual=None, out_dtype=None, alpha=1.0):
+    y = alpha * (x.float() @ w.float().t())
+    if bias is not None:
+        y = y + bias.float()
+    if act == "swiglu":
+        g, u = y[..., 0::2], y[..., 1::2]
+        y = F.silu(g) * u
+        if residual is not None:
+            y = y + residual.float()
+    else:
+        if residual is not None:
+            y = y + residual.float()
+        y = _act_ref(y, act)
+    return y.to(out_dtype or x.dtype)
+
+
+# ---------------------------------------------------------------------------
+# Norms
+# ---------------------------------------------------------------------------
+def _norm(x, gamma, beta, eps, residual, residual_out, mode):
+    _check(x.is_cuda and x.is_contiguous() and x.dtype in (torch.bfloat16, torch.float16), "norm: bad x")
+    D = x.shape[-1]
+    rows = x.numel() // D
+    _check(D % 256 == 0 and D <= 8192, "norm: D must be a multiple of 256, <= 8192")
+    _check(gamma.numel() == D and gamma.dtype == x.dtype, "norm: bad gamma")
+    if beta is not None:
+        _check(beta.numel() == D and beta.dtype == x.dtype, "norm: bad beta")
+    if residual is not None:
+        _check(residual.shape == x.shape and residual.is_contiguous() and residual.dtype == x.dtype, "norm: bad residual")
+    if residual_out is not None:
+        _check(residual_out.shape == x.shape and residual_out.is_contiguous(), "norm: bad residual_out")
+    y = torch.empty_like(x)
+    _ops().norm_fwd(DTYPE_CODE[x.dtype], mode, x.data_ptr(), _ptr(residual), _ptr(residual_out),
+                    gamma.data_ptr(), _ptr(beta), y.data_ptr(), rows, D, float(eps), _stream())
+    return y
+
+
+def layer_norm(x, gamma, beta, eps=1e-12, residual=None, residual_out=None):
+    """LayerNorm(x [+ residual]) (optionally also writing x + residual)."""
+    return _norm(x, gamma, beta, eps, residual, residual_out, 0)
+
+
+def rms_norm(x, gamma, eps=1e-5, residual=None, residual_out=None):
+    return _norm(x, gamma, None, eps, residual, residual_out, 1)
+
+
+def layer_norm_ref(x, gamma, beta, eps=1e-12, residual=None):
+    xf = x.float() + (residual.float() if residual is not None else 0)
+    return F.layer_norm(xf, (x.shape[-1],), gamma.float(), beta.float(), eps).to(x.dtype)
+
+
+def rms_norm_ref(x, gamma, eps=1e-5, residual=None):
+    xf = x.float() + (residual.float() if residual is not None else 0)
+    return (xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps) * gamma.float()).to(x.dtype)
+
+
+def embed_ln(ids, word, pos, typ, gamma, beta, eps=1e-12, types=None):
+    """BERT embeddings: LN(word[ids] + pos[t % S] + type[types or 0]); ids [B, S] int32."""
+    _check(ids.dtype == torch.int32 and ids.is_contiguous() and ids.dim() == 2, "embed_ln: ids must be [B, S] int32")
+    B, S = ids.shape
+    D = word.shape[1]
+    _check(pos.shape[0] >= S and pos.shape[1] == D and typ.shape[1] == D, "embed_ln: table shapes")
+    _check(D % 256 == 0, "embed_ln: hidden size must be a multiple of 256")
+    if types is not None:
+        _check(types.dtype == torch.int32 and types.shape == ids.shape and types.is_contiguous(), "embed_ln: bad types")
+    y = torch.empty(B * S, D, device=ids.device, dtype=word.dtype)
+    _ops().embed_ln_fwd(DTYPE_CODE[word.dtype], ids.data_ptr(), _ptr(types), word.data_ptr(), pos.data_ptr(),
+                        typ.data_ptr(), gamma.data_ptr(), beta.data_ptr(), y.data_ptr(), B * S, S, D,
+                        word.shape[0], float(eps), _stream())
+    return y
+
+
+def embed_ln_ref(ids, word, pos, typ, gamma, beta, eps=1e-12, types=None):
+    B, S = ids.shape
+    idl = ids.long().clamp(0, word.shape[0] - 1)
+    x = word.float()[idl] + pos.float()[:S][None] + typ.float()[(types.long() if types is not None else torch.zeros_like(idl))]
+    return F.layer_norm(x, (word.shape[1],), gamma.float(), beta.float(), eps).to(word.dtype).reshape(B * S, -1)
+
+
+# ---------------------------------------------------------------------------
+# Attention
+# ---------------------------------------------------------------------------
+def attention(qkv: torch.Tensor, B: int, S: int, H: int, Hkv: int, D: int, lens: Optional[torch.Tensor] = None,
+              causal: bool = False, scale: Optional[float] = None, out: Optional[torch.Tensor] = None,
+              q_off: int = 0, k_off: Optional[int] = None, v_off: Optional[int] = None) -> torch.Tensor:
+    """Fused MHA / GQA on the packed projection output qkv [B*S, ld] (q | k | v)."""
+    _check(qkv.is_cuda and qkv.dtype == torch.bfloat16 and qkv.dim() == 2 and qkv.stride(1) == 1, "attention: bad qkv")
+    _check(qkv.shape[0] == B * S, "attention: qkv rows must be B*S")
+    _check(D in (64, 128), "attention: head dim must be 64 or 128")
+    _check(H % Hkv == 0, "attention: H % Hkv")
+    k_off = H * D if k_off is None else k_off
+    v_off = (H + Hkv) * D if v_off is None else v_off
+    ld = qkv.stride(0)
+    _check(max(q_off + H * D, k_off + Hkv * D, v_off + Hkv * D) <= qkv.shape[1], "attention: offsets exceed row")
+    _check(ld % 8 == 0 and q_off % 8 == 0 and k_off % 8 == 0 and v_off % 8 == 0 and _aligned(qkv), "attention: alignment")
+    if lens is not None:
+        _check(lens.dtype == torch.int32 and lens.numel() == B and lens.is_cuda, "attention: lens must be int32 [B]")
+    if out is None:
+        out = torch.empty(B * S, H * D, device=qkv.device, dtype=qkv.dtype)
+    _check(out.is_contiguous() and out.shape == (B * S, H * D), "attention: bad out")
+    scale = 1.0 / math.sqrt(D) if scale is None else scale
+    _ops().attn_fwd(qkv.data_ptr(), ld, q_off, k_off, v_off, B, H, Hkv, S, D, _ptr(lens), int(causal),
+                    out.data_ptr(), H * D, float(scale), _stream())
+    return out
+
+
+def attention_ref(qkv, B, S, H, Hkv, D, lens=None, causal=False, scale=None, q_off=0, k_off=None, v_off=None):
+    k_off = H * D if k_off is None else k_off
+    v_off = (H + Hkv) * D if v_off is None else v_off
+    x = qkv.float()
+    q = x[:, q_off:q_off + H * D].reshape(B, S, H, D).transpose(1, 2)
+    k = x[:, k_off:k_off + Hkv * D].reshape(B, S, Hkv, D).transpose(1, 2)
+    v = x[:, v_off:v_off + Hkv * D].reshape(B, S, Hkv, D).transpose(1, 2)
+    if Hkv != H:
+        k = k.repeat_interleave(H // Hkv, dim=1)
+        v = v.repeat_interleave(H // Hkv, dim=1)
+    scale = 1.0 / math.sqrt(D) if scale is None else scale
+    s = (q @ k.transpose(-1, -2)) * scale
+    keys = torch.arange(S, device=qkv.device)
+    mask = torch.zeros(B, 1, S, S, dtype=torch.bool, device=qkv.device)
+    if lens is not None:
+        mask |= (keys[None, None, None, :] >= lens.long()[:, None, None, None])
+    if causal:
+        mask |= keys[None, None, None, :] > keys[None, None, :, None]
+    s = s.masked_fill(mask, float("-inf"))
+    p = torch.softmax(s, dim=-1)
+    p = torch.nan_to_num(p, nan=0.0)
+    o = (p @ v).transpose(1, 2).reshape(B * S, H * D)
+    return o.to(qkv.dtype)
+
+
+# ---------------------------------------------------------------------------
+# Heads / misc
+# ---------------------------------------------------------------------------
+def softmax_topk(logits: torch.Tensor, k: int) -> Tuple[torch.Tensor, torch.Tensor]:
+    _check(logits.is_cuda and logits.dtype == torch.float32 and logits.dim() == 2 and logits.is_contiguous(),
+           "softmax_topk: logits must be contiguous f32 [B, C]")
+    B, C = logits.shape
+    _check(C <= 4096 and 1 <= k <= min(16, C), "softmax_topk: C <= 4096 and 1 <= k <= 16")
+    probs = torch.empty(B, k, device=logits.device, dtype=torch.float32)
+    idx = torch.empty(B, k, device=logits.device, dtype=torch.int32)
+    _ops().softmax_topk(logits.data_ptr(), B, C, k, probs.data_ptr(), idx.data_ptr(), _stream())
+    return probs, idx
+
+
+def softmax_topk_ref(logits, k):
+    p = torch.softmax(logits.float(), dim=-1)
+    v, i = torch.topk(p, k, dim=-1)
+    return v, i.to(torch.int32)
+
+
+def rope_tables(max_pos: int, D: int, theta: float = 500000.0, device=None):
+    inv = 1.0 / (theta ** (torch.arange(0, D, 2, dtype=torch.float64) / D))
+    t = torch.arange(max_pos, dtype=torch.float64)
+    f = torch.outer(t, inv)
+    return f.cos().float().to(device), f.sin().float().to(device)
+
+
+def rope_(qkv, cos, sin, B, S, H, Hkv, D, q_off=0, k_off=None, pos_offset=0):
+    """In-place rotary embedding of the q and k heads of qkv [B*S, ld]."""
+    _check(qkv.is_cuda and qkv.dtype == torch.bfloat16 and qkv.dim() == 2 and qkv.stride(1) == 1, "rope: bad qkv")
+    _check(cos.dtype == torch.float32 and cos.shape[1] == D // 2 and cos.shape[0] >= S + pos_offset, "rope: bad tables")
+    k_off = H * D if k_off is None else k_off
+    _ops().rope(qkv.data_ptr(), qkv.stride(0), q_off, k_off, H, Hkv, D, S, cos.data_ptr(), sin.data_ptr(),
+                B * S, pos_offset, _stream())
+    return qkv
+
+
+def rope_ref(qkv, cos, sin, B, S, H, Hkv, D, q_off=0, k_off=None, pos_offset=0):
+    k_off = H * D if k_off is None else k_off
+    x = qkv.float().clone()
+    pos = (torch.arange(B * S, device=qkv.device) % S) + pos_offset
+    c, s = cos[pos][:, None, :], sin[pos][:, None, :]
+
+    def rot(a):
+        a1, a2 = a[..., : D // 2], a[..., D // 2:]
+        return torch.cat([a1 * c - a2 * s, a2 * c + a1 * s], dim=-1)
+
+    x[:, q_off:q_off + H * D] = rot(x[:, q_off:q_off + H * D].reshape(-1, H, D)).reshape(-1, H * D)
+    x[:, k_off:k_off + Hkv * D] = rot(x[:, k_off:k_off + Hkv * D].reshape(-1, Hkv, D)).reshape(-1, Hkv * D)
+    return x.to(qkv.dtype)
+
+
+def gather_rows(src_ptrs: torch.Tensor, n: int, rows: int, row_bytes: int, dst: torch.Tensor):
+    _ops().gather_rows(src_ptrs.data_ptr(), n, rows, row_bytes, dst.data_ptr(), _stream())
+
+
+def image_to_nhwc(img_u8: torch.Tensor, Cp: int = 8) -> torch.Tensor:
+    """uint8 [N, H, W, 3] -> normalised f16 [N, H, W, Cp] (ImageNet mean/std)."""
+    _check(img_u8.is_cuda and img_u8.dtype == torch.uint8 and img_u8.is_contiguous() and img_u8.shape[-1] == 3, "image_to_nhwc: bad input")
+    N, H, W, _ = img_u8.shape
+    out = torch.empty(N, H, W, Cp, device=img_u8.device, dtype=torch.float16)
+    _ops().image_to_nhwc(img_u8.data_ptr(), N, H * W, Cp, out.data_ptr(), _stream())
+    return out
+
+
+def image_to_nhwc_ref(img_u8, Cp=8):
+    mean = torch.tensor([0.485, 0.456, 0.406], device=img_u8.device)
+    std = torch.tensor([0.229, 0.224, 0.225], device=img_u8.device)
+    x = (img_u8.float() / 255.0 - mean) / std
+    pad = torch.zeros(*x.shape[:-1], Cp - 3, device=x.device)
+    return torch.cat([x, pad], -1).half()
+
+
+# ---------------------------------------------------------------------------
+# Convolution family (NHWC f16)
+# ---------------------------------------------------------------------------
+def conv2d_nhwc(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, stride: int = 1,
+                pad: int = 0, act: str = "none", residual: Optional[torch.Tensor] = None,
+                out: Optional[torch.Tensor] = None, tile_cfg: int = -1) -> torch.Tensor:
+    """x [N, H, W, C] f16, w [K, R, S, C] f16 (BN folded), bias [K]; fused residual + act."""
+    _check(x.is_cuda and x.dtype == torch.float16 and x.is_contiguous() and x.dim() == 4, "conv2d: bad x")
+    _check(w.dtype == torch.float16 and w.is_contiguous() and w.dim() == 4, "conv2d: bad w")
+    N, H, W, C = x.shape
+    K, R, S, C2 = w.shape
+    _check(C == C2 and C % 8 == 0, f"conv2d: channel mismatch/alignment {C} vs {C2}")
+    P = (H + 2 * pad - R) // stride + 1
+    Q = (W + 2 * pad - S) // stride + 1
+    if out is None:
+        out = torch.empty(N, P, Q, K, device=x.device, dtype=torch.float16)
+    _check(out.shape == (N, P, Q, K) and out.is_contiguous(), "conv2d: bad out")
+    if bias is not None:
+        _check(bias.numel() == K and bias.dtype == torch.float16, "conv2d: bad bias")
+    if residual is not None:
+        _check(residual.shape == (N, P, Q, K) and residual.is_contiguous() and residual.dtype == torch.float16, "conv2d: bad residual")
+    _check(_aligned(x) and _aligned(w), "conv2d: alignment")
+    _ops().conv2d_nhwc(x.data_ptr(), w.data_ptr(), _ptr(bias), _ptr(residual), out.data_ptr(), N, H, W, C, K, R, S,
+                       stride, pad, P, Q, ACT_CODE[act], _stream(), int(tile_cfg))
+    return out
+
+
+def conv2d_nhwc_ref(x, w, bias=None, stride=1, pad=0, act="none", residual=None):
+    y = F.conv2d(x.permute(0, 3, 1, 2).float(), w.permute(0, 3, 1, 2).float(),
+                 bias.float() if bias is not None else None, stride=stride, padding=pad)
+    y = y.permute(0, 2, 3, 1)
+    if residual is not None:
+        y = y + residual.float()
+    return _act_ref(y, act).to(torch.float16)
+
+
+def dwconv_nhwc(x, w, bias, stride=1, pad=1, act="none"):
+    """Depthwise conv: x [N, H, W, C], w [R, R, C], bias [C]."""
+    _check(x.is_cuda and x.dtype == torch.float16 and x.is_contiguous(), "dwconv: bad x")
+    N, H, W, C = x.shape
+    R = w.shape[0]
+    _check(w.shape == (R, R, C) and w.is_contiguous() and bias.numel() == C and C % 8 == 0, "dwconv: bad w/bias")
+    P = (H + 2 * pad - R) // stride + 1
+    Q = (W + 2 * pad - R) // stride + 1
+    out = torch.empty(N, P, Q, C, device=x.device, dtype=torch.float16)
+    _ops().dwconv_nhwc(x.data_ptr(), w.data_ptr(), bias.data_ptr(), out.data_ptr(), N, H, W, C, R, stride, pad, P, Q,
+                       ACT_CODE[act], _stream())
+    return out
+
+
+def dwconv_nhwc_ref(x, w, bias, stride=1, pad=1, act="none"):
+    C = x.shape[-1]
+    y = F.conv2d(x.permute(0, 3, 1, 2).float(), w.permute(2, 0, 1).unsqueeze(1).float(), bias.float(),
+                 stride=stride, padding=pad, groups=C)
+    return _act_ref(y.permute(0, 2, 3, 1), act).to(torch.float16)
+
+
+def maxpool_nhwc(x, k=3, stride=2, pad=1):
+    _check(x.is_cuda and x.dtype == torch.float16 and x.is_contiguous() and x.shape[-1] % 8 == 0, "maxpool: bad x")
+    N, H, W, C = x.shape
+    P = (H + 2 * pad - k) // stride + 1
+    Q = (W + 2 * pad - k) // stride + 1
+    out = torch.empty(N, P, Q, C, device=x.device, dtype=torch.float16)
+    _ops().maxpool_nhwc(x.data_ptr(), out.data_ptr(), N, H, W, C, k, stride, pad, P, Q, _stream())
+    return out
+
+
+def maxpool_nhwc_ref(x, k=3, stride=2, pad=1):
+    return F.max_pool2d(x.permute(0, 3, 1, 2).float(), k, stride, pad).permute(0, 2, 3, 1).half()
+
+
+def avgpool_nhwc(x):
+    _check(x.is_cuda and x.dtype == torch.float16 and x.is_contiguous() and x.shape[-1] % 8 == 0, "avgpool: bad x")
+    N, H, W, C = x.shape
+    out = torch.empty(N, C, device=x.device, dtype=torch.float16)
+    _ops().avgpool_nhwc(x.data_ptr(), out.data_ptr(), N, H * W, C, _stream())
+    return out
+
+
+def avgpool_nhwc_ref(x):
+    return x.float().mean(dim=(1, 2)).half()

@@ -1,0 +1,230 @@
+// Fused multi-head attention forward for gfx950 (flash-style, online softmax).
+//
+// Reads Q/K/V straight out of the packed projection output [T, (H+2*Hkv)*D]
+// (no transpose kernels), supports a per-sequence key length (padding mask),
+// causal masking and GQA (Hkv divides H).  Used by BERT-base (S=128, D=64,
+// bidirectional) and Llama-3 prefill (D=128, causal, GQA).
+//
+// One workgroup = 4 waves = 128 query rows of one (batch, head); each wave owns
+// 32 query rows.  K/V blocks of 128 keys are staged in LDS:
+//   * K row-major [key][D] with the 16-B chunk XOR swizzle (ds_read_b128 frags);
+//   * V transposed [D][128 + 8] (the +8 element pad makes the 8-byte fragment
+//     reads of 16 d-rows x 2 key groups conflict-free).
+// Swapped products keep softmax lane-local (cdna_hip_programming.md T12 idea):
+//   S^T = K . Q^T   (A = K frag from LDS, B = Q frag in registers)
+//        -> each lane holds 4 keys x (key tiles) for ONE query, so the row
+//           max / sum need only 2 cross-lane steps (xor 16, xor 32);
+//   O^T += V^T . P^T (A = V^T frag from LDS, B = P taken from the S^T
+//        accumulator registers with a permuted-but-consistent k order, §3)
+//        -> each lane holds 4 consecutive d of one query: 8-byte stores.
+#include "common.h"
+#include <stdexcept>
+
+namespace rdb {
+
+template <int D>
+struct AttnCfg {
+  static constexpr int KB = 128;                 // keys per LDS block
+  static constexpr int ROWB = D * 2;             // bytes per K row
+  static constexpr int CPR = ROWB / 16;          // 16-B chunks per K row (8 or 16)
+  static constexpr int VT_LD = KB + 8;           // V^T row length (elements)
+  static constexpr int K_BYTES = KB * ROWB;
+  static constexpr int V_BYTES = D * VT_LD * 2;
+};
+
+template <int CPR>
+__device__ __forceinline__ int kswz(int row, int chunk) {
+  if constexpr (CPR == 8) return row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4);
+  else return row * (CPR * 16) + ((chunk ^ (row & 15)) << 4);
+}
+
+template <int D>
+__global__ void __launch_bounds__(256, 2)
+attn_fwd_kernel(const bf16* __restrict__ qkv, int ld_qkv, int q_off, int k_off, int v_off,
+                int H, int Hkv, int S, const int* __restrict__ lens, int causal,
+                bf16* __restrict__ out, int ld_out, float scale_log2e) {
+  typedef AttnCfg<D> C;
+  constexpr int KB = C::KB;
+  constexpr int NKT = KB / 16;       // key tiles per block
+  constexpr int NKS = D / 32;        // k-steps for S = K.Q^T
+  constexpr int NDT = D / 16;        // d tiles of O^T
+  __shared__ __attribute__((aligned(16))) char smem[C::K_BYTES + C::V_BYTES];
+  char* Ks = smem;
+  bf16* Vt = reinterpret_cast<bf16*>(smem + C::K_BYTES);
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int fr = lane & 15, fg = lane >> 4;
+  const int b = blockIdx.z, h = blockIdx.y;
+  const int hk = h / (H / Hkv);
+  const int q0 = blockIdx.x * 128 + wid * 32;  // this wave's first query row
+  const size_t tok0 = (size_t)b * S;
+  int kv_len = lens ? lens[b] : S;
+  kv_len = kv_len > S ? S : kv_len;
+
+  // Q fragments (B operand): lane holds Q[q][ks*32 + 8*fg + j].
+  bf16x8 qf[2][NKS];
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt) {
+    const int q = q0 + qt * 16 + fr;
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+      if (q < S)
+        qf[qt][ks] = *reinterpret_cast<const bf16x8*>(qkv + (tok0 + q) * ld_qkv + q_off + h * D +
+                                                        ks * 32 + fg * 8);
+      else
+        qf[qt][ks] = bf16x8{};
+    }
+  }
+
+  f32x4 o[NDT][2];
+#pragma unroll
+  for (int i = 0; i < NDT; ++i) o[i][0] = o[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m_run[2] = {-INFINITY, -INFINITY}, l_run[2] = {0.f, 0.f};
+
+  // Causal: keys beyond the block's last query are never needed.
+  int key_end = kv_len;
+  if (causal) {
+    const int qlast = blockIdx.x * 128 + 127;
+    key_end = key_end < qlast + 1 ? key_end : qlast + 1;
+  }
+  const int nblk = (key_end + KB - 1) / KB;
+
+  for (int kb = 0; kb < nblk; ++kb) {
+    const int key0 = kb * KB;
+    __syncthreads();  // previous block's LDS reads are done
+    // ---- stage K (row-major, swizzled) ----
+#pragma unroll
+    for (int i = 0; i < KB * C::CPR / 256; ++i) {
+      const int qd = tid + 256 * i, row = qd / C::CPR, c = qd % C::CPR;
+      const int key = key0 + row;
+      u32x4 v = {0, 0, 0, 0};
+      if (key < S) v = *reinterpret_cast<const u32x4*>(qkv + (tok0 + key) * ld_qkv + k_off + hk * D + c * 8);
+      *reinterpret_cast<u32x4*>(Ks + kswz<C::CPR>(row, c)) = v;
+    }
+    // ---- stage V transposed: lanes of a wave take consecutive keys ----
+#pragma unroll
+    for (int i = 0; i < KB * C::CPR / 256; ++i) {
+      const int qd = tid + 256 * i, row = qd & (KB - 1), c = qd / KB;
+      const int key = key0 + row;
+      bf16x8 v = bf16x8{};
+      if (key < S) v = *reinterpret_cast<const bf16x8*>(qkv + (tok0 + key) * ld_qkv + v_off + hk * D + c * 8);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) Vt[(c * 8 + j) * C::VT_LD + row] = v[j];
+    }
+    __syncthreads();
+
+    // ---- S^T = K . Q^T ----
+    f32x4 s[NKT][2];
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt) {
+      s[kt][0] = s[kt][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < NKS; ++ks) {
+        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(Ks + kswz<C::CPR>(kt * 16 + fr, ks * 4 + fg));
+        s[kt][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[0][ks], s[kt][0], 0, 0, 0);
+        s[kt][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[1][ks], s[kt][1], 0, 0, 0);
+      }
+    }
+
+    // ---- mask, online softmax (lane-local query q = q0 + qt*16 + fr) ----
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) {
+      const int q = q0 + qt * 16 + fr;
+      float mx = -INFINITY;
+#pragma unroll
+      for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int key = key0 + kt * 16 + fg * 4 + e;
+          float x = s[kt][qt][e] * scale_log2e;
+          const bool masked = (key >= kv_len) || (causal && key > q);
+          x = masked ? -INFINITY : x;
+          s[kt][qt][e] = x;
+          mx = fmaxf(mx, x);
+        }
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float m_new = fmaxf(m_run[qt], mx);
+      const float m_use = (m_new == -INFINITY) ? 0.f : m_new;
+      const float alpha = exp2f(m_run[qt] - m_use);
+      m_run[qt] = m_new;
+      l_run[qt] *= alpha;
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt) o[dt][qt] *= alpha;
+      float ls = 0.f;
+#pragma unroll
+      for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float p = exp2f(s[kt][qt][e] - m_use);
+          s[kt][qt][e] = p;
+          ls += p;
+        }
+      l_run[qt] += ls;  // partial over this lane's keys; reduced across fg at the end
+    }
+
+    // ---- O^T += V^T . P^T over 4 chunks of 32 keys ----
+#pragma unroll
+    for (int c = 0; c < KB / 32; ++c) {
+      bf16x8 pf[2];
+#pragma unroll
+      for (int qt = 0; qt < 2; ++qt) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          pf[qt][e] = (bf16)s[2 * c][qt][e];
+          pf[qt][4 + e] = (bf16)s[2 * c + 1][qt][e];
+        }
+      }
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt) {
+        const bf16* vr = Vt + (dt * 16 + fr) * C::VT_LD + c * 32 + fg * 4;
+        const bf16x4 lo = *reinterpret_cast<const bf16x4*>(vr);
+        const bf16x4 hi = *reinterpret_cast<const bf16x4*>(vr + 16);
+        const bf16x8 vf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        o[dt][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[0], o[dt][0], 0, 0, 0);
+        o[dt][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[1], o[dt][1], 0, 0, 0);
+      }
+    }
+  }
+
+  // ---- normalise and store: lane holds O[q][dt*16 + 4*fg + e] ----
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt) {
+    float l = l_run[qt];
+    l += __shfl_xor(l, 16, 64);
+    l += __shfl_xor(l, 32, 64);
+    const float inv = l > 0.f ? 1.f / l : 0.f;
+    const int q = q0 + qt * 16 + fr;
+    if (q >= S) continue;
+    bf16* op = out + (tok0 + q) * ld_out + h * D;
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt) {
+      const bf16x4 v = {(bf16)(o[dt][qt][0] * inv), (bf16)(o[dt][qt][1] * inv),
+                        (bf16)(o[dt][qt][2] * inv), (bf16)(o[dt][qt][3] * inv)};
+      *reinterpret_cast<bf16x4*>(op + dt * 16 + fg * 4) = v;
+    }
+  }
+}
+
+void attn_fwd(uintptr_t qkv, int ld_qkv, int q_off, int k_off, int v_off, int B, int H, int Hkv,
+              int S, int D, uintptr_t lens, int causal, uintptr_t out, int ld_out, float scale,
+              uintptr_t stream) {
+  if (H % Hkv != 0) throw std::invalid_argument("attn: H must be a multiple of Hkv");
+  if (ld_qkv % 8 || q_off % 8 || k_off % 8 || v_off % 8 || ld_out % 4)
+    throw std::invalid_argument("attn: strides/offsets must be 16-byte aligned");
+  if (B <= 0 || S <= 0) return;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  dim3 grid((S + 127) / 128, H, B), blk(256);
+  const float sl2e = scale * 1.4426950408889634f;
+  if (D == 64)
+    hipLaunchKernelGGL((attn_fwd_kernel<64>), grid, blk, 0, s, (const bf16*)qkv, ld_qkv, q_off, k_off,
+                       v_off, H, Hkv, S, (const int*)lens, causal, (bf16*)out, ld_out, sl2e);
+  else if (D == 128)
+    hipLaunchKernelGGL((attn_fwd_kernel<128>), grid, blk, 0, s, (const bf16*)qkv, ld_qkv, q_off, k_off,
+                       v_off, H, Hkv, S, (const int*)lens, causal, (bf16*)out, ld_out, sl2e);
+  else
+    throw std::invalid_argument("attn: head dim must be 64 or 128");
+  RDB_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace rdb

@@ -1,0 +1,76 @@
+// pybind11 bindings of the gfx950 kernels.  Every tensor crosses the boundary
+// as a raw device address (uintptr_t) plus explicit shapes/strides, and every
+// launch goes on the caller's HIP stream, so the Python wrappers stay thin and
+// the launches are capturable into hipGraphs (torch.cuda.graph).
+#include <hip/hip_runtime.h>
+#include <pybind11/pybind11.h>
+#include <stdexcept>
+#include <string>
+
+namespace py = pybind11;
+
+namespace rdb {
+void gemm_tn(int in_dtype, int out_dtype, uintptr_t A, int lda, uintptr_t W, int ldw, uintptr_t C,
+             int ldc, uintptr_t bias, uintptr_t R, int ldr, int M, int N, int K, float alpha,
+             int act, uintptr_t stream, int force_cfg);
+void norm_fwd(int dtype, int mode, uintptr_t x, uintptr_t res, uintptr_t res_out, uintptr_t gamma,
+              uintptr_t beta, uintptr_t y, int rows, int D, float eps, uintptr_t stream);
+void embed_ln_fwd(int dtype, uintptr_t ids, uintptr_t types, uintptr_t word, uintptr_t pos,
+                  uintptr_t typ, uintptr_t gamma, uintptr_t beta, uintptr_t y, int tokens, int S,
+                  int D, int vocab, float eps, uintptr_t stream);
+void attn_fwd(uintptr_t qkv, int ld_qkv, int q_off, int k_off, int v_off, int B, int H, int Hkv,
+              int S, int D, uintptr_t lens, int causal, uintptr_t out, int ld_out, float scale,
+              uintptr_t stream);
+void softmax_topk(uintptr_t x, int rows, int C, int k, uintptr_t probs, uintptr_t idx, uintptr_t stream);
+void rope(uintptr_t qkv, int ld, int q_off, int k_off, int H, int Hkv, int D, int S, uintptr_t cos_t,
+          uintptr_t sin_t, int T, int pos_offset, uintptr_t stream);
+void gather_rows(uintptr_t src_ptrs, int n, int rows, int row_bytes, uintptr_t dst, uintptr_t stream);
+void image_to_nhwc(uintptr_t src, int N, int HW, int Cp, uintptr_t dst, uintptr_t stream);
+void conv2d_nhwc(uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t res, uintptr_t y, int N, int H,
+                 int W, int C, int K, int R, int S, int stride, int pad, int P, int Q, int act,
+                 uintptr_t stream, int force_cfg);
+void maxpool_nhwc(uintptr_t x, uintptr_t y, int N, int H, int W, int C, int k, int stride, int pad,
+                  int P, int Q, uintptr_t stream);
+void avgpool_nhwc(uintptr_t x, uintptr_t y, int N, int HW, int C, uintptr_t stream);
+void dwconv_nhwc(uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t y, int N, int H, int W, int C,
+                 int R, int stride, int pad, int P, int Q, int act, uintptr_t stream);
+void register_engine(py::module_& m);
+}  // namespace rdb
+
+static void hip_check(hipError_t e, const char* what) {
+  if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+PYBIND11_MODULE(_rdb_ops, m) {
+  m.doc() = "ray_dynamic_batching_amd gfx950 kernels (MFMA GEMM/conv, norm, attention, ...)";
+  m.def("gemm_tn", &rdb::gemm_tn, py::call_guard<py::gil_scoped_release>());
+  m.def("norm_fwd", &rdb::norm_fwd, py::call_guard<py::gil_scoped_release>());
+  m.def("embed_ln_fwd", &rdb::embed_ln_fwd, py::call_guard<py::gil_scoped_release>());
+  m.def("attn_fwd", &rdb::attn_fwd, py::call_guard<py::gil_scoped_release>());
+  m.def("softmax_topk", &rdb::softmax_topk, py::call_guard<py::gil_scoped_release>());
+  m.def("rope", &rdb::rope, py::call_guard<py::gil_scoped_release>());
+  m.def("gather_rows", &rdb::gather_rows, py::call_guard<py::gil_scoped_release>());
+  m.def("image_to_nhwc", &rdb::image_to_nhwc, py::call_guard<py::gil_scoped_release>());
+  m.def("conv2d_nhwc", &rdb::conv2d_nhwc, py::call_guard<py::gil_scoped_release>());
+  m.def("maxpool_nhwc", &rdb::maxpool_nhwc, py::call_guard<py::gil_scoped_release>());
+  m.def("avgpool_nhwc", &rdb::avgpool_nhwc, py::call_guard<py::gil_scoped_release>());
+  m.def("dwconv_nhwc", &rdb::dwconv_nhwc, py::call_guard<py::gil_scoped_release>());
+
+  // Pinning of shared-memory regions so the device can read request payloads
+  // in place (zero-copy H2D gather) -- the "pinned shm tensor arena".
+  m.def("host_register", [](uintptr_t ptr, size_t bytes) {
+    hip_check(hipHostRegister(reinterpret_cast<void*>(ptr), bytes, hipHostRegisterMapped), "hipHostRegister");
+    void* dev = nullptr;
+    hip_check(hipHostGetDevicePointer(&dev, reinterpret_cast<void*>(ptr), 0), "hipHostGetDevicePointer");
+    return reinterpret_cast<uintptr_t>(dev);
+  });
+  m.def("host_unregister", [](uintptr_t ptr) {
+    hip_check(hipHostUnregister(reinterpret_cast<void*>(ptr)), "hipHostUnregister");
+  });
+  m.def("device_count", []() {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+  });
+  rdb::register_engine(m);
+}

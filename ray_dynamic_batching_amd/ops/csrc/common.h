@@ -1,0 +1,79 @@
+// Shared device helpers for the gfx950 (CDNA4) kernels of ray_dynamic_batching_amd.
+//
+// Everything here is written for a 64-lane wavefront and the gfx950 MFMA
+// instruction set; there is no portability layer.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <hip/hip_bf16.h>
+#include <stdint.h>
+
+namespace rdb {
+
+typedef __bf16 bf16;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 f16;
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+
+constexpr int kWave = 64;
+
+__device__ __forceinline__ float bf2f(bf16 x) { return (float)x; }
+__device__ __forceinline__ bf16 f2bf(float x) { return (bf16)x; }  // RNE, NaN-preserving (v_cvt_pk_bf16_f32)
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Epilogue activations shared by GEMM / conv kernels.
+// ACT_SWIGLU is a GEMM-only pairing epilogue: W rows are interleaved (gate_j, up_j),
+// the output has N/2 columns and holds silu(gate_j) * up_j.
+enum Act : int { ACT_NONE = 0, ACT_GELU = 1, ACT_RELU = 2, ACT_TANH = 3, ACT_SILU = 4, ACT_GELU_TANH = 5, ACT_SWIGLU = 6 };
+
+template <int ACT>
+__device__ __forceinline__ float apply_act(float x) {
+  if constexpr (ACT == ACT_GELU) {
+    return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f));
+  } else if constexpr (ACT == ACT_RELU) {
+    return fmaxf(x, 0.0f);
+  } else if constexpr (ACT == ACT_TANH) {
+    return tanhf(x);
+  } else if constexpr (ACT == ACT_SILU) {
+    return x / (1.0f + __expf(-x));
+  } else if constexpr (ACT == ACT_GELU_TANH) {
+    const float c = 0.7978845608028654f;
+    return 0.5f * x * (1.0f + tanhf(c * (x + 0.044715f * x * x * x)));
+  } else {
+    return x;
+  }
+}
+
+// Bijective XCD-aware remap of a linear workgroup id (MI355X: 8 XCDs, blocks
+// dealt round-robin).  Consecutive *logical* tiles land on the same XCD so
+// they share that XCD's L2 (guide T1; bijective form for nwg % 8 != 0).
+__device__ __forceinline__ int xcd_remap(int orig, int nwg) {
+  const int q = nwg >> 3, r = nwg & 7;
+  const int xcd = orig & 7, idx = orig >> 3;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
+}
+
+}  // namespace rdb
+
+#define RDB_HIP_CHECK(expr)                                                        \
+  do {                                                                             \
+    hipError_t _e = (expr);                                                        \
+    if (_e != hipSuccess) throw std::runtime_error(std::string("HIP error: ") +    \
+                                                   hipGetErrorString(_e) + " @ " + \
+                                                   __FILE__ + ":" + std::to_string(__LINE__)); \
+  } while (0)

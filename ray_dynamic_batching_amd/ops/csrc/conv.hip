@@ -1,0 +1,156 @@
+// NHWC convolution family for gfx950 (ResNet-50 / ShuffleNet / EfficientNet
+// forward):
+//   * conv2d_nhwc  - implicit-GEMM conv on MFMA (f16): the im2col matrix is
+//                    gathered tile-by-tile into LDS by Im2colLoader (never
+//                    materialised); BN is folded into (W, bias) at load time and
+//                    bias + residual + ReLU/SiLU are fused into the epilogue.
+//   * dwconv_nhwc  - depthwise conv (memory-bound; 8 channels per lane, 16-B loads)
+//   * maxpool_nhwc / avgpool_nhwc (global average pool feeding the FC GEMM)
+#include "gemm_core.h"
+#include <stdexcept>
+
+namespace rdb {
+
+void conv2d_nhwc(uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t res, uintptr_t y, int N, int H,
+                 int W, int C, int K, int R, int S, int stride, int pad, int P, int Q, int act,
+                 uintptr_t stream, int force_cfg) {
+  if (C % 8 != 0) throw std::invalid_argument("conv2d_nhwc: C must be a multiple of 8 (pad channels)");
+  if ((x | w) & 15) throw std::invalid_argument("conv2d_nhwc: x/w must be 16-byte aligned");
+  const int M = N * P * Q, Kg = R * S * C;
+  if (M <= 0 || K <= 0) return;
+  ConvParams p{reinterpret_cast<const void*>(x), N, H, W, C, R, S, stride, pad, P, Q, M, Kg};
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (R == 1 && S == 1 && stride == 1 && pad == 0) {
+    // 1x1 stride-1 conv is a plain GEMM over the NHWC pixels.
+    DenseParams d{reinterpret_cast<const void*>(x), C, M, C};
+    launch_mfma_gemm<f16, f16, DenseLoader>(d, (const f16*)w, Kg, (f16*)y, K, (const f16*)bias,
+                                            (const f16*)res, K, M, K, Kg, 1.f, act, s, force_cfg);
+  } else {
+    launch_mfma_gemm<f16, f16, Im2colLoader>(p, (const f16*)w, Kg, (f16*)y, K, (const f16*)bias,
+                                             (const f16*)res, K, M, K, Kg, 1.f, act, s, force_cfg);
+  }
+  RDB_HIP_CHECK(hipGetLastError());
+}
+
+// Depthwise RxR conv, NHWC f16, weights [R][R][C] (channel-contiguous), bias [C].
+// One thread = 8 channels of one output pixel.
+__global__ void __launch_bounds__(256)
+dwconv_kernel(const f16* __restrict__ x, const f16* __restrict__ w, const f16* __restrict__ b,
+              f16* __restrict__ y, int N, int H, int W, int C, int R, int stride, int pad, int P, int Q,
+              int act) {
+  const int cg = C >> 3;
+  const long total = (long)N * P * Q * cg;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+    const int c8 = e % cg;
+    const long pix = e / cg;
+    const int q = pix % Q;
+    const int p = (pix / Q) % P;
+    const int n = pix / ((long)P * Q);
+    float acc[8];
+    const f16x8 bv = *reinterpret_cast<const f16x8*>(b + c8 * 8);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] = (float)bv[j];
+    for (int r = 0; r < R; ++r) {
+      const int h = p * stride - pad + r;
+      if ((unsigned)h >= (unsigned)H) continue;
+      for (int s = 0; s < R; ++s) {
+        const int ww = q * stride - pad + s;
+        if ((unsigned)ww >= (unsigned)W) continue;
+        const f16x8 xv = *reinterpret_cast<const f16x8*>(x + (((size_t)n * H + h) * W + ww) * C + c8 * 8);
+        const f16x8 wv = *reinterpret_cast<const f16x8*>(w + ((size_t)r * R + s) * C + c8 * 8);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] += (float)xv[j] * (float)wv[j];
+      }
+    }
+    f16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = (f16)act_rt(act, acc[j]);
+    *reinterpret_cast<f16x8*>(y + (size_t)pix * C + c8 * 8) = o;
+  }
+}
+
+void dwconv_nhwc(uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t y, int N, int H, int W, int C,
+                 int R, int stride, int pad, int P, int Q, int act, uintptr_t stream) {
+  if (C % 8 != 0) throw std::invalid_argument("dwconv_nhwc: C must be a multiple of 8");
+  const long total = (long)N * P * Q * (C / 8);
+  if (total <= 0) return;
+  int blocks = (int)std::min<long>((total + 255) / 256, 8192);
+  hipLaunchKernelGGL(dwconv_kernel, dim3(blocks), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+                     (const f16*)x, (const f16*)w, (const f16*)bias, (f16*)y, N, H, W, C, R, stride, pad,
+                     P, Q, act);
+  RDB_HIP_CHECK(hipGetLastError());
+}
+
+__global__ void __launch_bounds__(256)
+maxpool_kernel(const f16* __restrict__ x, f16* __restrict__ y, int N, int H, int W, int C, int k,
+               int stride, int pad, int P, int Q) {
+  const int cg = C >> 3;
+  const long total = (long)N * P * Q * cg;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+    const int c8 = e % cg;
+    const long pix = e / cg;
+    const int q = pix % Q;
+    const int p = (pix / Q) % P;
+    const int n = pix / ((long)P * Q);
+    float m[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) m[j] = -INFINITY;
+    for (int r = 0; r < k; ++r) {
+      const int h = p * stride - pad + r;
+      if ((unsigned)h >= (unsigned)H) continue;
+      for (int s = 0; s < k; ++s) {
+        const int ww = q * stride - pad + s;
+        if ((unsigned)ww >= (unsigned)W) continue;
+        const f16x8 xv = *reinterpret_cast<const f16x8*>(x + (((size_t)n * H + h) * W + ww) * C + c8 * 8);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) m[j] = fmaxf(m[j], (float)xv[j]);
+      }
+    }
+    f16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = (f16)m[j];
+    *reinterpret_cast<f16x8*>(y + (size_t)pix * C + c8 * 8) = o;
+  }
+}
+
+void maxpool_nhwc(uintptr_t x, uintptr_t y, int N, int H, int W, int C, int k, int stride, int pad,
+                  int P, int Q, uintptr_t stream) {
+  if (C % 8 != 0) throw std::invalid_argument("maxpool_nhwc: C must be a multiple of 8");
+  const long total = (long)N * P * Q * (C / 8);
+  if (total <= 0) return;
+  int blocks = (int)std::min<long>((total + 255) / 256, 8192);
+  hipLaunchKernelGGL(maxpool_kernel, dim3(blocks), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+                     (const f16*)x, (f16*)y, N, H, W, C, k, stride, pad, P, Q);
+  RDB_HIP_CHECK(hipGetLastError());
+}
+
+// Global average pool: one block per (n, 2048-channel slice); lanes own 8 channels.
+__global__ void __launch_bounds__(256)
+avgpool_kernel(const f16* __restrict__ x, f16* __restrict__ y, int N, int HW, int C) {
+  const int n = blockIdx.y;
+  const int c8 = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c8 * 8 >= C) return;
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const f16* base = x + (size_t)n * HW * C + c8 * 8;
+  for (int i = 0; i < HW; ++i) {
+    const f16x8 v = *reinterpret_cast<const f16x8*>(base + (size_t)i * C);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] += (float)v[j];
+  }
+  f16x8 o;
+  const float inv = 1.f / HW;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o[j] = (f16)(acc[j] * inv);
+  *reinterpret_cast<f16x8*>(y + (size_t)n * C + c8 * 8) = o;
+}
+
+void avgpool_nhwc(uintptr_t x, uintptr_t y, int N, int HW, int C, uintptr_t stream) {
+  if (C % 8 != 0) throw std::invalid_argument("avgpool_nhwc: C must be a multiple of 8");
+  if (N <= 0) return;
+  dim3 grid((C / 8 + 255) / 256, N);
+  hipLaunchKernelGGL(avgpool_kernel, grid, dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+                     (const f16*)x, (f16*)y, N, HW, C);
+  RDB_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace rdb

@@ -1,0 +1,524 @@
+// Replica engine: the native dynamic-batching loop of one GPU replica.
+//
+// Reference behaviour being re-designed:
+//   * serve/batching.py:146-197 _BatchQueue.wait_for_batch -- flush at
+//     max_batch_size or batch_wait_timeout_s after the FIRST item;
+//   * 293-project/src/scheduler.py:258-322 RequestQueue.get_batch -- per-model
+//     queues with stale-request dropping (arrival + SLO < now + lat(b));
+//   * scheduler.py:525-588 GPUWorker.execute_schedule -- one worker per GPU
+//     serving several model sessions;
+//   * scheduler.py:443-452 -- stack + .cuda() + synchronize around the forward.
+//
+// MI355X-native design:
+//   launcher thread : picks the session (model queue) with the earliest head
+//                     deadline (priority first), forms a batch by PEEKING the
+//                     shm ring, launches on the copy stream a gather kernel that
+//                     reads the payloads in place from hipHostRegister'ed shm
+//                     (zero-copy H2D, padded to the bucket), then on the compute
+//                     stream waits that event and replays the hipGraph captured
+//                     for (session, bucket, slot), then async D2H of the outputs
+//                     into pinned host memory.  `pipeline_depth` slots let the
+//                     gather of batch k+1 overlap the forward of batch k.
+//   completer thread: waits the batch events in FIFO order, writes the per-request
+//                     results into the clients' completion rings, releases the
+//                     request-ring slots and updates shm metrics.
+// No Python runs in steady state.
+#include <hip/hip_runtime.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <algorithm>
+#include <atomic>
+#include <condition_variable>
+#include <deque>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+#include "../../runtime/csrc/shm.h"
+
+namespace py = pybind11;
+using namespace rdb::rt;
+
+namespace rdb {
+void gather_rows(uintptr_t src_ptrs, int n, int rows, int row_bytes, uintptr_t dst, uintptr_t stream);
+
+namespace {
+
+#define ENG_CHECK(expr)                                                                     \
+  do {                                                                                      \
+    hipError_t _e = (expr);                                                                 \
+    if (_e != hipSuccess)                                                                   \
+      throw std::runtime_error(std::string("engine HIP error: ") + hipGetErrorString(_e) + \
+                               " at " #expr);                                               \
+  } while (0)
+
+struct Session {
+  uint32_t queue = 0;
+  int max_batch = 1;
+  int64_t max_wait_ns = 0;
+  std::vector<int> buckets;
+  int in_row_bytes = 0, out_row_bytes = 0;
+  int priority = 0;
+  int64_t slo_ns = 0;
+  bool drop_stale = false;
+  std::vector<double> est_ns;                        // per bucket service estimate
+  std::vector<std::vector<hipGraphExec_t>> graphs;   // [bucket][slot]
+  std::vector<std::vector<uintptr_t>> out_dev;       // [bucket][slot]
+  std::vector<uintptr_t> in_dev;                     // [slot]
+  Ring ring;
+  uint64_t peek_pos = 0;                             // next unread position
+  // duty-cycle mode (Nexus): share of the cycle, ms
+  double duty_share = 0.0;
+};
+
+struct InFlight {
+  int session = -1;
+  int slot = 0;
+  int bucket_idx = 0;
+  uint64_t pos_begin = 0, pos_end = 0;  // ring range covered (committed after completion)
+  std::vector<uint64_t> req_pos;        // ring positions of the requests in batch order
+  int64_t t_form_start = 0, t_launch = 0;
+  bool gpu = false;
+};
+
+class Engine {
+ public:
+  Engine(const std::string& job_name, uint32_t replica, int pipeline_depth, bool zero_copy,
+         int device, int policy)
+      : replica_(replica), depth_(std::max(1, pipeline_depth)), zero_copy_(zero_copy),
+        device_(device), policy_(policy) {
+    job_.attach(job_name, 30000000000LL);
+    job_.set_unlink_on_close(false);
+    if (replica_ >= job_.hdr()->n_replicas) throw std::out_of_range("replica index");
+    ENG_CHECK(hipSetDevice(device_));
+    ENG_CHECK(hipStreamCreateWithFlags(&copy_stream_, hipStreamNonBlocking));
+    ENG_CHECK(hipStreamCreateWithFlags(&compute_stream_, hipStreamNonBlocking));
+    if (zero_copy_) {
+      auto reg = job_.request_region();
+      host_base_ = reg.first;
+      ENG_CHECK(hipHostRegister(reg.first, reg.second, hipHostRegisterMapped));
+      void* dev = nullptr;
+      ENG_CHECK(hipHostGetDevicePointer(&dev, reg.first, 0));
+      dev_base_ = reinterpret_cast<char*>(dev);
+      registered_ = true;
+    }
+    slot_busy_.assign(depth_, false);
+    for (int s = 0; s < depth_; ++s) {
+      hipEvent_t a, b, c;
+      ENG_CHECK(hipEventCreateWithFlags(&a, hipEventDisableTiming));
+      ENG_CHECK(hipEventCreate(&b));
+      ENG_CHECK(hipEventCreate(&c));
+      ev_copy_.push_back(a);
+      ev_start_.push_back(b);
+      ev_done_.push_back(c);
+    }
+  }
+  ~Engine() {
+    stop();
+    for (auto e : ev_copy_) hipEventDestroy(e);
+    for (auto e : ev_start_) hipEventDestroy(e);
+    for (auto e : ev_done_) hipEventDestroy(e);
+    for (auto p : host_ptrs_) hipHostFree(p);
+    for (auto p : host_out_) hipHostFree(p);
+    if (registered_) hipHostUnregister(job_.request_region().first);
+    if (copy_stream_) hipStreamDestroy(copy_stream_);
+    if (compute_stream_) hipStreamDestroy(compute_stream_);
+  }
+
+  int add_session(uint32_t queue, int max_batch, double max_wait_s, std::vector<int> buckets,
+                  int in_row_bytes, int out_row_bytes, int priority, double slo_ms, bool drop_stale) {
+    if (running_) throw std::runtime_error("add_session after start");
+    if (queue >= job_.hdr()->n_queues) throw std::out_of_range("queue index");
+    if (buckets.empty()) buckets.push_back(max_batch);
+    std::sort(buckets.begin(), buckets.end());
+    if (buckets.back() != max_batch) throw std::invalid_argument("largest bucket must equal max_batch");
+    if (in_row_bytes % 16) throw std::invalid_argument("in_row_bytes must be a multiple of 16");
+    Ring ring = job_.req_ring(queue);
+    if ((uint32_t)in_row_bytes > ring.max_payload()) throw std::invalid_argument("request slot too small");
+    Session s;
+    s.queue = queue;
+    s.max_batch = max_batch;
+    s.max_wait_ns = (int64_t)(max_wait_s * 1e9);
+    s.buckets = buckets;
+    s.in_row_bytes = in_row_bytes;
+    s.out_row_bytes = out_row_bytes;
+    s.priority = priority;
+    s.slo_ns = (int64_t)(slo_ms * 1e6);
+    s.drop_stale = drop_stale;
+    s.est_ns.assign(buckets.size(), 0.0);
+    s.graphs.assign(buckets.size(), std::vector<hipGraphExec_t>(depth_, nullptr));
+    s.out_dev.assign(buckets.size(), std::vector<uintptr_t>(depth_, 0));
+    s.in_dev.assign(depth_, 0);
+    s.ring = ring;
+    s.peek_pos = ring.h->tail.load();
+    sessions_.push_back(std::move(s));
+    const int sid = (int)sessions_.size() - 1;
+    // per-slot pinned gather tables and output staging
+    for (int sl = 0; sl < depth_; ++sl) {
+      void* p = nullptr;
+      ENG_CHECK(hipHostMalloc(&p, sizeof(uint64_t) * max_batch, hipHostMallocDefault));
+      host_ptrs_.push_back(p);
+      void* o = nullptr;
+      ENG_CHECK(hipHostMalloc(&o, (size_t)out_row_bytes * max_batch + 64, hipHostMallocDefault));
+      host_out_.push_back(o);
+    }
+    return sid;
+  }
+  void set_input(int sid, int slot, uintptr_t dev_ptr) { sess(sid).in_dev.at(slot) = dev_ptr; }
+  void set_graph(int sid, int bucket_idx, int slot, uintptr_t graph_exec, uintptr_t out_dev) {
+    Session& s = sess(sid);
+    s.graphs.at(bucket_idx).at(slot) = reinterpret_cast<hipGraphExec_t>(graph_exec);
+    s.out_dev.at(bucket_idx).at(slot) = out_dev;
+  }
+  void set_latency_estimate(int sid, int bucket_idx, double ms) { sess(sid).est_ns.at(bucket_idx) = ms * 1e6; }
+  void set_duty_share(int sid, double ms) { sess(sid).duty_share = ms; }
+  void set_max_batch(int sid, int b) {
+    Session& s = sess(sid);
+    if (b < 1 || b > s.buckets.back()) throw std::invalid_argument("max_batch out of range");
+    s.max_batch = b;
+  }
+  void set_max_wait(int sid, double seconds) { sess(sid).max_wait_ns = (int64_t)(seconds * 1e9); }
+
+  void start() {
+    if (running_) return;
+    for (size_t i = 0; i < sessions_.size(); ++i)
+      for (size_t b = 0; b < sessions_[i].buckets.size(); ++b)
+        for (int sl = 0; sl < depth_; ++sl)
+          if (!sessions_[i].graphs[b][sl] || !sessions_[i].in_dev[sl])
+            throw std::runtime_error("engine: missing graph/input for a (session, bucket, slot)");
+    running_ = true;
+    ReplicaState* rs = job_.replica(replica_);
+    rs->gpu.store(device_);
+    rs->pid.store((uint32_t)getpid());
+    rs->heartbeat_ns.store(now_ns());
+    rs->status.store(RS_READY, std::memory_order_release);
+    completer_ = std::thread([this] { completer_loop(); });
+    launcher_ = std::thread([this] { launcher_loop(); });
+  }
+  void stop() {
+    if (!running_) return;
+    running_ = false;
+    for (auto& s : sessions_) s.ring.ring_bell();
+    cv_.notify_all();
+    if (launcher_.joinable()) launcher_.join();
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      stopping_completer_ = true;
+    }
+    cv_.notify_all();
+    if (completer_.joinable()) completer_.join();
+    job_.replica(replica_)->status.store(RS_DRAINING);
+  }
+  void heartbeat() { job_.replica(replica_)->heartbeat_ns.store(now_ns()); }
+  std::string error() {
+    std::lock_guard<std::mutex> lk(mu_);
+    return error_;
+  }
+  py::dict stats() {
+    py::dict d;
+    d["batches"] = batches_.load();
+    d["requests"] = requests_.load();
+    d["dropped"] = dropped_.load();
+    d["padded"] = padded_.load();
+    d["gpu_busy_ms"] = gpu_busy_ms_.load();
+    d["error"] = error();
+    return d;
+  }
+
+ private:
+  Session& sess(int sid) {
+    if (sid < 0 || sid >= (int)sessions_.size()) throw std::out_of_range("session id");
+    return sessions_[sid];
+  }
+  int bucket_for(const Session& s, int n) const {
+    for (size_t i = 0; i < s.buckets.size(); ++i)
+      if (s.buckets[i] >= n) return (int)i;
+    return (int)s.buckets.size() - 1;
+  }
+  int64_t head_deadline(Session& s) {
+    SlotHeader* h = s.ring.peek(s.peek_pos);
+    if (!h) return INT64_MAX;
+    if (h->deadline_ns) return h->deadline_ns;
+    return h->t_submit_ns + (s.slo_ns ? s.slo_ns : 1000000000LL);
+  }
+  // Session choice: highest priority with work; ties -> earliest head deadline (EDF).
+  int pick_session() {
+    int best = -1;
+    int best_pri = INT32_MIN;
+    int64_t best_dl = INT64_MAX;
+    for (size_t i = 0; i < sessions_.size(); ++i) {
+      const int64_t dl = head_deadline(sessions_[i]);
+      if (dl == INT64_MAX) continue;
+      const int pri = sessions_[i].priority;
+      if (pri > best_pri || (pri == best_pri && dl < best_dl)) {
+        best = (int)i;
+        best_pri = pri;
+        best_dl = dl;
+      }
+    }
+    return best;
+  }
+  void set_error(const std::string& e) {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (error_.empty()) error_ = e;
+  }
+  void write_completion(const SlotHeader* req, uint32_t queue, uint32_t status, const char* data,
+                        uint32_t len, int64_t t_done) {
+    Ring c = job_.cmp_ring(req->client);
+    uint64_t pos;
+    SlotHeader* s;
+    while ((s = c.reserve(&pos)) == nullptr) {
+      if (!running_ && job_.hdr()->shutdown.load()) return;
+      cpu_relax();
+    }
+    if (len > c.max_payload()) { status = ST_TOO_LARGE; len = 0; }
+    s->req_id = req->req_id;
+    s->t_submit_ns = req->t_submit_ns;
+    s->deadline_ns = req->deadline_ns;
+    s->len = len;
+    s->kind = 0;
+    s->client = req->client;
+    s->queue = queue;
+    s->status = status;
+    s->t_aux_ns = t_done;
+    if (len) memcpy(c.payload(s), data, len);
+    QueueState* qs = job_.queue(queue);
+    const int64_t e2e = t_done - req->t_submit_ns;
+    if (status == ST_OK) {
+      qs->hist_e2e.record((uint64_t)std::max<int64_t>(0, e2e));
+      const int64_t slo = qs->slo_ns.load(std::memory_order_relaxed);
+      if (slo > 0 && e2e > slo) qs->slo_violations.fetch_add(1, std::memory_order_relaxed);
+    } else if (status == ST_DROPPED_STALE) {
+      qs->dropped.fetch_add(1, std::memory_order_relaxed);
+    } else {
+      qs->errors.fetch_add(1, std::memory_order_relaxed);
+    }
+    qs->completed.fetch_add(1, std::memory_order_release);
+    c.publish(s, pos);
+  }
+
+  void launcher_loop() {
+    try {
+      ENG_CHECK(hipSetDevice(device_));
+      uint64_t counter = 0;
+      while (running_) {
+        const int slot = (int)(counter % depth_);
+        {  // wait for the slot to be free
+          std::unique_lock<std::mutex> lk(mu_);
+          cv_.wait(lk, [&] { return !slot_busy_[slot] || !running_; });
+          if (!running_) break;
+        }
+        // wait for any work
+        int sid = pick_session();
+        if (sid < 0) {
+          Session& s0 = sessions_[0];
+          for (int i = 0; i < 4000 && sid < 0; ++i) {  // short spin
+            cpu_relax();
+            if ((i & 63) == 63) sid = pick_session();
+          }
+          if (sid < 0) {
+            s0.ring.wait_for(s0.peek_pos, sessions_.size() == 1 ? 20000000LL : 200000LL, 0);
+            continue;
+          }
+        }
+        job_.replica(replica_)->heartbeat_ns.store(now_ns(), std::memory_order_relaxed);
+        Session& s = sessions_[sid];
+        InFlight f;
+        f.session = sid;
+        f.slot = slot;
+        f.pos_begin = s.peek_pos;
+        f.t_form_start = now_ns();
+        const int64_t flush_at = f.t_form_start + s.max_wait_ns;
+        uint64_t* tbl = reinterpret_cast<uint64_t*>(host_ptrs_[sid * depth_ + slot]);
+        int n = 0;
+        while (n < s.max_batch) {
+          SlotHeader* h = s.ring.peek(s.peek_pos);
+          if (!h) {
+            const int64_t left = flush_at - now_ns();
+            if (left <= 0 || !running_) break;
+            if (!s.ring.wait_for(s.peek_pos, left, 4000)) break;
+            continue;
+          }
+          // stale-request drop (fork semantics: arrival + SLO < now + lat(batch))
+          int64_t dl = h->deadline_ns;
+          if (!dl && s.drop_stale && s.slo_ns) dl = h->t_submit_ns + s.slo_ns;
+          if (dl) {
+            const double est = s.est_ns[bucket_for(s, std::min(s.max_batch, n + 1))];
+            if ((double)now_ns() + est > (double)dl) {
+              write_completion(h, s.queue, ST_DROPPED_STALE, nullptr, 0, now_ns());
+              dropped_.fetch_add(1, std::memory_order_relaxed);
+              ++s.peek_pos;
+              continue;
+            }
+          }
+          if (h->len != (uint32_t)s.in_row_bytes) {
+            write_completion(h, s.queue, ST_ERROR, nullptr, 0, now_ns());
+            ++s.peek_pos;
+            continue;
+          }
+          f.req_pos.push_back(s.peek_pos);
+          char* payload = reinterpret_cast<char*>(h) + sizeof(SlotHeader);
+          tbl[n++] = zero_copy_ ? reinterpret_cast<uint64_t>(dev_base_ + (payload - host_base_))
+                                : reinterpret_cast<uint64_t>(payload);
+          ++s.peek_pos;
+        }
+        f.pos_end = s.peek_pos;
+        if (n > 0) {
+          const int bi = bucket_for(s, n);
+          const int rows = s.buckets[bi];
+          f.bucket_idx = bi;
+          f.gpu = true;
+          const uintptr_t in = s.in_dev[slot];
+          if (zero_copy_) {
+            gather_rows(reinterpret_cast<uintptr_t>(tbl), n, rows, s.in_row_bytes, in,
+                        reinterpret_cast<uintptr_t>(copy_stream_));
+          } else {
+            for (int i = 0; i < n; ++i)
+              ENG_CHECK(hipMemcpyAsync(reinterpret_cast<char*>(in) + (size_t)i * s.in_row_bytes,
+                                       reinterpret_cast<void*>(tbl[i]), s.in_row_bytes,
+                                       hipMemcpyHostToDevice, copy_stream_));
+            if (rows > n)
+              ENG_CHECK(hipMemsetAsync(reinterpret_cast<char*>(in) + (size_t)n * s.in_row_bytes, 0,
+                                       (size_t)(rows - n) * s.in_row_bytes, copy_stream_));
+          }
+          ENG_CHECK(hipEventRecord(ev_copy_[slot], copy_stream_));
+          ENG_CHECK(hipStreamWaitEvent(compute_stream_, ev_copy_[slot], 0));
+          ENG_CHECK(hipEventRecord(ev_start_[slot], compute_stream_));
+          ENG_CHECK(hipGraphLaunch(s.graphs[bi][slot], compute_stream_));
+          ENG_CHECK(hipMemcpyAsync(host_out_[sid * depth_ + slot],
+                                   reinterpret_cast<void*>(s.out_dev[bi][slot]),
+                                   (size_t)n * s.out_row_bytes, hipMemcpyDeviceToHost, compute_stream_));
+          ENG_CHECK(hipEventRecord(ev_done_[slot], compute_stream_));
+          padded_.fetch_add(rows - n, std::memory_order_relaxed);
+        }
+        f.t_launch = now_ns();
+        {
+          std::lock_guard<std::mutex> lk(mu_);
+          slot_busy_[slot] = true;
+          inflight_.push_back(std::move(f));
+        }
+        cv_.notify_all();
+        ++counter;
+      }
+    } catch (const std::exception& e) {
+      set_error(std::string("launcher: ") + e.what());
+      job_.replica(replica_)->status.store(RS_DEAD);
+      running_ = false;
+      cv_.notify_all();
+    }
+  }
+
+  void completer_loop() {
+    try {
+      ENG_CHECK(hipSetDevice(device_));
+      ReplicaState* rs = job_.replica(replica_);
+      for (;;) {
+        InFlight f;
+        {
+          std::unique_lock<std::mutex> lk(mu_);
+          cv_.wait(lk, [&] { return !inflight_.empty() || stopping_completer_; });
+          if (inflight_.empty()) break;
+          f = std::move(inflight_.front());
+          inflight_.pop_front();
+        }
+        Session& s = sessions_[f.session];
+        const int n = (int)f.req_pos.size();
+        if (f.gpu) {
+          // low-latency wait: spin on the event, yielding
+          for (;;) {
+            hipError_t q = hipEventQuery(ev_done_[f.slot]);
+            if (q == hipSuccess) break;
+            if (q != hipErrorNotReady) ENG_CHECK(q);
+            std::this_thread::yield();
+          }
+          float ms = 0.f;
+          if (hipEventElapsedTime(&ms, ev_start_[f.slot], ev_done_[f.slot]) == hipSuccess) {
+            gpu_busy_ms_.store(gpu_busy_ms_.load() + ms);
+            rs->busy_ns.fetch_add((uint64_t)(ms * 1e6), std::memory_order_relaxed);
+            // EMA of the service time of this bucket (drives stale dropping)
+            double& est = s.est_ns[f.bucket_idx];
+            est = est == 0.0 ? ms * 1e6 : 0.9 * est + 0.1 * ms * 1e6;
+          }
+          const char* out = reinterpret_cast<const char*>(host_out_[f.session * depth_ + f.slot]);
+          const int64_t t_done = now_ns();
+          QueueState* qs = job_.queue(s.queue);
+          for (int i = 0; i < n; ++i) {
+            SlotHeader* h = s.ring.slot(f.req_pos[i]);
+            qs->hist_queue_wait.record((uint64_t)std::max<int64_t>(0, f.t_launch - h->t_submit_ns));
+            write_completion(h, s.queue, ST_OK, out + (size_t)i * s.out_row_bytes, s.out_row_bytes, t_done);
+          }
+          rs->batches.fetch_add(1, std::memory_order_relaxed);
+          rs->batch_items.fetch_add(n, std::memory_order_relaxed);
+          rs->padded_items.fetch_add(s.buckets[f.bucket_idx] - n, std::memory_order_relaxed);
+          rs->graph_replays.fetch_add(1, std::memory_order_relaxed);
+          rs->hist_batch_size.record((uint64_t)n);
+          rs->hist_service.record((uint64_t)(t_done - f.t_form_start));
+          batches_.fetch_add(1, std::memory_order_relaxed);
+          requests_.fetch_add(n, std::memory_order_relaxed);
+        }
+        s.ring.commit(f.pos_end);
+        {
+          std::lock_guard<std::mutex> lk(mu_);
+          slot_busy_[f.slot] = false;
+        }
+        cv_.notify_all();
+      }
+    } catch (const std::exception& e) {
+      set_error(std::string("completer: ") + e.what());
+      job_.replica(replica_)->status.store(RS_DEAD);
+      running_ = false;
+      cv_.notify_all();
+    }
+  }
+
+  Job job_;
+  uint32_t replica_;
+  int depth_;
+  bool zero_copy_;
+  int device_;
+  int policy_;
+  bool registered_ = false;
+  char* host_base_ = nullptr;
+  char* dev_base_ = nullptr;
+  hipStream_t copy_stream_ = nullptr, compute_stream_ = nullptr;
+  std::vector<hipEvent_t> ev_copy_, ev_start_, ev_done_;
+  std::vector<void*> host_ptrs_, host_out_;
+  std::vector<Session> sessions_;
+  std::vector<bool> slot_busy_;
+  std::deque<InFlight> inflight_;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::thread launcher_, completer_;
+  std::atomic<bool> running_{false};
+  bool stopping_completer_ = false;
+  std::string error_;
+  std::atomic<uint64_t> batches_{0}, requests_{0}, dropped_{0}, padded_{0};
+  std::atomic<double> gpu_busy_ms_{0.0};
+};
+
+}  // namespace
+
+void register_engine(py::module_& m) {
+  py::class_<Engine>(m, "Engine")
+      .def(py::init<const std::string&, uint32_t, int, bool, int, int>(), py::arg("job_name"),
+           py::arg("replica"), py::arg("pipeline_depth") = 2, py::arg("zero_copy") = true,
+           py::arg("device") = 0, py::arg("policy") = 0)
+      .def("add_session", &Engine::add_session, py::arg("queue"), py::arg("max_batch"),
+           py::arg("max_wait_s"), py::arg("buckets"), py::arg("in_row_bytes"),
+           py::arg("out_row_bytes"), py::arg("priority") = 0, py::arg("slo_ms") = 0.0,
+           py::arg("drop_stale") = false)
+      .def("set_input", &Engine::set_input)
+      .def("set_graph", &Engine::set_graph)
+      .def("set_latency_estimate", &Engine::set_latency_estimate)
+      .def("set_duty_share", &Engine::set_duty_share)
+      .def("set_max_batch", &Engine::set_max_batch)
+      .def("set_max_wait", &Engine::set_max_wait)
+      .def("start", &Engine::start, py::call_guard<py::gil_scoped_release>())
+      .def("stop", &Engine::stop, py::call_guard<py::gil_scoped_release>())
+      .def("heartbeat", &Engine::heartbeat)
+      .def("error", &Engine::error)
+      .def("stats", &Engine::stats);
+}
+
+}  // namespace rdb

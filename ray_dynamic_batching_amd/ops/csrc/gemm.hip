@@ -1,0 +1,51 @@
+// Dense MFMA GEMM with fused epilogue (gfx950).  Kernel body: gemm_core.h.
+//
+//   C[m, n] = act(alpha * sum_k A[m, k] * W[n, k] + bias[n] + R[m, n])
+//
+// A is [M, K] (row stride lda), W is [N, K] (nn.Linear layout, row stride ldw).
+// The op behind every projection of the batched forward pass (SURVEY.md §2.7:
+// BERT QKV / out / FFN GEMMs with bias/GELU/residual epilogues, pooler tanh,
+// ResNet FC, Llama SwiGLU gate/up pair).
+#include "gemm_core.h"
+#include <stdexcept>
+
+namespace rdb {
+
+// dtype codes shared with the Python side: 0 = bf16, 1 = f16, 2 = f32
+void gemm_tn(int in_dtype, int out_dtype, uintptr_t A, int lda, uintptr_t W, int ldw, uintptr_t C,
+             int ldc, uintptr_t bias, uintptr_t R, int ldr, int M, int N, int K, float alpha,
+             int act, uintptr_t stream, int force_cfg) {
+  if (K % 8 != 0) throw std::invalid_argument("gemm_tn: K must be a multiple of 8");
+  if (lda % 8 != 0 || ldw % 8 != 0) throw std::invalid_argument("gemm_tn: lda/ldw must be multiples of 8");
+  if ((A | W) & 15) throw std::invalid_argument("gemm_tn: A/W must be 16-byte aligned");
+  if (act == ACT_SWIGLU && N % 4 != 0) throw std::invalid_argument("gemm_tn: SWIGLU needs N % 4 == 0");
+  if (M <= 0 || N <= 0 || K <= 0) return;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  DenseParams p{reinterpret_cast<const void*>(A), lda, M, K};
+  if (in_dtype == 0) {
+    auto w = reinterpret_cast<const bf16*>(W);
+    auto b = reinterpret_cast<const bf16*>(bias);
+    auto r = reinterpret_cast<const bf16*>(R);
+    if (out_dtype == 0)
+      launch_mfma_gemm<bf16, bf16, DenseLoader>(p, w, ldw, reinterpret_cast<bf16*>(C), ldc, b, r, ldr, M, N, K, alpha, act, s, force_cfg);
+    else if (out_dtype == 2)
+      launch_mfma_gemm<bf16, float, DenseLoader>(p, w, ldw, reinterpret_cast<float*>(C), ldc, b, r, ldr, M, N, K, alpha, act, s, force_cfg);
+    else
+      throw std::invalid_argument("gemm_tn: bf16 input supports bf16/f32 output");
+  } else if (in_dtype == 1) {
+    auto w = reinterpret_cast<const f16*>(W);
+    auto b = reinterpret_cast<const f16*>(bias);
+    auto r = reinterpret_cast<const f16*>(R);
+    if (out_dtype == 1)
+      launch_mfma_gemm<f16, f16, DenseLoader>(p, w, ldw, reinterpret_cast<f16*>(C), ldc, b, r, ldr, M, N, K, alpha, act, s, force_cfg);
+    else if (out_dtype == 2)
+      launch_mfma_gemm<f16, float, DenseLoader>(p, w, ldw, reinterpret_cast<float*>(C), ldc, b, r, ldr, M, N, K, alpha, act, s, force_cfg);
+    else
+      throw std::invalid_argument("gemm_tn: f16 input supports f16/f32 output");
+  } else {
+    throw std::invalid_argument("gemm_tn: unsupported input dtype");
+  }
+  RDB_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace rdb

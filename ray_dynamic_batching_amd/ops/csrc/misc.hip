@@ -1,0 +1,160 @@
+// Small fused kernels for the serving path on gfx950:
+//   * softmax_topk   - classification head: row softmax fused with top-k
+//                      (ResNet-50 Serve workload: softmax + argmax)
+//   * rope           - in-place rotary embedding on the packed QKV buffer (Llama)
+//   * gather_rows    - batch formation on the device: copies request payloads
+//                      straight out of host-mapped (pinned shm) ring slots into
+//                      the padded device input, zero-filling pad rows.  This is
+//                      the H2D step of the replica engine, run on a side stream.
+//   * image_to_nhwc  - uint8 HWC images -> normalised f16 NHWC model input.
+#include "common.h"
+#include <stdexcept>
+
+namespace rdb {
+
+// One wave per row, C <= 64 * 64 = 4096, k <= 16.
+__global__ void __launch_bounds__(256)
+softmax_topk_kernel(const float* __restrict__ x, int rows, int C, int k,
+                    float* __restrict__ probs, int* __restrict__ idx) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const float* xr = x + (size_t)row * C;
+  float v[64];
+  float mx = -INFINITY;
+#pragma unroll
+  for (int i = 0; i < 64; ++i) {
+    const int c = lane + 64 * i;
+    v[i] = (c < C) ? xr[c] : -INFINITY;
+    mx = fmaxf(mx, v[i]);
+  }
+  mx = wave_max(mx);
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < 64; ++i) s += (lane + 64 * i < C) ? __expf(v[i] - mx) : 0.f;
+  s = wave_sum(s);
+  const float inv = 1.f / s;
+  for (int t = 0; t < k; ++t) {
+    float best = -INFINITY;
+    int bi = 0x7fffffff;
+#pragma unroll
+    for (int i = 0; i < 64; ++i) {
+      const int c = lane + 64 * i;
+      if (v[i] > best || (v[i] == best && c < bi)) { best = v[i]; bi = c; }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float ob = __shfl_xor(best, o, 64);
+      const int oi = __shfl_xor(bi, o, 64);
+      if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
+    }
+    if (lane == 0) {
+      probs[(size_t)row * k + t] = __expf(best - mx) * inv;
+      idx[(size_t)row * k + t] = bi < C ? bi : -1;
+    }
+    // remove the winner
+#pragma unroll
+    for (int i = 0; i < 64; ++i)
+      if (lane + 64 * i == bi) v[i] = -INFINITY;
+  }
+}
+
+void softmax_topk(uintptr_t x, int rows, int C, int k, uintptr_t probs, uintptr_t idx, uintptr_t stream) {
+  if (C > 4096 || k < 1 || k > 16 || k > C) throw std::invalid_argument("softmax_topk: need C <= 4096, 1 <= k <= min(16, C)");
+  if (rows <= 0) return;
+  hipLaunchKernelGGL(softmax_topk_kernel, dim3((rows + 3) / 4), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), (const float*)x, rows, C, k,
+                     (float*)probs, (int*)idx);
+  RDB_HIP_CHECK(hipGetLastError());
+}
+
+// Rotary embedding (HF "rotate_half" convention) on Q and K heads of the packed
+// [T, ld] projection output.  cos/sin tables are [max_pos, D/2] f32 built on the
+// host (Appendix B: precomputed trig tables).  One thread per (token, head, i<D/2).
+__global__ void rope_kernel(bf16* __restrict__ qkv, int ld, int q_off, int k_off, int H, int Hkv,
+                            int D, int S, const float* __restrict__ cos_t,
+                            const float* __restrict__ sin_t, int T, int pos_offset) {
+  const int half = D >> 1;
+  const long total = (long)T * (H + Hkv) * half;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+    const int i = e % half;
+    const long r = e / half;
+    const int hh = r % (H + Hkv);
+    const int t = r / (H + Hkv);
+    const int pos = t % S + pos_offset;
+    bf16* base = qkv + (size_t)t * ld + (hh < H ? q_off + hh * D : k_off + (hh - H) * D);
+    const float c = cos_t[pos * half + i], s = sin_t[pos * half + i];
+    const float x1 = (float)base[i], x2 = (float)base[i + half];
+    base[i] = (bf16)(x1 * c - x2 * s);
+    base[i + half] = (bf16)(x2 * c + x1 * s);
+  }
+}
+
+void rope(uintptr_t qkv, int ld, int q_off, int k_off, int H, int Hkv, int D, int S, uintptr_t cos_t,
+          uintptr_t sin_t, int T, int pos_offset, uintptr_t stream) {
+  if (T <= 0) return;
+  const long total = (long)T * (H + Hkv) * (D / 2);
+  int blocks = (int)((total + 255) / 256);
+  blocks = blocks > 4096 ? 4096 : blocks;
+  hipLaunchKernelGGL(rope_kernel, dim3(blocks), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+                     (bf16*)qkv, ld, q_off, k_off, H, Hkv, D, S, (const float*)cos_t,
+                     (const float*)sin_t, T, pos_offset);
+  RDB_HIP_CHECK(hipGetLastError());
+}
+
+// dst[r, :] = src_ptrs[r][0:row_bytes) for r < n, zeros for n <= r < rows.
+// src_ptrs lives in pinned host memory and the payloads in hipHostRegister'ed
+// (device-mapped) shared memory, so this one kernel replaces n hipMemcpyAsync's.
+__global__ void __launch_bounds__(256)
+gather_rows_kernel(const uint64_t* __restrict__ src_ptrs, int n, int rows, int row_bytes,
+                   char* __restrict__ dst) {
+  const int r = blockIdx.x;
+  char* d = dst + (size_t)r * row_bytes;
+  const int nvec = row_bytes >> 4;
+  if (r < n) {
+    const char* s = reinterpret_cast<const char*>(src_ptrs[r]);
+    for (int i = threadIdx.x; i < nvec; i += blockDim.x)
+      reinterpret_cast<u32x4*>(d)[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(s) + i);
+    for (int i = (nvec << 4) + threadIdx.x; i < row_bytes; i += blockDim.x) d[i] = s[i];
+  } else {
+    for (int i = threadIdx.x; i < nvec; i += blockDim.x) reinterpret_cast<u32x4*>(d)[i] = u32x4{0, 0, 0, 0};
+    for (int i = (nvec << 4) + threadIdx.x; i < row_bytes; i += blockDim.x) d[i] = 0;
+  }
+}
+
+void gather_rows(uintptr_t src_ptrs, int n, int rows, int row_bytes, uintptr_t dst, uintptr_t stream) {
+  if (rows <= 0) return;
+  if (row_bytes % 16 != 0) throw std::invalid_argument("gather_rows: row_bytes must be a multiple of 16");
+  hipLaunchKernelGGL(gather_rows_kernel, dim3(rows), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+                     (const uint64_t*)src_ptrs, n, rows, row_bytes, (char*)dst);
+  RDB_HIP_CHECK(hipGetLastError());
+}
+
+// uint8 HWC (RGB) -> f16 NHWC normalised with per-channel mean/std, C padded to Cp
+// (Cp = 4 keeps the first conv's channel dim 8-byte aligned; pad channels are 0).
+__global__ void image_to_nhwc_kernel(const uint8_t* __restrict__ src, int N, int HW, int Cp,
+                                     float m0, float m1, float m2, float s0, float s1, float s2,
+                                     f16* __restrict__ dst) {
+  const long total = (long)N * HW;
+  for (long p = blockIdx.x * (long)blockDim.x + threadIdx.x; p < total; p += (long)gridDim.x * blockDim.x) {
+    const uint8_t* s = src + p * 3;
+    f16* d = dst + p * Cp;
+    d[0] = (f16)((s[0] * (1.f / 255.f) - m0) / s0);
+    d[1] = (f16)((s[1] * (1.f / 255.f) - m1) / s1);
+    d[2] = (f16)((s[2] * (1.f / 255.f) - m2) / s2);
+    for (int c = 3; c < Cp; ++c) d[c] = (f16)0.f;
+  }
+}
+
+void image_to_nhwc(uintptr_t src, int N, int HW, int Cp, uintptr_t dst, uintptr_t stream) {
+  if (N <= 0) return;
+  const long total = (long)N * HW;
+  int blocks = (int)((total + 255) / 256);
+  blocks = blocks > 8192 ? 8192 : blocks;
+  hipLaunchKernelGGL(image_to_nhwc_kernel, dim3(blocks), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+                     (const uint8_t*)src, N, HW, Cp, 0.485f, 0.456f, 0.406f, 0.229f, 0.224f, 0.225f,
+                     (f16*)dst);
+  RDB_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace rdb

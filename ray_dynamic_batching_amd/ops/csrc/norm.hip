@@ -1,0 +1,219 @@
+// Row normalisation kernels for gfx950: LayerNorm (+ fused residual add),
+// RMSNorm (+ fused residual add) and the BERT embedding gather fused with its
+// LayerNorm.  Memory-bound ops: one wave per row, 8-byte (4 x 16-bit) vector
+// loads per lane (cdna_hip_programming.md Guideline 13), the row is kept in
+// registers between the statistics pass and the output pass, so each element
+// is read from HBM exactly once.
+#include "common.h"
+#include <stdexcept>
+
+namespace rdb {
+
+constexpr int kMaxVec = 32;  // 32 x 4 elements x 64 lanes = rows up to 8192
+// NV = D / 256 is a template parameter so the row lives in exactly NV*4 VGPRs.
+
+template <typename T>
+__device__ __forceinline__ void load4(const T* p, float* o) {
+  typedef T v4 __attribute__((ext_vector_type(4)));
+  v4 v = *reinterpret_cast<const v4*>(p);
+  o[0] = (float)v[0]; o[1] = (float)v[1]; o[2] = (float)v[2]; o[3] = (float)v[3];
+}
+template <typename T>
+__device__ __forceinline__ void st4(T* p, const float* o) {
+  typedef T v4 __attribute__((ext_vector_type(4)));
+  v4 v = {(T)o[0], (T)o[1], (T)o[2], (T)o[3]};
+  *reinterpret_cast<v4*>(p) = v;
+}
+
+// MODE 0 = LayerNorm, 1 = RMSNorm.
+template <typename T, int MODE, int NV>
+__global__ void __launch_bounds__(256)
+norm_kernel(const T* __restrict__ x, const T* __restrict__ res, T* __restrict__ res_out,
+            const T* __restrict__ gamma, const T* __restrict__ beta, T* __restrict__ y,
+            int rows, int D, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const T* xr = x + (size_t)row * D;
+  float v[NV][4];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    {
+      const int c = i * 256 + lane * 4;
+      load4(xr + c, v[i]);
+      if (res != nullptr) {
+        float r[4];
+        load4(res + (size_t)row * D + c, r);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[i][e] += r[e];
+        if (res_out != nullptr) st4(res_out + (size_t)row * D + c, v[i]);
+      }
+      if (MODE == 0) s += v[i][0] + v[i][1] + v[i][2] + v[i][3];
+      else s += v[i][0] * v[i][0] + v[i][1] * v[i][1] + v[i][2] * v[i][2] + v[i][3] * v[i][3];
+    }
+  }
+  s = wave_sum(s);
+  float mean = 0.f, rstd;
+  if (MODE == 0) {
+    mean = s / D;
+    float q = 0.f;
+#pragma unroll
+    for (int i = 0; i < NV; ++i)
+  #pragma unroll
+        for (int e = 0; e < 4; ++e) { const float d = v[i][e] - mean; q += d * d; }
+    q = wave_sum(q);
+    rstd = rsqrtf(q / D + eps);
+  } else {
+    rstd = rsqrtf(s / D + eps);
+  }
+  T* yr = y + (size_t)row * D;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    {
+      const int c = i * 256 + lane * 4;
+      float g[4], o[4];
+      load4(gamma + c, g);
+      if (MODE == 0) {
+        float b[4];
+        load4(beta + c, b);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] = (v[i][e] - mean) * rstd * g[e] + b[e];
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] = v[i][e] * rstd * g[e];
+      }
+      st4(yr + c, o);
+    }
+  }
+}
+
+// BERT embeddings: y[t] = LN(word[ids[t]] + pos[t % S] + type[types ? types[t] : 0])
+template <typename T, int NV>
+__global__ void __launch_bounds__(256)
+embed_ln_kernel(const int* __restrict__ ids, const int* __restrict__ types,
+                const T* __restrict__ word, const T* __restrict__ pos, const T* __restrict__ typ,
+                const T* __restrict__ gamma, const T* __restrict__ beta, T* __restrict__ y,
+                int tokens, int S, int D, int vocab, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (t >= tokens) return;
+  int id = ids[t];
+  id = id < 0 ? 0 : (id >= vocab ? vocab - 1 : id);
+  const int tt = types ? types[t] : 0;
+  const int p = t % S;
+  float v[NV][4];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    {
+      const int c = i * 256 + lane * 4;
+      float a[4], b[4], d[4];
+      load4(word + (size_t)id * D + c, a);
+      load4(pos + (size_t)p * D + c, b);
+      load4(typ + (size_t)tt * D + c, d);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { v[i][e] = a[e] + b[e] + d[e]; s += v[i][e]; }
+    }
+  }
+  const float mean = wave_sum(s) / D;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { const float d = v[i][e] - mean; q += d * d; }
+  const float rstd = rsqrtf(wave_sum(q) / D + eps);
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    {
+      const int c = i * 256 + lane * 4;
+      float g[4], b[4], o[4];
+      load4(gamma + c, g);
+      load4(beta + c, b);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = (v[i][e] - mean) * rstd * g[e] + b[e];
+      st4(y + (size_t)t * D + c, o);
+    }
+  }
+}
+
+// NV values instantiated: rows of 256 * NV elements.
+#define RDB_NV_LIST(X) X(1) X(2) X(3) X(4) X(5) X(6) X(8) X(10) X(12) X(14) X(16) X(20) X(24) X(28) X(32)
+
+static void check_d(int D) {
+  const int nv = D / 256;
+  bool ok = (D % 256 == 0);
+  bool listed = false;
+#define RDB_CHK(N) listed |= (nv == N);
+  RDB_NV_LIST(RDB_CHK)
+#undef RDB_CHK
+  if (!ok || !listed)
+    throw std::invalid_argument("norm: row length must be 256*NV with NV in {1..6,8,10,12,14,16,20,24,28,32}");
+}
+
+template <typename T, int MODE>
+static void launch_norm(dim3 grid, hipStream_t s, uintptr_t x, uintptr_t res, uintptr_t res_out,
+                        uintptr_t gamma, uintptr_t beta, uintptr_t y, int rows, int D, float eps) {
+  const int nv = D / 256;
+#define RDB_CASE(N)                                                                             \
+  if (nv == N) {                                                                                \
+    hipLaunchKernelGGL((norm_kernel<T, MODE, N>), grid, dim3(256), 0, s, (const T*)x,          \
+                       (const T*)res, (T*)res_out, (const T*)gamma, (const T*)beta, (T*)y, rows, \
+                       D, eps);                                                                 \
+    return;                                                                                     \
+  }
+  RDB_NV_LIST(RDB_CASE)
+#undef RDB_CASE
+}
+
+template <typename T>
+static void launch_embed(dim3 grid, hipStream_t s, uintptr_t ids, uintptr_t types, uintptr_t word,
+                         uintptr_t pos, uintptr_t typ, uintptr_t gamma, uintptr_t beta, uintptr_t y,
+                         int tokens, int S, int D, int vocab, float eps) {
+  const int nv = D / 256;
+#define RDB_CASE(N)                                                                              \
+  if (nv == N) {                                                                                 \
+    hipLaunchKernelGGL((embed_ln_kernel<T, N>), grid, dim3(256), 0, s, (const int*)ids,         \
+                       (const int*)types, (const T*)word, (const T*)pos, (const T*)typ,          \
+                       (const T*)gamma, (const T*)beta, (T*)y, tokens, S, D, vocab, eps);        \
+    return;                                                                                      \
+  }
+  RDB_NV_LIST(RDB_CASE)
+#undef RDB_CASE
+}
+
+void norm_fwd(int dtype, int mode, uintptr_t x, uintptr_t res, uintptr_t res_out, uintptr_t gamma,
+              uintptr_t beta, uintptr_t y, int rows, int D, float eps, uintptr_t stream) {
+  check_d(D);
+  if (rows <= 0) return;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  dim3 grid((rows + 3) / 4);
+  if (dtype == 0) {
+    if (mode == 0) launch_norm<bf16, 0>(grid, s, x, res, res_out, gamma, beta, y, rows, D, eps);
+    else launch_norm<bf16, 1>(grid, s, x, res, res_out, gamma, beta, y, rows, D, eps);
+  } else if (dtype == 1) {
+    if (mode == 0) launch_norm<f16, 0>(grid, s, x, res, res_out, gamma, beta, y, rows, D, eps);
+    else launch_norm<f16, 1>(grid, s, x, res, res_out, gamma, beta, y, rows, D, eps);
+  } else {
+    throw std::invalid_argument("norm: dtype must be bf16 or f16");
+  }
+  RDB_HIP_CHECK(hipGetLastError());
+}
+
+void embed_ln_fwd(int dtype, uintptr_t ids, uintptr_t types, uintptr_t word, uintptr_t pos,
+                  uintptr_t typ, uintptr_t gamma, uintptr_t beta, uintptr_t y, int tokens, int S,
+                  int D, int vocab, float eps, uintptr_t stream) {
+  check_d(D);
+  if (tokens <= 0) return;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  dim3 grid((tokens + 3) / 4);
+  if (dtype == 0)
+    launch_embed<bf16>(grid, s, ids, types, word, pos, typ, gamma, beta, y, tokens, S, D, vocab, eps);
+  else if (dtype == 1)
+    launch_embed<f16>(grid, s, ids, types, word, pos, typ, gamma, beta, y, tokens, S, D, vocab, eps);
+  else
+    throw std::invalid_argument("embed_ln: dtype must be bf16 or f16");
+  RDB_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace rdb

@@ -1,0 +1,200 @@
+"""Numerics of every HIP kernel against a plain-PyTorch fp32 reference (GPU)."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _ops():
+    from ray_dynamic_batching_amd import ops
+
+    return ops
+
+
+def _close(a, b, atol, rtol):
+    a, b = a.float(), b.float()
+    err = (a - b).abs()
+    tol = atol + rtol * b.abs()
+    bad = (err > tol).sum().item()
+    assert bad == 0, f"{bad} / {a.numel()} elements out of tolerance; max err {err.max().item():.4g}"
+
+
+@pytest.mark.parametrize("M,N,K", [(4096, 768, 768), (4096, 2304, 768), (512, 3072, 768), (256, 768, 3072),
+                                   (128, 768, 768), (7, 1000, 2048), (33, 40, 72), (1, 2, 768)])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_linear_plain(M, N, K, dtype):
+    ops = _ops()
+    torch.manual_seed(0)
+    x = torch.randn(M, K, device="cuda", dtype=dtype)
+    w = torch.randn(N, K, device="cuda", dtype=dtype) * (K ** -0.5)
+    y = ops.linear(x, w)
+    _close(y, ops.linear_ref(x, w), 2e-2, 2e-2)
+
+
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3])
+def test_linear_tile_configs_asymmetric(cfg):
+    """A = I with an asymmetric W catches a transposed C-write (guide §3)."""
+    ops = _ops()
+    M = K = 256
+    N = 192
+    x = torch.eye(M, K, device="cuda", dtype=torch.bfloat16)
+    w = (torch.arange(N * K, device="cuda").reshape(N, K) % 97).to(torch.bfloat16)
+    y = ops.linear(x, w, tile_cfg=cfg)
+    _close(y, w.t().contiguous(), 0, 0)
+
+
+@pytest.mark.parametrize("act", ["gelu", "relu", "tanh", "silu", "gelu_tanh"])
+def test_linear_epilogues(act):
+    ops = _ops()
+    torch.manual_seed(1)
+    x = torch.randn(512, 768, device="cuda", dtype=torch.bfloat16)
+    w = torch.randn(1024, 768, device="cuda", dtype=torch.bfloat16) * 0.03
+    b = torch.randn(1024, device="cuda", dtype=torch.bfloat16)
+    r = torch.randn(512, 1024, device="cuda", dtype=torch.bfloat16)
+    _close(ops.linear(x, w, b, act=act), ops.linear_ref(x, w, b, act=act), 3e-2, 2e-2)
+    _close(ops.linear(x, w, b, residual=r), ops.linear_ref(x, w, b, residual=r), 3e-2, 2e-2)
+
+
+def test_linear_swiglu_and_f32_out():
+    ops = _ops()
+    torch.manual_seed(2)
+    x = torch.randn(256, 512, device="cuda", dtype=torch.bfloat16)
+    w = torch.randn(1024, 512, device="cuda", dtype=torch.bfloat16) * 0.05
+    _close(ops.linear(x, w, act="swiglu"), ops.linear_ref(x, w, act="swiglu"), 3e-2, 3e-2)
+    y = ops.linear(x, w, out_dtype=torch.float32)
+    assert y.dtype == torch.float32
+    _close(y, ops.linear_ref(x, w, out_dtype=torch.float32), 1e-2, 1e-2)
+
+
+def test_linear_strided_rows():
+    """Pooler path: CLS rows of [B, S, D] as a row-strided view."""
+    ops = _ops()
+    h = torch.randn(8, 128, 768, device="cuda", dtype=torch.bfloat16)
+    w = torch.randn(768, 768, device="cuda", dtype=torch.bfloat16) * 0.03
+    cls = h[:, 0, :]
+    _close(ops.linear(cls, w, act="tanh"), ops.linear_ref(cls.contiguous(), w, act="tanh"), 2e-2, 2e-2)
+
+
+@pytest.mark.parametrize("D", [768, 1024, 4096])
+def test_norms(D):
+    ops = _ops()
+    torch.manual_seed(3)
+    x = torch.randn(300, D, device="cuda", dtype=torch.bfloat16)
+    r = torch.randn(300, D, device="cuda", dtype=torch.bfloat16)
+    g = torch.rand(D, device="cuda", dtype=torch.bfloat16) + 0.5
+    b = torch.randn(D, device="cuda", dtype=torch.bfloat16)
+    _close(ops.layer_norm(x, g, b), ops.layer_norm_ref(x, g, b), 3e-2, 2e-2)
+    ro = torch.empty_like(x)
+    _close(ops.layer_norm(x, g, b, residual=r, residual_out=ro), ops.layer_norm_ref(x, g, b, residual=r), 3e-2, 2e-2)
+    _close(ro, x.float() + r.float(), 2e-2, 1e-2)
+    _close(ops.rms_norm(x, g, 1e-5), ops.rms_norm_ref(x, g, 1e-5), 3e-2, 2e-2)
+
+
+def test_embed_ln():
+    ops = _ops()
+    torch.manual_seed(4)
+    V, D, S = 30522, 768, 128
+    word = torch.randn(V, D, device="cuda", dtype=torch.bfloat16)
+    pos = torch.randn(512, D, device="cuda", dtype=torch.bfloat16)
+    typ = torch.randn(2, D, device="cuda", dtype=torch.bfloat16)
+    g = torch.rand(D, device="cuda", dtype=torch.bfloat16) + 0.5
+    b = torch.randn(D, device="cuda", dtype=torch.bfloat16)
+    ids = torch.randint(0, V, (4, S), device="cuda", dtype=torch.int32)
+    _close(ops.embed_ln(ids, word, pos, typ, g, b), ops.embed_ln_ref(ids, word, pos, typ, g, b), 3e-2, 2e-2)
+
+
+@pytest.mark.parametrize("B,S,H,Hkv,D,causal,use_lens", [
+    (4, 128, 12, 12, 64, False, False),
+    (3, 128, 12, 12, 64, False, True),
+    (2, 100, 4, 4, 64, False, True),
+    (2, 256, 8, 2, 128, True, False),
+    (1, 200, 4, 1, 128, True, False),
+    (2, 300, 4, 4, 64, False, True),
+])
+def test_attention(B, S, H, Hkv, D, causal, use_lens):
+    ops = _ops()
+    torch.manual_seed(5)
+    qkv = torch.randn(B * S, (H + 2 * Hkv) * D, device="cuda", dtype=torch.bfloat16)
+    lens = None
+    if use_lens:
+        lens = torch.randint(1, S + 1, (B,), device="cuda", dtype=torch.int32)
+        lens[0] = S
+    y = ops.attention(qkv, B, S, H, Hkv, D, lens=lens, causal=causal)
+    ref = ops.attention_ref(qkv, B, S, H, Hkv, D, lens=lens, causal=causal)
+    _close(y, ref, 2e-2, 2e-2)
+
+
+def test_attention_spike_rescale():
+    """Force the online-softmax rescale branch: a key block late in the sequence
+    dominates one query (guide rule 26)."""
+    ops = _ops()
+    B, S, H, D = 1, 384, 2, 64
+    qkv = torch.randn(B * S, 3 * H * D, device="cuda", dtype=torch.bfloat16) * 0.1
+    qkv[5, 0:D] = 3.0            # query 5, head 0
+    qkv[300, H * D:H * D + D] = 3.0  # key 300 (third key block), head 0
+    _close(ops.attention(qkv, B, S, H, H, D), ops.attention_ref(qkv, B, S, H, H, D), 2e-2, 2e-2)
+
+
+def test_softmax_topk():
+    ops = _ops()
+    torch.manual_seed(6)
+    x = torch.randn(37, 1000, device="cuda")
+    p, i = ops.softmax_topk(x, 5)
+    pr, ir = ops.softmax_topk_ref(x, 5)
+    assert torch.equal(i, ir)
+    _close(p, pr, 1e-5, 1e-4)
+
+
+def test_rope():
+    ops = _ops()
+    torch.manual_seed(7)
+    B, S, H, Hkv, D = 2, 64, 8, 2, 128
+    cos, sin = ops.rope_tables(4096, D, device="cuda")
+    qkv = torch.randn(B * S, (H + 2 * Hkv) * D, device="cuda", dtype=torch.bfloat16)
+    ref = ops.rope_ref(qkv, cos, sin, B, S, H, Hkv, D)
+    ops.rope_(qkv, cos, sin, B, S, H, Hkv, D)
+    _close(qkv, ref, 2e-2, 2e-2)
+
+
+@pytest.mark.parametrize("N,H,C,K,R,stride,pad", [
+    (2, 56, 64, 64, 3, 1, 1), (2, 56, 64, 256, 1, 1, 0), (2, 56, 256, 128, 1, 2, 0),
+    (1, 224, 8, 64, 7, 2, 3), (3, 14, 256, 256, 3, 2, 1), (2, 7, 512, 2048, 1, 1, 0)])
+def test_conv2d(N, H, C, K, R, stride, pad):
+    ops = _ops()
+    torch.manual_seed(8)
+    x = torch.randn(N, H, H, C, device="cuda", dtype=torch.float16)
+    w = torch.randn(K, R, R, C, device="cuda", dtype=torch.float16) * (R * R * C) ** -0.5
+    b = torch.randn(K, device="cuda", dtype=torch.float16) * 0.1
+    y = ops.conv2d_nhwc(x, w, b, stride=stride, pad=pad, act="relu")
+    _close(y, ops.conv2d_nhwc_ref(x, w, b, stride=stride, pad=pad, act="relu"), 2e-2, 2e-2)
+    r = torch.randn_like(y)
+    y2 = ops.conv2d_nhwc(x, w, b, stride=stride, pad=pad, act="relu", residual=r)
+    _close(y2, ops.conv2d_nhwc_ref(x, w, b, stride=stride, pad=pad, act="relu", residual=r), 2e-2, 2e-2)
+
+
+def test_pools_and_dwconv():
+    ops = _ops()
+    torch.manual_seed(9)
+    x = torch.randn(2, 112, 112, 64, device="cuda", dtype=torch.float16)
+    _close(ops.maxpool_nhwc(x), ops.maxpool_nhwc_ref(x), 0, 0)
+    _close(ops.avgpool_nhwc(x), ops.avgpool_nhwc_ref(x), 1e-3, 1e-2)
+    w = torch.randn(3, 3, 64, device="cuda", dtype=torch.float16) * 0.3
+    b = torch.randn(64, device="cuda", dtype=torch.float16) * 0.1
+    for stride in (1, 2):
+        _close(ops.dwconv_nhwc(x, w, b, stride=stride, pad=1, act="silu"),
+               ops.dwconv_nhwc_ref(x, w, b, stride=stride, pad=1, act="silu"), 2e-2, 2e-2)
+
+
+def test_image_to_nhwc_and_gather():
+    ops = _ops()
+    img = torch.randint(0, 256, (3, 32, 32, 3), device="cuda", dtype=torch.uint8)
+    _close(ops.image_to_nhwc(img), ops.image_to_nhwc_ref(img), 1e-2, 1e-2)
+    # gather from pinned host rows
+    rows = torch.arange(4 * 64, dtype=torch.int32).reshape(4, 64).pin_memory()
+    ptrs = torch.tensor([rows[i].data_ptr() for i in (2, 0, 3)], dtype=torch.int64).pin_memory()
+    dst = torch.full((5, 64), -1, device="cuda", dtype=torch.int32)
+    ops.gather_rows(ptrs, 3, 5, 256, dst)
+    torch.cuda.synchronize()
+    exp = torch.zeros(5, 64, dtype=torch.int32)
+    exp[0], exp[1], exp[2] = rows[2], rows[0], rows[3]
+    assert torch.equal(dst.cpu(), exp)
