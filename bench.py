@@ -1,0 +1,173 @@
+#!/usr/bin/env python3
+"""Headline benchmark: whole-node req/s vs p99 latency, BERT-base seq128 bf16,
+dynamic batching <= 32, one replica per MI355X (BASELINE.json metric).
+
+    python bench.py --gpus N --steps K --warmup W
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+Every rank is one replica process pinned to its GPU (LOCAL_RANK).  Rank 0 also
+creates the shared-memory job and runs the ingress: a native closed-loop load
+generator whose requests go through the power-of-two-choices router over the
+shm queue depths of ALL replicas.  Each request is one 128-token sequence
+(synthetic token ids, random-init weights); each replica's native engine
+coalesces up to 32 requests or 5 ms, pads to a bucket, gathers the payloads
+H2D on a side stream, replays the hipGraph of the batched forward, and returns
+per-request logits through the completion ring.
+
+One "step" = 32 x N completed requests (one full dynamic batch per replica).
+The timed region is bracketed by barrier + torch.cuda.synchronize() on every
+rank; the reported time is the max over ranks.  Latency percentiles are
+client-side end-to-end (submit -> result received).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+METRIC = "req/s (whole node) vs p99 latency, BERT-base dyn-batch<=32, at 1/2/4/8 MI355X"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=300)
+    ap.add_argument("--warmup", type=int, default=30)
+    ap.add_argument("--max-batch", type=int, default=32)
+    ap.add_argument("--max-wait-ms", type=float, default=5.0)
+    ap.add_argument("--concurrency", type=int, default=96, help="closed-loop requests in flight per GPU")
+    ap.add_argument("--rate", type=float, default=0.0, help="open-loop Poisson rate per GPU (req/s); 0 = closed loop")
+    ap.add_argument("--seq", type=int, default=128)
+    ap.add_argument("--backend", default="hip", choices=["hip", "torch"])
+    ap.add_argument("--pipeline-depth", type=int, default=2)
+    ap.add_argument("--layers", type=int, default=12)
+    ap.add_argument("--json-out", default="")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+
+    from ray_dynamic_batching_amd.models.bert import BertConfig, BertForSequenceClassification
+    from ray_dynamic_batching_amd.runtime import job as rjob
+    from ray_dynamic_batching_amd.runtime.engine import EngineRunner, SessionSpec
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    port = os.environ.get("MASTER_PORT", str(os.getpid()))
+    name = f"bench_{port}"
+    n = world
+    if rank == 0:
+        job = rjob.Job(name, create=True, n_replicas=n, n_queues=n, n_clients=4, req_capacity=4096,
+                       req_slot_bytes=args.seq * 4, cmp_capacity=16384, cmp_slot_bytes=64)
+    barrier()
+    if rank != 0:
+        job = rjob.Job(name, create=False)
+    # each rank owns queue `rank` (model 0) on replica `rank`
+    job.configure_queue(rank, rank, 0, args.concurrency * 2, 0.0, True)
+
+    cfg = BertConfig(seq_len=args.seq, layers=args.layers)
+    model = BertForSequenceClassification(cfg, device="cuda", backend=args.backend)
+    spec = SessionSpec(model=model, queue=rank, max_batch=args.max_batch, max_wait_s=args.max_wait_ms / 1e3)
+    runner = EngineRunner(name, rank, [spec], pipeline_depth=args.pipeline_depth).build()
+    runner.start()
+    barrier()
+
+    result = {}
+    per_step = args.max_batch * n
+    if rank == 0:
+        client = rjob.Client(job)
+        g = torch.Generator().manual_seed(1234)
+        payloads = []
+        for _ in range(256):
+            ids = torch.randint(1, cfg.vocab_size, (args.seq,), generator=g, dtype=torch.int32)
+            ids[0] = 101
+            payloads.append(ids.numpy().tobytes())
+        lg = rjob.LoadGen(client, 0, payloads)
+        conc = args.concurrency * n
+        rate = args.rate * n
+        lg.run(args.warmup * per_step, conc, rate, 0.0, False, 600.0)
+    barrier()
+    torch.cuda.synchronize()
+    if rank == 0:
+        job.reset_stats()
+        rep0 = [job.replica_stats(r) for r in range(n)]
+    barrier()
+    t0 = time.perf_counter()
+    if rank == 0:
+        result = lg.run(args.steps * per_step, conc, rate, 0.0, True, 1200.0)
+    barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    barrier()
+    err = runner.error()
+    if world > 1:
+        t = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+    if rank == 0:
+        rep1 = [job.replica_stats(r) for r in range(n)]
+        rep = [{k: rep1[i][k] - rep0[i][k] for k in ("batches", "batch_items", "busy_ms")} for i in range(n)]
+        ok = result["ok"]
+        value = ok / elapsed
+        lat = result["latency"]
+        line = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "req/s",
+            "n_gpus": n,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic (random token ids, random-init weights)",
+            "config": {"model": "bert-base (12L, 768H, 12 heads), sequence classification",
+                       "global_batch": args.max_batch * n, "seq_len": args.seq,
+                       "parallelism": f"dp{n}", "max_batch": args.max_batch,
+                       "batch_wait_timeout_ms": args.max_wait_ms, "backend": args.backend,
+                       "load": (f"closed-loop x{args.concurrency}/GPU" if args.rate <= 0 else f"poisson {args.rate}/s/GPU")},
+            "p50_ms": round(lat["p50_ms"], 3),
+            "p99_ms": round(lat["p99_ms"], 3),
+            "p999_ms": round(lat["p999_ms"], 3),
+            "mean_ms": round(lat["mean_ms"], 3),
+            "completed": result["completed"],
+            "dropped": result["dropped"],
+            "errors": result["errors"],
+            "mean_batch": round(sum(r["batch_items"] for r in rep) / max(1, sum(r["batches"] for r in rep)), 2),
+            "gpu_busy_frac": round(sum(r["busy_ms"] for r in rep) / (n * elapsed * 1e3), 3) if elapsed > 0 else None,
+            "per_replica_requests": [r["batch_items"] for r in rep],
+        }
+        if err:
+            line["engine_error"] = err
+        print(json.dumps(line), flush=True)
+        if args.json_out:
+            with open(args.json_out, "w") as f:
+                json.dump(line, f, indent=1)
+    runner.stop()
+    barrier()
+    job.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,169 @@
+"""BERT-base sequence classifier (random init) on the gfx950 kernels.
+
+The north-star serving model (BASELINE.json: "BERT-base seq128 bf16").  The
+``hip`` backend runs every op of the batched forward on the hand-written
+kernels of :mod:`ray_dynamic_batching_amd.ops`:
+
+  embed_ln (gather + LN fused) -> 12 x [ QKV GEMM(+bias) -> fused attention
+  (reads the packed QKV, key-padding mask from per-row lengths) -> out GEMM
+  (+bias +residual) -> LN -> FFN1 GEMM(+bias +GELU) -> FFN2 GEMM(+bias
+  +residual) -> LN ] -> pooler GEMM(+tanh) on the strided CLS rows ->
+  classifier GEMM (f32 logits)
+
+so one layer is 7 kernel launches and the whole forward is 87; it is captured
+once per batch bucket into a hipGraph by the replica engine.  The ``torch``
+backend is the eager PyTorch baseline (what the reference's serving path
+runs: ``model(inputs)`` at scheduler.py:450).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+
+import torch
+import torch.nn.functional as F
+
+from .. import ops
+
+
+@dataclass
+class BertConfig:
+    vocab_size: int = 30522
+    hidden: int = 768
+    layers: int = 12
+    heads: int = 12
+    intermediate: int = 3072
+    max_position: int = 512
+    type_vocab: int = 2
+    eps: float = 1e-12
+    num_labels: int = 2
+    seq_len: int = 128
+    pad_token_id: int = 0
+
+    @staticmethod
+    def base(**kw) -> "BertConfig":
+        return BertConfig(**kw)
+
+    @staticmethod
+    def tiny(**kw) -> "BertConfig":
+        d = dict(vocab_size=1000, hidden=256, layers=2, heads=4, intermediate=512, max_position=128, seq_len=32)
+        d.update(kw)
+        return BertConfig(**d)
+
+
+class BertForSequenceClassification:
+    """Weights are plain tensors (random N(0, 0.02) init, as BERT's initializer)."""
+
+    def __init__(self, cfg: BertConfig = None, device="cuda", dtype=torch.bfloat16, backend: str = "hip",
+                 seed: int = 0):
+        self.cfg = cfg = cfg or BertConfig()
+        self.device = torch.device(device)
+        self.dtype = dtype
+        if backend == "hip" and self.device.type != "cuda":
+            raise ValueError("the hip backend needs a GPU device")
+        self.backend = backend
+        g = torch.Generator(device="cpu").manual_seed(seed)
+        D, I = cfg.hidden, cfg.intermediate
+
+        def w(*shape, std=0.02):
+            return (torch.randn(*shape, generator=g) * std).to(device=self.device, dtype=dtype)
+
+        def ones(n):
+            return torch.ones(n, device=self.device, dtype=dtype)
+
+        def zeros(n):
+            return torch.zeros(n, device=self.device, dtype=dtype)
+
+        self.word = w(cfg.vocab_size, D)
+        self.pos = w(cfg.max_position, D)
+        self.typ = w(cfg.type_vocab, D)
+        self.emb_g, self.emb_b = ones(D), zeros(D)
+        self.layers = []
+        for _ in range(cfg.layers):
+            self.layers.append(dict(
+                w_qkv=w(3 * D, D), b_qkv=w(3 * D), w_o=w(D, D), b_o=w(D),
+                ln1_g=ones(D), ln1_b=zeros(D), w_i=w(I, D), b_i=w(I), w_out=w(D, I), b_out=w(D),
+                ln2_g=ones(D), ln2_b=zeros(D)))
+        self.w_pool, self.b_pool = w(D, D), w(D)
+        self.w_cls, self.b_cls = w(cfg.num_labels, D), w(cfg.num_labels)
+
+    # -- serving contract (see runtime.engine.EngineRunner) --------------------
+    @property
+    def input_shape(self):
+        return (self.cfg.seq_len,)
+
+    input_dtype = torch.int32
+
+    @property
+    def output_shape(self):
+        return (self.cfg.num_labels,)
+
+    output_dtype = torch.float32
+
+    def param_bytes(self) -> int:
+        n = sum(t.numel() for t in [self.word, self.pos, self.typ, self.w_pool, self.w_cls])
+        n += sum(t.numel() for L in self.layers for t in L.values())
+        return n * torch.finfo(self.dtype).bits // 8
+
+    def flops_per_sequence(self) -> float:
+        c, S = self.cfg, self.cfg.seq_len
+        per_tok = 2 * (4 * c.hidden * c.hidden + 2 * c.hidden * c.intermediate)
+        attn = 2 * 2 * S * c.hidden
+        return c.layers * S * (per_tok + attn)
+
+    def __call__(self, ids: torch.Tensor) -> torch.Tensor:
+        return self.forward(ids)
+
+    @torch.no_grad()
+    def forward(self, ids: torch.Tensor) -> torch.Tensor:
+        if self.backend == "hip":
+            return self._forward_hip(ids)
+        return self._forward_torch(ids)
+
+    def _forward_hip(self, ids: torch.Tensor) -> torch.Tensor:
+        c = self.cfg
+        B, S = ids.shape
+        D, H = c.hidden, c.heads
+        lens = (ids != c.pad_token_id).sum(dim=1, dtype=torch.int32).clamp_(min=1)
+        h = ops.embed_ln(ids, self.word, self.pos, self.typ, self.emb_g, self.emb_b, c.eps)
+        for L in self.layers:
+            qkv = ops.linear(h, L["w_qkv"], L["b_qkv"])
+            ctx = ops.attention(qkv, B, S, H, H, D // H, lens=lens)
+            a = ops.linear(ctx, L["w_o"], L["b_o"], residual=h)
+            h1 = ops.layer_norm(a, L["ln1_g"], L["ln1_b"], c.eps)
+            inter = ops.linear(h1, L["w_i"], L["b_i"], act="gelu")
+            o = ops.linear(inter, L["w_out"], L["b_out"], residual=h1)
+            h = ops.layer_norm(o, L["ln2_g"], L["ln2_b"], c.eps)
+        cls = h.view(B, S, D)[:, 0, :]
+        pooled = ops.linear(cls, self.w_pool, self.b_pool, act="tanh")
+        return ops.linear(pooled, self.w_cls, self.b_cls, out_dtype=torch.float32)
+
+    def _forward_torch(self, ids: torch.Tensor) -> torch.Tensor:
+        c = self.cfg
+        B, S = ids.shape
+        D, H = c.hidden, c.heads
+        Dh = D // H
+        idl = ids.long()
+        mask = (idl != c.pad_token_id)
+        x = self.word[idl] + self.pos[:S][None] + self.typ[0][None, None]
+        h = F.layer_norm(x, (D,), self.emb_g, self.emb_b, c.eps)
+        attn_mask = mask[:, None, None, :]
+        for L in self.layers:
+            qkv = F.linear(h, L["w_qkv"], L["b_qkv"])
+            q, k, v = qkv.split(D, dim=-1)
+            q = q.view(B, S, H, Dh).transpose(1, 2)
+            k = k.view(B, S, H, Dh).transpose(1, 2)
+            v = v.view(B, S, H, Dh).transpose(1, 2)
+            ctx = F.scaled_dot_product_attention(q, k, v, attn_mask=attn_mask)
+            ctx = ctx.transpose(1, 2).reshape(B, S, D)
+            h1 = F.layer_norm(F.linear(ctx, L["w_o"], L["b_o"]) + h, (D,), L["ln1_g"], L["ln1_b"], c.eps)
+            inter = F.gelu(F.linear(h1, L["w_i"], L["b_i"]))
+            h = F.layer_norm(F.linear(inter, L["w_out"], L["b_out"]) + h1, (D,), L["ln2_g"], L["ln2_b"], c.eps)
+        pooled = torch.tanh(F.linear(h[:, 0], self.w_pool, self.b_pool))
+        return F.linear(pooled, self.w_cls, self.b_cls).float()
+
+    def example_input(self, batch: int, seed: int = 0, device=None) -> torch.Tensor:
+        g = torch.Generator(device="cpu").manual_seed(seed)
+        ids = torch.randint(1, self.cfg.vocab_size, (batch, self.cfg.seq_len), generator=g, dtype=torch.int32)
+        ids[:, 0] = 101  # [CLS]
+        return ids.to(device or self.device)

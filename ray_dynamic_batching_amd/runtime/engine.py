@@ -1,0 +1,135 @@
+"""GPU replica engine driver: captures one hipGraph per (batch bucket, pipeline
+slot) for a servable model and hands them to the native Engine, which then runs
+the whole batching / H2D / replay / D2H / completion loop without Python.
+
+A *servable model* exposes ``input_shape``, ``input_dtype``, ``output_shape``,
+``output_dtype`` (per request) and ``forward(x[B, *input_shape])``.
+"""
+from __future__ import annotations
+
+import time
+from dataclasses import dataclass, field
+from typing import List, Optional, Sequence
+
+import torch
+
+from ..utils.native import require_gpu_ops
+
+
+def default_buckets(max_batch: int) -> List[int]:
+    b, out = 1, []
+    while b < max_batch:
+        out.append(b)
+        b *= 2
+    out.append(max_batch)
+    # finer buckets near the top where padding waste costs the most
+    extra = [max_batch * 3 // 4] if max_batch >= 8 else []
+    return sorted(set(out + [e for e in extra if e > 0]))
+
+
+@dataclass
+class SessionSpec:
+    model: object
+    queue: int
+    max_batch: int = 32
+    max_wait_s: float = 0.005
+    buckets: Optional[Sequence[int]] = None
+    priority: int = 0
+    slo_ms: float = 0.0
+    drop_stale: bool = False
+    name: str = ""
+    # filled by the runner
+    sid: int = -1
+    graphs: list = field(default_factory=list)
+    inputs: list = field(default_factory=list)
+    outputs: list = field(default_factory=list)
+
+
+class EngineRunner:
+    def __init__(self, job_name: str, replica: int, sessions: Sequence[SessionSpec], pipeline_depth: int = 2,
+                 zero_copy: bool = True, device: Optional[int] = None, warmup_iters: int = 2):
+        self.ops = require_gpu_ops()
+        self.device = torch.cuda.current_device() if device is None else device
+        self.job_name = job_name
+        self.replica = replica
+        self.depth = pipeline_depth
+        self.sessions = list(sessions)
+        self.engine = self.ops.Engine(job_name, replica, pipeline_depth, zero_copy, self.device, 0)
+        self.pool = None
+        self.capture_s = 0.0
+        self.warmup_iters = warmup_iters
+
+    def _bytes(self, shape, dtype) -> int:
+        n = 1
+        for s in shape:
+            n *= s
+        return n * torch.empty((), dtype=dtype).element_size()
+
+    def build(self) -> "EngineRunner":
+        t0 = time.perf_counter()
+        dev = torch.device("cuda", self.device)
+        self.pool = torch.cuda.graph_pool_handle()
+        for s in self.sessions:
+            m = s.model
+            buckets = sorted(set(s.buckets or default_buckets(s.max_batch)))
+            if buckets[-1] != s.max_batch:
+                buckets.append(s.max_batch)
+            s.buckets = buckets
+            in_bytes = self._bytes(m.input_shape, m.input_dtype)
+            out_bytes = self._bytes(m.output_shape, m.output_dtype)
+            s.sid = self.engine.add_session(s.queue, s.max_batch, s.max_wait_s, buckets, in_bytes, out_bytes,
+                                            s.priority, s.slo_ms, s.drop_stale)
+            s.inputs = []
+            for slot in range(self.depth):
+                x = torch.zeros((s.max_batch,) + tuple(m.input_shape), dtype=m.input_dtype, device=dev)
+                if hasattr(m, "example_input") and m.input_dtype in (torch.int32, torch.int64):
+                    x.copy_(m.example_input(s.max_batch, seed=slot, device=dev))
+                s.inputs.append(x)
+                self.engine.set_input(s.sid, slot, x.data_ptr())
+            # warm up every bucket eagerly on a side stream (lazy init, caches)
+            side = torch.cuda.Stream(device=dev)
+            side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side):
+                for b in buckets:
+                    for _ in range(self.warmup_iters):
+                        m.forward(s.inputs[0][:b])
+            torch.cuda.current_stream().wait_stream(side)
+            torch.cuda.synchronize()
+            s.graphs = [[None] * self.depth for _ in buckets]
+            s.outputs = [[None] * self.depth for _ in buckets]
+            for bi, b in enumerate(buckets):
+                for slot in range(self.depth):
+                    g = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(g, pool=self.pool):
+                        y = m.forward(s.inputs[slot][:b])
+                    if not y.is_contiguous():
+                        raise RuntimeError("servable model output must be contiguous")
+                    s.graphs[bi][slot] = g
+                    s.outputs[bi][slot] = y
+                    self.engine.set_graph(s.sid, bi, slot, g.raw_cuda_graph_exec(), y.data_ptr())
+            # latency estimates per bucket (used for stale-request dropping)
+            for bi, b in enumerate(buckets):
+                g = s.graphs[bi][0]
+                g.replay()
+                torch.cuda.synchronize()
+                t = time.perf_counter()
+                for _ in range(3):
+                    g.replay()
+                torch.cuda.synchronize()
+                self.engine.set_latency_estimate(s.sid, bi, (time.perf_counter() - t) / 3 * 1e3)
+        torch.cuda.synchronize()
+        self.capture_s = time.perf_counter() - t0
+        return self
+
+    def start(self):
+        self.engine.start()
+        return self
+
+    def stop(self):
+        self.engine.stop()
+
+    def stats(self):
+        return self.engine.stats()
+
+    def error(self) -> str:
+        return self.engine.error()
