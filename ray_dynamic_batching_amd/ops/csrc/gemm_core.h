@@ -11,8 +11,9 @@
 //  * v_mfma_f32_16x16x32_{bf16,f16} with SWAPPED operands (W fragment as the
 //    MFMA A operand): the accumulator then holds 4 consecutive n for one m per
 //    lane, so the fused epilogue stores 8 contiguous bytes per lane.
-//  * BK = 64, two LDS buffers, register-staged prefetch of tile k+1 issued
-//    before the MFMAs of tile k (async-STAGE split, T14), one barrier per K-step.
+//  * BK = 64, two LDS stages filled by LDS-DMA (buffer_load ... lds, bounds-
+//    checked: out-of-range rows/k read as 0 with no branch); the DMA of tile k+1
+//    is issued before the MFMAs of tile k; one barrier per K-step.
 //  * LDS rows are 128 B; the 16-B chunk index is XOR-swizzled with (row>>1)&7 so
 //    each 16-lane group of ds_read_b128 hits 16 distinct bank quads (T2).
 //  * XCD-aware bijective block remap: the N-tiles of one M-panel share an L2 (T1).
@@ -67,7 +68,33 @@ __device__ __forceinline__ float act_rt(int act, float x) {
   }
 }
 
-// ---- A-operand loaders ------------------------------------------------------
+// ---- buffer-resource helpers (T8): out-of-range loads return 0 with no branch ----
+constexpr uint32_t kOOB = 0x80000000u;  // voffset sentinel beyond every num_records
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ u32x4 bload16(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+}
+__device__ __forceinline__ u32x2 bload8(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0);
+}
+__device__ __forceinline__ uint32_t bload4(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0);
+}
+
+// ---- A-operand loaders -------------------------------------------------------
+// Staging is LDS-DMA (buffer_load ... lds): each wave instruction writes 1 KiB =
+// 8 rows x 128 B of the tile LINEARLY into LDS, lane l -> row 8*j + l/8,
+// physical chunk l%8.  The XOR swizzle of the LDS image is therefore applied on
+// the SOURCE side (guide rule 21): lane l fetches logical chunk
+// (l%8) ^ ((row>>1)&7).  Loaders return the byte offset of that 16-B chunk in
+// their buffer resource, or kOOB (zero fill, no branch).
+__device__ __forceinline__ int dma_row(int tid, int nch, int i) {
+  return (((tid >> 6) * nch + i) << 3) + ((tid & 63) >> 3);
+}
+__device__ __forceinline__ int dma_chunk(int tid, int row) { return (tid & 7) ^ ((row >> 1) & 7); }
+
 struct DenseParams {
   const void* A;
   int lda, M, K;
@@ -75,22 +102,24 @@ struct DenseParams {
 template <typename T, int NCH>
 struct DenseLoader {
   typedef DenseParams Params;
-  const T* rowp[NCH];
-  bool ok[NCH];
+  __amdgpu_buffer_rsrc_t rsrc;
+  uint32_t rowoff[NCH];
+  int chunk[NCH];
   int K;
   __device__ __forceinline__ void init(const Params& p, int tid, int m0) {
     K = p.K;
+    rsrc = make_rsrc(p.A, (uint32_t)((size_t)(p.M - 1) * p.lda * sizeof(T) + (size_t)p.K * sizeof(T)));
 #pragma unroll
     for (int i = 0; i < NCH; ++i) {
-      const int row = (tid + 256 * i) >> 3;
+      const int row = dma_row(tid, NCH, i);
+      chunk[i] = dma_chunk(tid, row);
       const int gm = m0 + row;
-      ok[i] = gm < p.M;
-      rowp[i] = reinterpret_cast<const T*>(p.A) + (size_t)(ok[i] ? gm : 0) * p.lda;
+      rowoff[i] = gm < p.M ? (uint32_t)((size_t)gm * p.lda * sizeof(T)) : kOOB;
     }
   }
-  __device__ __forceinline__ u32x4 load(int i, int gk) const {
-    if (ok[i] && gk < K) return *reinterpret_cast<const u32x4*>(rowp[i] + gk);
-    return u32x4{0, 0, 0, 0};
+  __device__ __forceinline__ uint32_t offset(int i, int k0) const {
+    const int gk = k0 + chunk[i] * 8;
+    return (gk < K && rowoff[i] != kOOB) ? rowoff[i] + (uint32_t)(gk * sizeof(T)) : kOOB;
   }
 };
 
@@ -102,40 +131,46 @@ struct ConvParams {
 template <typename T, int NCH>
 struct Im2colLoader {
   typedef ConvParams Params;
-  const T* img[NCH];
-  int h0[NCH], w0[NCH];
-  bool ok[NCH];
+  __amdgpu_buffer_rsrc_t rsrc;
+  uint32_t imgoff[NCH];
+  int h0[NCH], w0[NCH], chunk[NCH];
   int K, C, S, H, W;
   __device__ __forceinline__ void init(const Params& p, int tid, int m0) {
     K = p.K; C = p.C; S = p.S; H = p.H; W = p.W;
+    rsrc = make_rsrc(p.x, (uint32_t)((size_t)p.N * p.H * p.W * p.C * sizeof(T)));
 #pragma unroll
     for (int i = 0; i < NCH; ++i) {
-      const int row = (tid + 256 * i) >> 3;
-      int gm = m0 + row;
-      ok[i] = gm < p.M;
-      gm = ok[i] ? gm : 0;
+      const int row = dma_row(tid, NCH, i);
+      chunk[i] = dma_chunk(tid, row);
+      const int gm = m0 + row;
       const int pq = p.P * p.Q;
       const int n = gm / pq;
       const int rem = gm - n * pq;
-      const int pp = rem / p.Q, qq = rem - (rem / p.Q) * p.Q;
-      h0[i] = pp * p.stride - p.pad;
+      const int pp = rem / p.Q, qq = rem - pp * p.Q;
+      h0[i] = gm < p.M ? pp * p.stride - p.pad : -(1 << 20);
       w0[i] = qq * p.stride - p.pad;
-      img[i] = reinterpret_cast<const T*>(p.x) + (size_t)n * p.H * p.W * p.C;
+      imgoff[i] = (uint32_t)((size_t)n * p.H * p.W * p.C * sizeof(T));
     }
   }
-  __device__ __forceinline__ u32x4 load(int i, int gk) const {
-    if (!ok[i] || gk >= K) return u32x4{0, 0, 0, 0};
+  __device__ __forceinline__ uint32_t offset(int i, int k0) const {
+    const int gk = k0 + chunk[i] * 8;
     const int rs = gk / C;
     const int cc = gk - rs * C;
-    const int r = rs / S, s = rs - (rs / S) * S;
+    const int r = rs / S, s = rs - r * S;
     const int h = h0[i] + r, w = w0[i] + s;
-    if ((unsigned)h >= (unsigned)H || (unsigned)w >= (unsigned)W) return u32x4{0, 0, 0, 0};
-    return *reinterpret_cast<const u32x4*>(img[i] + ((size_t)h * W + w) * C + cc);
+    const bool ok = gk < K && (unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W;
+    return ok ? imgoff[i] + (uint32_t)((((size_t)h * W + w) * C + cc) * sizeof(T)) : kOOB;
   }
 };
 
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, char* lds, uint32_t off) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_ptr_t)lds, 16, off, 0, 0, 0);
+}
+
 // ---- the kernel ---------------------------------------------------------------
-template <typename T, typename OutT, int BM, int BN, template <typename, int> class LoaderT>
+template <typename T, typename OutT, int BM, int BN, template <typename, int> class LoaderT, bool HAS_BIAS,
+          bool HAS_RES>
 __global__ void __launch_bounds__(256, 2)
 mfma_gemm_kernel(typename LoaderT<T, BM * 8 / 256>::Params ap, const T* __restrict__ W, int ldw,
                  OutT* __restrict__ C, int ldc, const T* __restrict__ bias,
@@ -164,36 +199,28 @@ mfma_gemm_kernel(typename LoaderT<T, BM * 8 / 256>::Params ap, const T* __restri
 
   LoaderT<T, A_CH> la;
   la.init(ap, tid, m0);
-  const int cA = tid & 7;
 
-  const T* wrow[W_CH];
-  bool wok[W_CH];
+  const __amdgpu_buffer_rsrc_t wsrc = make_rsrc(W, (uint32_t)((size_t)(N - 1) * ldw * sizeof(T) + (size_t)K * sizeof(T)));
+  uint32_t woff[W_CH];
+  int wch[W_CH];
 #pragma unroll
   for (int i = 0; i < W_CH; ++i) {
-    const int gn = n0 + ((tid + 256 * i) >> 3);
-    wok[i] = gn < N;
-    wrow[i] = W + (size_t)(wok[i] ? gn : 0) * ldw;
+    const int row = dma_row(tid, W_CH, i);
+    wch[i] = dma_chunk(tid, row);
+    const int gn = n0 + row;
+    woff[i] = gn < N ? (uint32_t)((size_t)gn * ldw * sizeof(T)) : kOOB;
   }
-
-  u32x4 ra[A_CH], rw[W_CH];
-  auto gload = [&](int k0) {
-    const int gk = k0 + cA * 8;
+  // wave-uniform LDS bases of this wave's DMA pieces
+  const int wid_u = __builtin_amdgcn_readfirstlane(wid);
+  auto stage = [&](int buf, int k0) {
+    char* base = smem + buf * kStage;
 #pragma unroll
-    for (int i = 0; i < A_CH; ++i) ra[i] = la.load(i, gk);
-#pragma unroll
-    for (int i = 0; i < W_CH; ++i)
-      rw[i] = (wok[i] && gk < K) ? *reinterpret_cast<const u32x4*>(wrow[i] + gk) : u32x4{0, 0, 0, 0};
-  };
-  auto lstore = [&](int buf) {
-#pragma unroll
-    for (int i = 0; i < A_CH; ++i) {
-      const int row = (tid + 256 * i) >> 3;
-      *reinterpret_cast<u32x4*>(smem + buf * kStage + swz_off(row, cA)) = ra[i];
-    }
+    for (int i = 0; i < A_CH; ++i) dma16(la.rsrc, base + (wid_u * A_CH + i) * 1024, la.offset(i, k0));
 #pragma unroll
     for (int i = 0; i < W_CH; ++i) {
-      const int row = (tid + 256 * i) >> 3;
-      *reinterpret_cast<u32x4*>(smem + buf * kStage + BM * BK * 2 + swz_off(row, cA)) = rw[i];
+      const int gk = k0 + wch[i] * 8;
+      const uint32_t off = (gk < K && woff[i] != kOOB) ? woff[i] + (uint32_t)(gk * sizeof(T)) : kOOB;
+      dma16(wsrc, base + BM * BK * 2 + (wid_u * W_CH + i) * 1024, off);
     }
   };
 
@@ -203,16 +230,9 @@ mfma_gemm_kernel(typename LoaderT<T, BM * 8 / 256>::Params ap, const T* __restri
 #pragma unroll
     for (int j = 0; j < TM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int nk = (K + BK - 1) / BK;
-  gload(0);
-  lstore(0);
-  __syncthreads();
-
   const int fr = lane & 15, fg = lane >> 4;
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nk) gload((kt + 1) * BK);
-    const char* sa = smem + cur * kStage;
+  auto compute = [&](int buf) {
+    const char* sa = smem + buf * kStage;
     const char* sw = sa + BM * BK * 2;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
@@ -229,51 +249,129 @@ mfma_gemm_kernel(typename LoaderT<T, BM * 8 / 256>::Params ap, const T* __restri
 #pragma unroll
         for (int j = 0; j < TM; ++j) acc[i][j] = MfmaOp<T>::mma(wf[i], af[j], acc[i][j]);
     }
-    if (kt + 1 < nk) lstore(cur ^ 1);
+  };
+
+  // Two LDS stages: the DMA of tile k+1 runs under the MFMAs of tile k; the
+  // __syncthreads() at the end of a step waits the issuing waves' DMA
+  // (vmcnt(0)) and orders every wave's reads before the buffer is refilled.
+  const int nk = (K + BK - 1) / BK;
+  stage(0, 0);
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    if (kt + 1 < nk) stage((kt + 1) & 1, (kt + 1) * BK);
+    compute(kt & 1);
     __syncthreads();
   }
 
   // ---- fused epilogue: lane holds C[m][n..n+3] ----
+  // All bias / residual loads are issued up front as vector buffer loads (OOB ->
+  // 0, no per-element branch or wait), then the activation is applied in a loop
+  // selected ONCE (no per-element switch).
+  const bool swiglu = act == ACT_SWIGLU;
+  const int n_out = swiglu ? (N >> 1) : N;
+  float bv[TN][4];
+#pragma unroll
+  for (int i = 0; i < TN; ++i) {
+    const int n = n0 + wn * WN + i * 16 + fg * 4;
+    if constexpr (HAS_BIAS) {
+      const __amdgpu_buffer_rsrc_t bsrc = make_rsrc(bias, (uint32_t)(N * sizeof(T)));
+      const u32x2 raw = bload8(bsrc, (uint32_t)(n * sizeof(T)));
+      const T* e = reinterpret_cast<const T*>(&raw);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) bv[i][q] = (float)e[q];
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) bv[i][q] = 0.f;
+    }
+  }
+  float rv[TM][TN][4];
+  if constexpr (HAS_RES) {
+    const __amdgpu_buffer_rsrc_t rsrc = make_rsrc(R, (uint32_t)((size_t)(M - 1) * ldr * sizeof(T) + (size_t)n_out * sizeof(T)));
+#pragma unroll
+    for (int j = 0; j < TM; ++j) {
+      const int m = m0 + wm * WM + j * 16 + fr;
+#pragma unroll
+      for (int i = 0; i < TN; ++i) {
+        const int n = n0 + wn * WN + i * 16 + fg * 4;
+        if (!swiglu) {
+          const uint32_t off = (m < M && n < N) ? (uint32_t)(((size_t)m * ldr + n) * sizeof(T)) : kOOB;
+          const u32x2 raw = bload8(rsrc, off);
+          const T* e = reinterpret_cast<const T*>(&raw);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) rv[j][i][q] = (float)e[q];
+        } else {
+          const uint32_t off = (m < M && n < N) ? (uint32_t)(((size_t)m * ldr + (n >> 1)) * sizeof(T)) : kOOB;
+          const uint32_t raw = bload4(rsrc, off);
+          const T* e = reinterpret_cast<const T*>(&raw);
+          rv[j][i][0] = (float)e[0];
+          rv[j][i][1] = (float)e[1];
+        }
+      }
+    }
+  }
+  // x = alpha * acc + bias (in place)
+#pragma unroll
+  for (int i = 0; i < TN; ++i)
+#pragma unroll
+    for (int j = 0; j < TM; ++j)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) acc[i][j][q] = alpha * acc[i][j][q] + bv[i][q];
+
+  if (swiglu) {
+#pragma unroll
+    for (int j = 0; j < TM; ++j) {
+      const int m = m0 + wm * WM + j * 16 + fr;
+#pragma unroll
+      for (int i = 0; i < TN; ++i) {
+        const int n = n0 + wn * WN + i * 16 + fg * 4;
+        float r0 = apply_act<ACT_SILU>(acc[i][j][0]) * acc[i][j][1];
+        float r1 = apply_act<ACT_SILU>(acc[i][j][2]) * acc[i][j][3];
+        if constexpr (HAS_RES) { r0 += rv[j][i][0]; r1 += rv[j][i][1]; }
+        if (m < M && n < N) {
+          OutT* cp = C + (size_t)m * ldc + (n >> 1);
+          cp[0] = (OutT)r0;
+          cp[1] = (OutT)r1;
+        }
+      }
+    }
+    return;
+  }
+  if constexpr (HAS_RES) {
+#pragma unroll
+    for (int i = 0; i < TN; ++i)
+#pragma unroll
+      for (int j = 0; j < TM; ++j)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc[i][j][q] += rv[j][i][q];
+  }
+#define RDB_ACT_LOOP(A)                                       \
+  _Pragma("unroll") for (int i = 0; i < TN; ++i)             \
+  _Pragma("unroll") for (int j = 0; j < TM; ++j)             \
+  _Pragma("unroll") for (int q = 0; q < 4; ++q) acc[i][j][q] = apply_act<A>(acc[i][j][q]);
+  switch (act) {
+    case ACT_GELU: RDB_ACT_LOOP(ACT_GELU) break;
+    case ACT_RELU: RDB_ACT_LOOP(ACT_RELU) break;
+    case ACT_TANH: RDB_ACT_LOOP(ACT_TANH) break;
+    case ACT_SILU: RDB_ACT_LOOP(ACT_SILU) break;
+    case ACT_GELU_TANH: RDB_ACT_LOOP(ACT_GELU_TANH) break;
+    default: break;
+  }
+#undef RDB_ACT_LOOP
+  const bool vec_ok = ((ldc & 3) == 0);
 #pragma unroll
   for (int j = 0; j < TM; ++j) {
     const int m = m0 + wm * WM + j * 16 + fr;
-    if (m >= M) continue;
 #pragma unroll
     for (int i = 0; i < TN; ++i) {
       const int n = n0 + wn * WN + i * 16 + fg * 4;
-      if (n >= N) continue;
-      if (act == ACT_SWIGLU) {  // W rows interleaved (gate_j, up_j) -> out column n/2
-        float g0 = alpha * acc[i][j][0], u0 = alpha * acc[i][j][1];
-        float g1 = alpha * acc[i][j][2], u1 = alpha * acc[i][j][3];
-        if (bias != nullptr) {
-          g0 += (float)bias[n]; u0 += (float)bias[n + 1];
-          g1 += (float)bias[n + 2]; u1 += (float)bias[n + 3];
-        }
-        float r0 = apply_act<ACT_SILU>(g0) * u0, r1 = apply_act<ACT_SILU>(g1) * u1;
-        if (R != nullptr) {
-          r0 += (float)R[(size_t)m * ldr + (n >> 1)];
-          r1 += (float)R[(size_t)m * ldr + (n >> 1) + 1];
-        }
-        OutT* cp = C + (size_t)m * ldc + (n >> 1);
-        cp[0] = (OutT)r0;
-        cp[1] = (OutT)r1;
-        continue;
-      }
-      float v[4];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        float x = alpha * acc[i][j][e];
-        if (bias != nullptr && n + e < N) x += (float)bias[n + e];
-        if (R != nullptr && n + e < N) x += (float)R[(size_t)m * ldr + n + e];
-        v[e] = act_rt(act, x);
-      }
+      if (m >= M || n >= N) continue;
       OutT* cp = C + (size_t)m * ldc + n;
-      if (n + 3 < N && ((ldc & 3) == 0)) {
-        store4<OutT>(cp, v[0], v[1], v[2], v[3]);
+      if (n + 3 < N && vec_ok) {
+        store4<OutT>(cp, acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
       } else {
 #pragma unroll
         for (int e = 0; e < 4; ++e)
-          if (n + e < N) cp[e] = (OutT)v[e];
+          if (n + e < N) cp[e] = (OutT)acc[i][j][e];
       }
     }
   }
@@ -289,30 +387,43 @@ inline int pick_tile_cfg(int M, int N) {
   return 3;
 }
 
-template <typename T, typename OutT, template <typename, int> class LoaderT, typename P>
-void launch_mfma_gemm(const P& ap, const T* W, int ldw, OutT* C, int ldc, const T* bias, const T* R,
-                      int ldr, int M, int N, int K, float alpha, int act, hipStream_t s, int cfg) {
-  if (cfg < 0) cfg = pick_tile_cfg(M, N);
+template <typename T, typename OutT, template <typename, int> class LoaderT, bool HB, bool HR, typename P>
+void launch_mfma_gemm_t(const P& ap, const T* W, int ldw, OutT* C, int ldc, const T* bias, const T* R,
+                        int ldr, int M, int N, int K, float alpha, int act, hipStream_t s, int cfg) {
   auto nwg = [&](int bm, int bn) { return ((M + bm - 1) / bm) * ((N + bn - 1) / bn); };
   dim3 blk(256);
   switch (cfg) {
     case 0:
-      hipLaunchKernelGGL((mfma_gemm_kernel<T, OutT, 128, 128, LoaderT>), dim3(nwg(128, 128)), blk, 0, s,
+      hipLaunchKernelGGL((mfma_gemm_kernel<T, OutT, 128, 128, LoaderT, HB, HR>), dim3(nwg(128, 128)), blk, 0, s,
                          ap, W, ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act);
       break;
     case 1:
-      hipLaunchKernelGGL((mfma_gemm_kernel<T, OutT, 64, 128, LoaderT>), dim3(nwg(64, 128)), blk, 0, s,
+      hipLaunchKernelGGL((mfma_gemm_kernel<T, OutT, 64, 128, LoaderT, HB, HR>), dim3(nwg(64, 128)), blk, 0, s,
                          ap, W, ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act);
       break;
     case 2:
-      hipLaunchKernelGGL((mfma_gemm_kernel<T, OutT, 128, 64, LoaderT>), dim3(nwg(128, 64)), blk, 0, s,
+      hipLaunchKernelGGL((mfma_gemm_kernel<T, OutT, 128, 64, LoaderT, HB, HR>), dim3(nwg(128, 64)), blk, 0, s,
                          ap, W, ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act);
       break;
     default:
-      hipLaunchKernelGGL((mfma_gemm_kernel<T, OutT, 64, 64, LoaderT>), dim3(nwg(64, 64)), blk, 0, s,
+      hipLaunchKernelGGL((mfma_gemm_kernel<T, OutT, 64, 64, LoaderT, HB, HR>), dim3(nwg(64, 64)), blk, 0, s,
                          ap, W, ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act);
       break;
   }
+}
+
+template <typename T, typename OutT, template <typename, int> class LoaderT, typename P>
+void launch_mfma_gemm(const P& ap, const T* W, int ldw, OutT* C, int ldc, const T* bias, const T* R,
+                      int ldr, int M, int N, int K, float alpha, int act, hipStream_t s, int cfg) {
+  if (cfg < 0) cfg = pick_tile_cfg(M, N);
+  if (bias && R)
+    launch_mfma_gemm_t<T, OutT, LoaderT, true, true>(ap, W, ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act, s, cfg);
+  else if (bias)
+    launch_mfma_gemm_t<T, OutT, LoaderT, true, false>(ap, W, ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act, s, cfg);
+  else if (R)
+    launch_mfma_gemm_t<T, OutT, LoaderT, false, true>(ap, W, ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act, s, cfg);
+  else
+    launch_mfma_gemm_t<T, OutT, LoaderT, false, false>(ap, W, ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act, s, cfg);
 }
 
 }  // namespace rdb
