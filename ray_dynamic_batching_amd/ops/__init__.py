@@ -11,7 +11,8 @@ eager baseline path of the models (``backend="torch"``).
 from __future__ import annotations
 
 import math
-from typing import Optional, Tuple
+import os
+from typing import Callable, Dict, Optional, Tuple
 
 import torch
 import torch.nn.functional as F
@@ -41,6 +42,47 @@ def _check(cond: bool, msg: str) -> None:
 
 def _aligned(t: torch.Tensor, n: int = 16) -> bool:
     return t.data_ptr() % n == 0
+
+
+# ---------------------------------------------------------------------------
+# Per-shape autotuning of the GEMM / conv tile configuration.  The kernels
+# take a tile index (see gemm_core.h kTileBM/kTileBN); on the first eager call
+# of a shape every candidate is timed and the fastest is cached.  Never runs
+# while a hipGraph is being captured (those calls use the cached choice, or the
+# on-device heuristic if the shape was never seen eagerly).
+# ---------------------------------------------------------------------------
+NUM_TILE_CFGS = 8
+_TUNE: Dict[tuple, int] = {}
+
+
+def autotune_enabled() -> bool:
+    return os.environ.get("RDB_AUTOTUNE", "1") == "1"
+
+
+def tuning_table() -> Dict[tuple, int]:
+    return dict(_TUNE)
+
+
+def _tuned_cfg(key: tuple, launch: Callable[[int], None], candidates=range(NUM_TILE_CFGS)) -> int:
+    cfg = _TUNE.get(key)
+    if cfg is not None:
+        return cfg
+    if not autotune_enabled() or torch.cuda.is_current_stream_capturing():
+        return -1
+    best_t, best_c = float("inf"), -1
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for c in candidates:
+        launch(c)
+        s.record()
+        for _ in range(4):
+            launch(c)
+        e.record()
+        e.synchronize()
+        t = s.elapsed_time(e)
+        if t < best_t:
+            best_t, best_c = t, c
+    _TUNE[key] = best_c
+    return best_c
 
 
 # ---------------------------------------------------------------------------
@@ -79,9 +121,13 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
         _check(residual.dtype == x.dtype and residual.shape[-1] == n_out and residual.is_contiguous()
                and residual.numel() == M * n_out, "linear: bad residual")
         ldr = n_out
-    _ops().gemm_tn(DTYPE_CODE[x.dtype], DTYPE_CODE[od], x2.data_ptr(), lda, w.data_ptr(), K, out.data_ptr(),
-                   n_out, _ptr(bias), _ptr(residual), ldr, M, N, K, float(alpha), ACT_CODE[act], _stream(),
-                   int(tile_cfg))
+    args = (DTYPE_CODE[x.dtype], DTYPE_CODE[od], x2.data_ptr(), lda, w.data_ptr(), K, out.data_ptr(),
+            n_out, _ptr(bias), _ptr(residual), ldr, M, N, K, float(alpha), ACT_CODE[act])
+    fn = _ops().gemm_tn
+    if tile_cfg < 0 and od != torch.float32:
+        key = ("gemm", x.dtype, M, N, K, lda, act, bias is not None, residual is not None)
+        tile_cfg = _tuned_cfg(key, lambda c: fn(*args, _stream(), c))
+    fn(*args, _stream(), int(tile_cfg))
     return out
 
 
@@ -325,8 +371,13 @@ def conv2d_nhwc(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] =
     if residual is not None:
         _check(residual.shape == (N, P, Q, K) and residual.is_contiguous() and residual.dtype == torch.float16, "conv2d: bad residual")
     _check(_aligned(x) and _aligned(w), "conv2d: alignment")
-    _ops().conv2d_nhwc(x.data_ptr(), w.data_ptr(), _ptr(bias), _ptr(residual), out.data_ptr(), N, H, W, C, K, R, S,
-                       stride, pad, P, Q, ACT_CODE[act], _stream(), int(tile_cfg))
+    args = (x.data_ptr(), w.data_ptr(), _ptr(bias), _ptr(residual), out.data_ptr(), N, H, W, C, K, R, S,
+            stride, pad, P, Q, ACT_CODE[act])
+    fn = _ops().conv2d_nhwc
+    if tile_cfg < 0:
+        key = ("conv", N, H, W, C, K, R, S, stride, pad, act, bias is not None, residual is not None)
+        tile_cfg = _tuned_cfg(key, lambda c: fn(*args, _stream(), c))
+    fn(*args, _stream(), int(tile_cfg))
     return out
 
 

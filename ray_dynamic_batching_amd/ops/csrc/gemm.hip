@@ -11,6 +11,11 @@
 
 namespace rdb {
 
+void gemm_tn_bf16(const DenseParams& p, uintptr_t W, int ldw, uintptr_t C, int ldc, uintptr_t bias, uintptr_t R,
+                  int ldr, int M, int N, int K, float alpha, int act, hipStream_t s, int cfg, int out_dtype);
+void gemm_tn_f16(const DenseParams& p, uintptr_t W, int ldw, uintptr_t C, int ldc, uintptr_t bias, uintptr_t R,
+                 int ldr, int M, int N, int K, float alpha, int act, hipStream_t s, int cfg, int out_dtype);
+
 // dtype codes shared with the Python side: 0 = bf16, 1 = f16, 2 = f32
 void gemm_tn(int in_dtype, int out_dtype, uintptr_t A, int lda, uintptr_t W, int ldw, uintptr_t C,
              int ldc, uintptr_t bias, uintptr_t R, int ldr, int M, int N, int K, float alpha,
@@ -23,25 +28,9 @@ void gemm_tn(int in_dtype, int out_dtype, uintptr_t A, int lda, uintptr_t W, int
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   DenseParams p{reinterpret_cast<const void*>(A), lda, M, K};
   if (in_dtype == 0) {
-    auto w = reinterpret_cast<const bf16*>(W);
-    auto b = reinterpret_cast<const bf16*>(bias);
-    auto r = reinterpret_cast<const bf16*>(R);
-    if (out_dtype == 0)
-      launch_mfma_gemm<bf16, bf16, DenseLoader>(p, w, ldw, reinterpret_cast<bf16*>(C), ldc, b, r, ldr, M, N, K, alpha, act, s, force_cfg);
-    else if (out_dtype == 2)
-      launch_mfma_gemm<bf16, float, DenseLoader>(p, w, ldw, reinterpret_cast<float*>(C), ldc, b, r, ldr, M, N, K, alpha, act, s, force_cfg);
-    else
-      throw std::invalid_argument("gemm_tn: bf16 input supports bf16/f32 output");
+    gemm_tn_bf16(p, W, ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act, s, force_cfg, out_dtype);
   } else if (in_dtype == 1) {
-    auto w = reinterpret_cast<const f16*>(W);
-    auto b = reinterpret_cast<const f16*>(bias);
-    auto r = reinterpret_cast<const f16*>(R);
-    if (out_dtype == 1)
-      launch_mfma_gemm<f16, f16, DenseLoader>(p, w, ldw, reinterpret_cast<f16*>(C), ldc, b, r, ldr, M, N, K, alpha, act, s, force_cfg);
-    else if (out_dtype == 2)
-      launch_mfma_gemm<f16, float, DenseLoader>(p, w, ldw, reinterpret_cast<float*>(C), ldc, b, r, ldr, M, N, K, alpha, act, s, force_cfg);
-    else
-      throw std::invalid_argument("gemm_tn: f16 input supports f16/f32 output");
+    gemm_tn_f16(p, W, ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act, s, force_cfg, out_dtype);
   } else {
     throw std::invalid_argument("gemm_tn: unsupported input dtype");
   }

@@ -19,6 +19,8 @@
 //  * XCD-aware bijective block remap: the N-tiles of one M-panel share an L2 (T1).
 #pragma once
 #include "common.h"
+#include <algorithm>
+#include <type_traits>
 
 namespace rdb {
 
@@ -377,45 +379,71 @@ mfma_gemm_kernel(typename LoaderT<T, BM * 8 / 256>::Params ap, const T* __restri
   }
 }
 
-// Tile selection: the largest tile that still puts >= 256 workgroups on the
-// 256 CUs (fewer leaves CUs idle), else 64x64.
+// Tile table (index = the `cfg` argument).  4 waves per block in a 2x2 grid;
+// LDS = 2 stages x (BM + BN) x 64 x 2 B (64..96 KiB).  The host picks the entry
+// (autotuned per shape from Python, or the heuristic below): for the serving
+// shapes the dominant effect is wave quantisation -- #tiles vs 256 CUs x
+// blocks/CU -- so non-power-of-two tiles (128x192) matter.
+constexpr int kNumTiles = 8;
+constexpr int kTileBM[kNumTiles] = {128, 64, 128, 64, 128, 192, 256, 128};
+constexpr int kTileBN[kNumTiles] = {128, 128, 64, 64, 192, 128, 128, 256};
+
+inline int tile_blocks_per_cu(int cfg) {
+  const int lds = 2 * (kTileBM[cfg] + kTileBN[cfg]) * 64 * 2;
+  return std::min(2, 163840 / lds);
+}
+// Heuristic: minimise (rounds of blocks over 256 CUs) x (tile work / tile efficiency).
 inline int pick_tile_cfg(int M, int N) {
-  auto nwg = [&](int bm, int bn) { return ((M + bm - 1) / bm) * ((N + bn - 1) / bn); };
-  if (nwg(128, 128) >= 256) return 0;
-  if (nwg(64, 128) >= 256) return 1;
-  if (nwg(128, 64) >= 256) return 2;
-  return 3;
+  int best = 3;
+  double best_t = 1e30;
+  for (int c = 0; c < kNumTiles; ++c) {
+    const int bm = kTileBM[c], bn = kTileBN[c];
+    const long tiles = (long)((M + bm - 1) / bm) * ((N + bn - 1) / bn);
+    const long slots = 256L * tile_blocks_per_cu(c);
+    const long rounds = (tiles + slots - 1) / slots;
+    const double eff = 1.0 / (1.0 + 48.0 / bm + 48.0 / bn);        // LDS/issue overhead per FLOP
+    const double t = (double)rounds * bm * bn * tile_blocks_per_cu(c) / eff;
+    if (t < best_t * 0.98) { best_t = t; best = c; }
+  }
+  return best;
+}
+
+template <typename T, typename OutT, template <typename, int> class LoaderT, bool HB, bool HR, int BM, int BN,
+          typename P>
+void launch_one(const P& ap, const T* W, int ldw, OutT* C, int ldc, const T* bias, const T* R, int ldr, int M,
+                int N, int K, float alpha, int act, hipStream_t s) {
+  const int nwg = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  hipLaunchKernelGGL((mfma_gemm_kernel<T, OutT, BM, BN, LoaderT, HB, HR>), dim3(nwg), dim3(256), 0, s, ap, W, ldw,
+                     C, ldc, bias, R, ldr, M, N, K, alpha, act);
 }
 
 template <typename T, typename OutT, template <typename, int> class LoaderT, bool HB, bool HR, typename P>
 void launch_mfma_gemm_t(const P& ap, const T* W, int ldw, OutT* C, int ldc, const T* bias, const T* R,
                         int ldr, int M, int N, int K, float alpha, int act, hipStream_t s, int cfg) {
-  auto nwg = [&](int bm, int bn) { return ((M + bm - 1) / bm) * ((N + bn - 1) / bn); };
-  dim3 blk(256);
-  switch (cfg) {
-    case 0:
-      hipLaunchKernelGGL((mfma_gemm_kernel<T, OutT, 128, 128, LoaderT, HB, HR>), dim3(nwg(128, 128)), blk, 0, s,
-                         ap, W, ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act);
-      break;
-    case 1:
-      hipLaunchKernelGGL((mfma_gemm_kernel<T, OutT, 64, 128, LoaderT, HB, HR>), dim3(nwg(64, 128)), blk, 0, s,
-                         ap, W, ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act);
-      break;
-    case 2:
-      hipLaunchKernelGGL((mfma_gemm_kernel<T, OutT, 128, 64, LoaderT, HB, HR>), dim3(nwg(128, 64)), blk, 0, s,
-                         ap, W, ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act);
-      break;
-    default:
-      hipLaunchKernelGGL((mfma_gemm_kernel<T, OutT, 64, 64, LoaderT, HB, HR>), dim3(nwg(64, 64)), blk, 0, s,
-                         ap, W, ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act);
-      break;
+#define RDB_TILE(IDX, BM_, BN_) \
+  case IDX: launch_one<T, OutT, LoaderT, HB, HR, BM_, BN_>(ap, W, ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act, s); break;
+  if constexpr (std::is_same<OutT, float>::value) {
+    // f32 output is only used by small heads: one tile shape
+    launch_one<T, OutT, LoaderT, HB, HR, 64, 64>(ap, W, ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act, s);
+  } else {
+    switch (cfg) {
+      RDB_TILE(0, 128, 128)
+      RDB_TILE(1, 64, 128)
+      RDB_TILE(2, 128, 64)
+      RDB_TILE(4, 128, 192)
+      RDB_TILE(5, 192, 128)
+      RDB_TILE(6, 256, 128)
+      RDB_TILE(7, 128, 256)
+      default: launch_one<T, OutT, LoaderT, HB, HR, 64, 64>(ap, W, ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act, s);
+    }
   }
+#undef RDB_TILE
 }
 
 template <typename T, typename OutT, template <typename, int> class LoaderT, typename P>
 void launch_mfma_gemm(const P& ap, const T* W, int ldw, OutT* C, int ldc, const T* bias, const T* R,
                       int ldr, int M, int N, int K, float alpha, int act, hipStream_t s, int cfg) {
-  if (cfg < 0) cfg = pick_tile_cfg(M, N);
+  if (cfg < 0 || cfg >= kNumTiles) cfg = pick_tile_cfg(M, N);
   if (bias && R)
     launch_mfma_gemm_t<T, OutT, LoaderT, true, true>(ap, W, ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act, s, cfg);
   else if (bias)

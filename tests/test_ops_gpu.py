@@ -31,12 +31,12 @@ def test_linear_plain(M, N, K, dtype):
     _close(y, ops.linear_ref(x, w), 2e-2, 2e-2)
 
 
-@pytest.mark.parametrize("cfg", [0, 1, 2, 3])
+@pytest.mark.parametrize("cfg", list(range(8)))
 def test_linear_tile_configs_asymmetric(cfg):
     """A = I with an asymmetric W catches a transposed C-write (guide §3)."""
     ops = _ops()
-    M = K = 256
-    N = 192
+    M = K = 384
+    N = 320
     x = torch.eye(M, K, device="cuda", dtype=torch.bfloat16)
     w = (torch.arange(N * K, device="cuda").reshape(N, K) % 97).to(torch.bfloat16)
     y = ops.linear(x, w, tile_cfg=cfg)
@@ -198,3 +198,26 @@ def test_image_to_nhwc_and_gather():
     exp = torch.zeros(5, 64, dtype=torch.int32)
     exp[0], exp[1], exp[2] = rows[2], rows[0], rows[3]
     assert torch.equal(dst.cpu(), exp)
+
+
+@pytest.mark.parametrize("cfg", list(range(8)))
+def test_linear_all_tiles_random(cfg):
+    ops = _ops()
+    torch.manual_seed(11)
+    x = torch.randn(300, 520, device="cuda", dtype=torch.bfloat16)
+    w = torch.randn(392, 520, device="cuda", dtype=torch.bfloat16) * 0.05
+    b = torch.randn(392, device="cuda", dtype=torch.bfloat16)
+    r = torch.randn(300, 392, device="cuda", dtype=torch.bfloat16)
+    _close(ops.linear(x, w, b, act="gelu", residual=r, tile_cfg=cfg),
+           ops.linear_ref(x, w, b, act="gelu", residual=r), 3e-2, 2e-2)
+
+
+@pytest.mark.parametrize("cfg", list(range(8)))
+def test_conv_all_tiles(cfg):
+    ops = _ops()
+    torch.manual_seed(12)
+    x = torch.randn(2, 20, 20, 48, device="cuda", dtype=torch.float16)
+    w = torch.randn(200, 3, 3, 48, device="cuda", dtype=torch.float16) * 0.07
+    b = torch.randn(200, device="cuda", dtype=torch.float16) * 0.1
+    _close(ops.conv2d_nhwc(x, w, b, stride=1, pad=1, act="relu", tile_cfg=cfg),
+           ops.conv2d_nhwc_ref(x, w, b, stride=1, pad=1, act="relu"), 2e-2, 2e-2)
