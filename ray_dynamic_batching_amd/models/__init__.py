@@ -1,0 +1,58 @@
+"""Model zoo of the serving stack (random init, synthetic inputs; no downloads).
+
+Every model follows the *servable* contract used by the replica engine:
+``input_shape``, ``input_dtype``, ``output_shape``, ``output_dtype`` per request
+and ``forward(x[B, *input_shape]) -> y[B, *output_shape]``.
+
+| name            | reference use                                    | module        |
+|-----------------|--------------------------------------------------|---------------|
+| mlp             | BASELINE config 1 (CPU plumbing)                 | mlp.py        |
+| bert-base       | north-star metric (seq128, bf16)                 | bert.py       |
+| resnet50        | fork registry / profiles, BASELINE config 2      | resnet.py     |
+| vit-b16         | fork registry (scheduler.py:41)                  | vit.py        |
+| shufflenet-v2   | fork registry (scheduler.py:42)                  | shufflenet.py |
+| efficientnet-v2s| fork profile (efficientnetv2_* csv)              | efficientnet.py |
+| llama3-8b (TP)  | BASELINE config 4                                | llama.py      |
+"""
+from __future__ import annotations
+
+from typing import Callable, Dict
+
+REGISTRY: Dict[str, Callable] = {}
+
+
+def register(name: str):
+    def deco(fn):
+        REGISTRY[name] = fn
+        return fn
+    return deco
+
+
+def create(name: str, **kw):
+    _load_all()
+    if name not in REGISTRY:
+        raise KeyError(f"unknown model {name!r}; known: {sorted(REGISTRY)}")
+    return REGISTRY[name](**kw)
+
+
+def _load_all():
+    from . import bert, mlp  # noqa: F401
+    for mod in ("resnet", "vit", "shufflenet", "efficientnet", "llama"):
+        try:
+            __import__(f"{__name__}.{mod}")
+        except ImportError:  # pragma: no cover
+            pass
+
+
+@register("mlp")
+def _mlp(**kw):
+    from .mlp import MLP
+
+    return MLP(**kw)
+
+
+@register("bert-base")
+def _bert(device="cuda", backend="hip", seq_len=128, layers=12, **kw):
+    from .bert import BertConfig, BertForSequenceClassification
+
+    return BertForSequenceClassification(BertConfig(seq_len=seq_len, layers=layers), device=device, backend=backend, **kw)

@@ -101,6 +101,8 @@ class JobHandle {
     s->status.store(status, std::memory_order_release);
   }
   uint32_t replica_status(uint32_t r) { check_r(r); return job_.replica(r)->status.load(); }
+  uint32_t replica_generation(uint32_t r) { check_r(r); return job_.replica(r)->restarts.load(); }
+  uint32_t queue_replica(uint32_t q) { check_q(q); return job_.queue(q)->replica.load(); }
   void heartbeat(uint32_t r) { check_r(r); job_.replica(r)->heartbeat_ns.store(now_ns()); }
   double heartbeat_age_s(uint32_t r) {
     check_r(r);
@@ -261,15 +263,18 @@ class Client {
   int choose_queue(uint32_t model) {
     JobHeader* h = job_.hdr();
     cand_.clear();
+    int serving = 0;
     for (uint32_t q = 0; q < h->n_queues; ++q) {
       QueueState* s = job_.queue(q);
       if (!s->active.load(std::memory_order_acquire) || s->model.load() != model) continue;
+      ++serving;
       const uint32_t r = s->replica.load();
       if (r < h->n_replicas && job_.replica(r)->status.load(std::memory_order_relaxed) != RS_READY) continue;
       cand_.push_back(q);
     }
     const size_t n = cand_.size();
-    if (n == 0) return -2;
+    if (serving == 0) return -2;  // no queue serves this model at all
+    if (n == 0) return -1;        // queues exist but no replica is ready (starting / restarting)
     auto depth = [&](uint32_t q) {
       QueueState* s = job_.queue(q);
       return (int64_t)(s->submitted.load(std::memory_order_relaxed) - s->completed.load(std::memory_order_relaxed));
@@ -544,6 +549,10 @@ class Consumer {
       s->t_aux_ns = now_ns();
       if (!p.empty()) memcpy(c.payload(s), p.data(), p.size());
       QueueState* qs = job_.queue(queue);
+      if (kind == 2) {  // streaming item: not a terminal completion
+        c.publish(s, pos);
+        return fits;
+      }
       qs->completed.fetch_add(1, std::memory_order_relaxed);
       if (status == ST_DROPPED_STALE) qs->dropped.fetch_add(1, std::memory_order_relaxed);
       else if (status != ST_OK) qs->errors.fetch_add(1, std::memory_order_relaxed);
@@ -604,6 +613,8 @@ PYBIND11_MODULE(_rdb_runtime, m) {
       .def("set_replica_status", &JobHandle::set_replica_status, py::arg("replica"),
            py::arg("status"), py::arg("gpu") = -1, py::arg("pid") = 0)
       .def("replica_status", &JobHandle::replica_status)
+      .def("replica_generation", &JobHandle::replica_generation)
+      .def("queue_replica", &JobHandle::queue_replica)
       .def("heartbeat", &JobHandle::heartbeat)
       .def("heartbeat_age_s", &JobHandle::heartbeat_age_s)
       .def("bump_restarts", &JobHandle::bump_restarts)

@@ -1,0 +1,127 @@
+"""Deployment configuration schema, field names kept compatible with Ray Serve
+(reference: serve/_private/config.py:81-170 DeploymentConfig, serve/config.py:33-78
+AutoscalingConfig, serve/_private/constants.py:107-110 health-check defaults),
+plus the Nexus fields of the fork (SLO-aware planning: ``slo_ms``,
+``profile_csv``, ``priority``) and the MI355X engine knobs."""
+from __future__ import annotations
+
+from typing import Any, Dict, List, Optional, Union
+
+from pydantic import BaseModel, Field, field_validator, model_validator
+
+DEFAULT_MAX_ONGOING_REQUESTS = 5
+DEFAULT_HEALTH_CHECK_PERIOD_S = 10.0
+DEFAULT_HEALTH_CHECK_TIMEOUT_S = 30.0
+DEFAULT_HEALTH_CHECK_FAILURE_THRESHOLD = 3
+DEFAULT_GRACEFUL_SHUTDOWN_WAIT_LOOP_S = 2.0
+DEFAULT_GRACEFUL_SHUTDOWN_TIMEOUT_S = 20.0
+CONTROL_LOOP_INTERVAL_S = 0.1
+
+
+class AutoscalingConfig(BaseModel):
+    """Queue-length autoscaling (serve/config.py:33-78)."""
+    min_replicas: int = 1
+    initial_replicas: Optional[int] = None
+    max_replicas: int = 1
+    target_ongoing_requests: float = 2.0
+    metrics_interval_s: float = 10.0
+    look_back_period_s: float = 30.0
+    smoothing_factor: float = 1.0
+    upscale_smoothing_factor: Optional[float] = None
+    downscale_smoothing_factor: Optional[float] = None
+    upscaling_factor: Optional[float] = None
+    downscaling_factor: Optional[float] = None
+    downscale_delay_s: float = 600.0
+    upscale_delay_s: float = 30.0
+
+    @model_validator(mode="after")
+    def _check(self):
+        if self.min_replicas < 0:
+            raise ValueError("min_replicas must be >= 0")
+        if self.max_replicas < max(1, self.min_replicas):
+            raise ValueError("max_replicas must be >= max(1, min_replicas)")
+        if self.initial_replicas is not None and not (self.min_replicas <= self.initial_replicas <= self.max_replicas):
+            raise ValueError("initial_replicas must be within [min_replicas, max_replicas]")
+        if self.target_ongoing_requests <= 0:
+            raise ValueError("target_ongoing_requests must be > 0")
+        return self
+
+    def get_upscaling_factor(self) -> float:
+        return self.upscaling_factor or self.upscale_smoothing_factor or self.smoothing_factor
+
+    def get_downscaling_factor(self) -> float:
+        return self.downscaling_factor or self.downscale_smoothing_factor or self.smoothing_factor
+
+
+class EngineConfig(BaseModel):
+    """MI355X replica-engine knobs for servable (natively executed) models."""
+    buckets: Optional[List[int]] = None          # padded batch sizes captured as hipGraphs
+    pipeline_depth: int = 2                      # batches in flight (H2D of k+1 under compute of k)
+    zero_copy: bool = True                       # GPU gathers payloads straight from pinned shm
+    request_slot_bytes: Optional[int] = None     # per-request payload bytes (default: model input size)
+
+
+class DeploymentConfig(BaseModel):
+    name: str = ""
+    num_replicas: Union[int, str, None] = 1
+    max_ongoing_requests: int = DEFAULT_MAX_ONGOING_REQUESTS
+    max_queued_requests: int = -1
+    user_config: Optional[Any] = None
+    autoscaling_config: Optional[AutoscalingConfig] = None
+    graceful_shutdown_wait_loop_s: float = DEFAULT_GRACEFUL_SHUTDOWN_WAIT_LOOP_S
+    graceful_shutdown_timeout_s: float = DEFAULT_GRACEFUL_SHUTDOWN_TIMEOUT_S
+    health_check_period_s: float = DEFAULT_HEALTH_CHECK_PERIOD_S
+    health_check_timeout_s: float = DEFAULT_HEALTH_CHECK_TIMEOUT_S
+    health_check_failure_threshold: int = DEFAULT_HEALTH_CHECK_FAILURE_THRESHOLD
+    ray_actor_options: Dict[str, Any] = Field(default_factory=dict)
+    placement_group_bundles: Optional[List[Dict[str, float]]] = None
+    placement_group_strategy: Optional[str] = None
+    max_replicas_per_node: Optional[int] = None
+    logging_config: Optional[Dict[str, Any]] = None
+    # Nexus / fork extensions
+    slo_ms: Optional[float] = None
+    profile_csv: Optional[str] = None
+    priority: int = 0
+    drop_stale: bool = False
+    engine: EngineConfig = Field(default_factory=EngineConfig)
+
+    @field_validator("max_ongoing_requests")
+    @classmethod
+    def _pos(cls, v):
+        if v <= 0:
+            raise ValueError("max_ongoing_requests must be > 0")
+        return v
+
+    @field_validator("max_queued_requests")
+    @classmethod
+    def _queued(cls, v):
+        if v != -1 and v <= 0:
+            raise ValueError("max_queued_requests must be -1 (no limit) or > 0")
+        return v
+
+    @model_validator(mode="after")
+    def _replicas(self):
+        if self.num_replicas == "auto":
+            if self.autoscaling_config is None:
+                self.autoscaling_config = AutoscalingConfig(min_replicas=1, max_replicas=8, initial_replicas=1)
+        elif self.num_replicas is not None:
+            if not isinstance(self.num_replicas, int) or self.num_replicas < 0:
+                raise ValueError("num_replicas must be a non-negative int or 'auto'")
+            if self.autoscaling_config is not None and self.num_replicas not in (None, 1):
+                raise ValueError("num_replicas and autoscaling_config cannot both be set")
+        g = self.ray_actor_options.get("num_gpus", 0)
+        if not isinstance(g, (int, float)) or g < 0:
+            raise ValueError("ray_actor_options.num_gpus must be a non-negative number")
+        if g > 1 and g != int(g):
+            raise ValueError("fractional num_gpus must be < 1")
+        return self
+
+    def initial_num_replicas(self) -> int:
+        if self.autoscaling_config is not None:
+            a = self.autoscaling_config
+            return a.initial_replicas if a.initial_replicas is not None else a.min_replicas
+        return int(self.num_replicas or 0)
+
+    @property
+    def num_gpus(self) -> float:
+        return float(self.ray_actor_options.get("num_gpus", 0) or 0)

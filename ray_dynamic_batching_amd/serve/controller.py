@@ -1,0 +1,544 @@
+"""Serve controller + node agent (single node, in the driver process).
+
+Reference parity:
+* ServeController control loop every 0.1 s (serve/_private/controller.py:370-471):
+  deployment state update, health checks, autoscaling;
+* DeploymentState replica state machine (deployment_state.py): start, health-check,
+  restart dead replicas, scale up/down, graceful drain;
+* raylet worker pool + GPU allocation (node_manager / worker_pool /
+  resource_instance_set.cc): replica PROCESSES pinned to GPUs with
+  HIP_VISIBLE_DEVICES, GPU slots from runtime.resources.GpuAllocator;
+* GCS health checks / actor restarts (gcs_health_check_manager.cc): heartbeats
+  in the shm job segment, exponential restart back-off;
+* config checkpoint (controller.py:510-563 KV): the last applied application
+  config is written to a JSON KV file and can be restored.
+"""
+from __future__ import annotations
+
+import atexit
+import json
+import logging
+import os
+import subprocess
+import sys
+import tempfile
+import threading
+import time
+import traceback
+from dataclasses import dataclass, field
+from typing import Any, Dict, List, Optional, Tuple
+
+from .api import Application, Deployment
+from .autoscaling_policy import AutoscalingState
+from .config import CONTROL_LOOP_INTERVAL_S, DeploymentConfig
+from .exceptions import RayServeException
+from .handle import DeploymentHandle
+from .router import LocalRouter, ShmRouter
+from .replica import LocalReplica
+
+logger = logging.getLogger("ray_dynamic_batching_amd.serve")
+
+_CONTROLLER: Optional["ServeController"] = None
+_CTRL_LOCK = threading.Lock()
+
+
+def get_controller(create: bool = True) -> Optional["ServeController"]:
+    global _CONTROLLER
+    with _CTRL_LOCK:
+        if _CONTROLLER is None and create:
+            _CONTROLLER = ServeController()
+        return _CONTROLLER
+
+
+def lookup_router(app_name: str, deployment: str):
+    """Router for a handle: the controller in the driver, the routing table in
+    a replica process (handles shipped for composition)."""
+    table = os.environ.get("RDB_ROUTING_TABLE")
+    if table and _CONTROLLER is None:
+        with open(table) as f:
+            routes = json.load(f)
+        r = routes.get(f"{app_name}/{deployment}")
+        if r is None:
+            raise RayServeException(f"no route for {app_name}/{deployment}")
+        codec = None
+        if r.get("codec"):
+            from .servable import TensorCodec
+            import torch
+
+            c = r["codec"]
+            codec = TensorCodec(c["input_shape"], getattr(torch, c["input_dtype"]), c["output_shape"],
+                                getattr(torch, c["output_dtype"]))
+        return ShmRouter(r["job"], r["model_id"], deployment, r.get("max_queued", -1), codec)
+    ctrl = get_controller(create=False)
+    if ctrl is None:
+        raise RayServeException("serve is not running; call serve.run() first")
+    return ctrl.router_for(app_name, deployment)
+
+
+@dataclass
+class ProcReplica:
+    slot: int                 # replica index in the job segment (== queue id)
+    proc: Optional[subprocess.Popen] = None
+    alloc: Any = None
+    started_at: float = 0.0
+    ready: bool = False
+    restarts: int = 0
+    next_restart_at: float = 0.0
+    health_failures: int = 0
+    draining: bool = False
+
+
+@dataclass
+class DeploymentState:
+    app_name: str
+    name: str
+    deployment: Deployment
+    app: Application
+    config: DeploymentConfig
+    mode: str
+    model_id: int = 0
+    router: Any = None
+    target: int = 1
+    local_replicas: List[LocalReplica] = field(default_factory=list)
+    proc_replicas: List[ProcReplica] = field(default_factory=list)
+    autoscaler: Optional[AutoscalingState] = None
+    init_args: tuple = ()
+    init_kwargs: dict = field(default_factory=dict)
+    next_index: int = 0
+    codec: Any = None
+    spec_path: str = ""
+    slots: List[int] = field(default_factory=list)   # job replica slots reserved for this deployment
+
+
+class ServeController:
+    def __init__(self):
+        from ..runtime.resources import GpuAllocator
+
+        self.apps: Dict[str, Dict[str, DeploymentState]] = {}
+        self.ingress: Dict[str, str] = {}
+        self.jobs: Dict[str, Any] = {}            # app -> job segment handle (process mode)
+        self.allocator = GpuAllocator()
+        self.lock = threading.RLock()
+        self.workdir = tempfile.mkdtemp(prefix="rdb_serve_")
+        self.kv_path = os.environ.get("RDB_SERVE_KV", os.path.join(self.workdir, "serve_kv.json"))
+        self.default_mode = os.environ.get("RDB_SERVE_MODE", "auto")
+        self._stop = threading.Event()
+        self._thread = threading.Thread(target=self._control_loop, name="rdb-serve-controller", daemon=True)
+        self._thread.start()
+        atexit.register(self.shutdown)
+
+    def configure(self, mode: str = None, **_):
+        if mode:
+            self.default_mode = mode
+
+    # ------------------------------------------------------------------ deploy
+    def _resolve_mode(self, app: Application, mode: Optional[str]) -> str:
+        mode = mode or self.default_mode
+        if mode in ("local", "process"):
+            return mode
+        wants_gpu = any(a.deployment.config.num_gpus > 0 for a in app.walk())
+        return "process" if wants_gpu else "local"
+
+    def deploy_application(self, app: Application, name: str = "default", route_prefix: Optional[str] = "/",
+                           mode: Optional[str] = None) -> DeploymentHandle:
+        with self.lock:
+            if name in self.apps:
+                self.delete_application(name)
+            mode = self._resolve_mode(app, mode)
+            graph = app.walk()
+            names = [a.deployment.name for a in graph]
+            if len(set(names)) != len(names):
+                raise RayServeException(f"duplicate deployment names in application {name!r}: {names}")
+            states: Dict[str, DeploymentState] = {}
+            self.apps[name] = states
+            self.ingress[name] = app.deployment.name
+            if mode == "process":
+                self._create_job(name, graph)
+            for mid, a in enumerate(graph):
+                d = a.deployment
+                cfg = d.config
+                st = DeploymentState(name, d.name, d, a, cfg, mode, model_id=mid)
+                st.target = cfg.initial_num_replicas()
+                if cfg.autoscaling_config is not None:
+                    st.autoscaler = AutoscalingState(cfg.autoscaling_config)
+                # composition: bound Applications become handles
+                st.init_args = tuple(self._to_handle(name, x) for x in a.init_args)
+                st.init_kwargs = {k: self._to_handle(name, v) for k, v in a.init_kwargs.items()}
+                if mode == "local":
+                    st.router = LocalRouter(d.name, cfg.max_queued_requests)
+                else:
+                    self._prepare_process_deployment(st)
+                states[d.name] = st
+            if mode == "process":
+                self._write_routing_table(name)
+            for st in states.values():
+                self._reconcile(st, wait=True)
+            self._checkpoint()
+            return DeploymentHandle(app.deployment.name, name)
+
+    def _to_handle(self, app_name: str, x):
+        if isinstance(x, Application):
+            return DeploymentHandle(x.deployment.name, app_name)
+        return x
+
+    # --- process mode plumbing ------------------------------------------------
+    def _max_replicas(self, cfg: DeploymentConfig) -> int:
+        if cfg.autoscaling_config is not None:
+            return cfg.autoscaling_config.max_replicas
+        return max(1, int(cfg.num_replicas or 1))
+
+    def _create_job(self, app_name: str, graph: List[Application]) -> None:
+        from ..runtime import job as rjob
+
+        n = sum(self._max_replicas(a.deployment.config) for a in graph)
+        req_bytes, cmp_bytes = 64 * 1024, 64 * 1024
+        for a in graph:
+            sv = getattr(a.deployment, "servable", None)
+            if a.deployment.config.engine.request_slot_bytes:
+                req_bytes = max(req_bytes, a.deployment.config.engine.request_slot_bytes)
+        jname = f"serve_{os.getpid()}_{app_name}_{int(time.time() * 1000) % 10**8}"
+        job = rjob.Job(jname, create=True, n_replicas=n, n_queues=n, n_clients=16 + n, req_capacity=1024,
+                       req_slot_bytes=req_bytes, cmp_capacity=4096, cmp_slot_bytes=cmp_bytes)
+        self.jobs[app_name] = job
+
+    def _prepare_process_deployment(self, st: DeploymentState) -> None:
+        import cloudpickle
+
+        job = self.jobs[st.app_name]
+        used = sum(len(s.slots) for s in self.apps[st.app_name].values())
+        st.slots = list(range(used, used + self._max_replicas(st.config)))
+        sv = getattr(st.deployment, "servable", None)
+        spec = dict(app_name=st.app_name, deployment=st.name, func_or_class=st.deployment.func_or_class,
+                    init_args=st.init_args, init_kwargs=st.init_kwargs, config=st.config.model_dump(),
+                    job=job.info()["name"], model_id=st.model_id, servable=sv)
+        st.spec_path = os.path.join(self.workdir, f"{st.app_name}.{st.name}.spec.pkl")
+        with open(st.spec_path, "wb") as f:
+            cloudpickle.dump(spec, f)
+        if sv is not None:
+            st.codec = _codec_for_servable(sv)
+        st.router = ShmRouter(job.info()["name"], st.model_id, st.name, st.config.max_queued_requests, st.codec)
+
+    def _write_routing_table(self, app_name: str) -> None:
+        routes = {}
+        for st in self.apps[app_name].values():
+            r = dict(job=self.jobs[app_name].info()["name"], model_id=st.model_id,
+                     max_queued=st.config.max_queued_requests)
+            if st.codec is not None:
+                c = st.codec
+                r["codec"] = dict(input_shape=list(c.input_shape), output_shape=list(c.output_shape),
+                                  input_dtype=str(_torch_dtype_name(c.in_np)), output_dtype=str(_torch_dtype_name(c.out_np)))
+            routes[f"{app_name}/{st.name}"] = r
+        path = os.path.join(self.workdir, f"{app_name}.routes.json")
+        with open(path, "w") as f:
+            json.dump(routes, f)
+        self._routes_path = path
+
+    def _spawn(self, st: DeploymentState, rep: ProcReplica) -> bool:
+        from ..runtime.resources import visible_devices_env
+
+        owner = f"{st.app_name}#{st.name}#{rep.slot}"
+        self.allocator.release(owner)
+        alloc = self.allocator.allocate(owner, st.config.num_gpus)
+        if alloc is None:
+            logger.warning("no GPU capacity for %s (num_gpus=%s)", owner, st.config.num_gpus)
+            return False
+        rep.alloc = alloc
+        job = self.jobs[st.app_name]
+        job.configure_queue(rep.slot, rep.slot, st.model_id, st.config.max_ongoing_requests,
+                            float(st.config.slo_ms or 0.0), True)
+        job.set_replica_status(rep.slot, 1, alloc.gpus[0] if alloc.gpus else -1, 0)
+        env = dict(os.environ)
+        env.update(visible_devices_env(alloc.gpus))
+        env["RDB_ROUTING_TABLE"] = self._routes_path
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        pkg_root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        env["PYTHONPATH"] = pkg_root + os.pathsep + env.get("PYTHONPATH", "")
+        cmd = [sys.executable, "-m", "ray_dynamic_batching_amd.serve.replica_main", "--spec", st.spec_path,
+               "--replica", str(rep.slot), "--gpu", ",".join(map(str, alloc.gpus))]
+        log = open(os.path.join(self.workdir, f"{owner.replace('#', '.')}.log"), "ab")
+        rep.proc = subprocess.Popen(cmd, env=env, stdout=log, stderr=subprocess.STDOUT)
+        rep.started_at = time.time()
+        rep.ready = False
+        rep.health_failures = 0
+        return True
+
+    # ------------------------------------------------------------- reconcile
+    def _reconcile(self, st: DeploymentState, wait: bool = False) -> None:
+        if st.mode == "local":
+            self._reconcile_local(st)
+        else:
+            self._reconcile_process(st, wait)
+
+    def _reconcile_local(self, st: DeploymentState) -> None:
+        alive = [r for r in st.local_replicas if not r.dead]
+        changed = False
+        while len(alive) < st.target:
+            idx = st.next_index
+            st.next_index += 1
+            r = LocalReplica(st.app_name, st.name, idx, st.deployment.func_or_class, st.init_args, st.init_kwargs,
+                             st.config)
+            alive.append(r)
+            changed = True
+        while len(alive) > st.target:
+            victim = min(alive, key=lambda r: r.ongoing)
+            alive.remove(victim)
+            threading.Thread(target=victim.shutdown, args=(st.config.graceful_shutdown_timeout_s,), daemon=True).start()
+            changed = True
+        st.local_replicas = alive
+        if changed:
+            st.router.update_replicas(alive)
+
+    def _reconcile_process(self, st: DeploymentState, wait: bool) -> None:
+        job = self.jobs[st.app_name]
+        live = [r for r in st.proc_replicas if not r.draining]
+        now = time.time()
+        while len(live) < st.target:
+            used = {r.slot for r in st.proc_replicas}
+            free = [s for s in st.slots if s not in used]
+            if not free:
+                break
+            rep = ProcReplica(free[0])
+            st.proc_replicas.append(rep)
+            live.append(rep)
+            self._spawn(st, rep)
+        while len(live) > st.target:
+            victim = live.pop()
+            self._drain(st, victim)
+        if wait:
+            deadline = now + float(os.environ.get("RDB_REPLICA_START_TIMEOUT_S", "900"))
+            for rep in live:
+                while time.time() < deadline:
+                    if job.replica_status(rep.slot) == 2:
+                        rep.ready = True
+                        break
+                    if rep.proc is not None and rep.proc.poll() is not None:
+                        raise RayServeException(f"replica {st.name}#{rep.slot} exited during startup "
+                                                f"(code {rep.proc.returncode}); log: {self.workdir}")
+                    time.sleep(0.02)
+                else:
+                    raise RayServeException(f"replica {st.name}#{rep.slot} did not become ready")
+        st.router.update_replicas(None)
+
+    def _drain(self, st: DeploymentState, rep: ProcReplica) -> None:
+        """Graceful drain: stop routing (queue inactive), let in-flight finish, SIGTERM."""
+        job = self.jobs[st.app_name]
+        rep.draining = True
+        job.configure_queue(rep.slot, rep.slot, st.model_id, st.config.max_ongoing_requests, 0.0, False)
+
+        def _finish():
+            deadline = time.time() + st.config.graceful_shutdown_timeout_s
+            while time.time() < deadline and job.queue_depth(rep.slot) > 0:
+                time.sleep(st.config.graceful_shutdown_wait_loop_s / 20)
+            if rep.proc is not None and rep.proc.poll() is None:
+                rep.proc.terminate()
+                try:
+                    rep.proc.wait(5)
+                except subprocess.TimeoutExpired:
+                    rep.proc.kill()
+            job.fail_queue(rep.slot, 6)
+            job.set_replica_status(rep.slot, 4, -1, 0)
+            self.allocator.release(f"{st.app_name}#{st.name}#{rep.slot}")
+            with self.lock:
+                if rep in st.proc_replicas:
+                    st.proc_replicas.remove(rep)
+        threading.Thread(target=_finish, daemon=True).start()
+
+    # ------------------------------------------------------------ control loop
+    def _control_loop(self) -> None:
+        last_health: Dict[Tuple[str, str], float] = {}
+        while not self._stop.wait(CONTROL_LOOP_INTERVAL_S):
+            try:
+                with self.lock:
+                    for app_name, states in list(self.apps.items()):
+                        for st in states.values():
+                            self._health_tick(st, last_health)
+                            self._autoscale_tick(st)
+            except Exception:  # pragma: no cover
+                logger.error("controller loop error:\n%s", traceback.format_exc())
+
+    def _health_tick(self, st: DeploymentState, last: Dict) -> None:
+        now = time.time()
+        if st.mode == "local":
+            key = (st.app_name, st.name)
+            if now - last.get(key, 0) < st.config.health_check_period_s:
+                return
+            last[key] = now
+            changed = False
+            for r in list(st.local_replicas):
+                if not r.check_health(st.config.health_check_timeout_s):
+                    r.health_failures = getattr(r, "health_failures", 0) + 1
+                    if r.health_failures >= st.config.health_check_failure_threshold:
+                        logger.warning("replica %s unhealthy; replacing", r.replica_id)
+                        r.shutdown(0)
+                        st.local_replicas.remove(r)
+                        changed = True
+                else:
+                    r.health_failures = 0
+            if changed:
+                self._reconcile_local(st)
+            return
+        job = self.jobs.get(st.app_name)
+        if job is None:
+            return
+        for rep in list(st.proc_replicas):
+            if rep.draining:
+                continue
+            status = job.replica_status(rep.slot)
+            if status == 2:
+                rep.ready = True
+            died = rep.proc is not None and rep.proc.poll() is not None
+            stale = rep.ready and job.heartbeat_age_s(rep.slot) > st.config.health_check_timeout_s
+            if died or stale or status == 4:
+                if rep.next_restart_at == 0.0:
+                    logger.warning("replica %s#%d %s; restarting", st.name, rep.slot,
+                                   "died" if died else "missed heartbeats")
+                    if rep.proc is not None and rep.proc.poll() is None:
+                        rep.proc.kill()
+                    job.set_replica_status(rep.slot, 4, -1, 0)
+                    job.fail_queue(rep.slot, 6)   # REPLICA_DIED -> clients retry elsewhere
+                    job.bump_restarts(rep.slot)
+                    rep.restarts += 1
+                    backoff = min(30.0, 0.5 * (2 ** min(rep.restarts - 1, 6)))
+                    rep.next_restart_at = now + backoff
+                    rep.ready = False
+                elif now >= rep.next_restart_at:
+                    rep.next_restart_at = 0.0
+                    self._spawn(st, rep)
+
+    def _autoscale_tick(self, st: DeploymentState) -> None:
+        if st.autoscaler is None:
+            return
+        if st.mode == "local":
+            total = st.router.total_ongoing()
+            running = len(st.local_replicas)
+        else:
+            job = self.jobs[st.app_name]
+            live = [r for r in st.proc_replicas if not r.draining]
+            total = sum(job.queue_depth(r.slot) for r in live) + st.router.num_queued()
+            running = sum(1 for r in live if r.ready)
+        new_target = st.autoscaler.step(total, running, st.target)
+        if new_target != st.target:
+            logger.info("autoscaling %s: %d -> %d (ongoing=%s)", st.name, st.target, new_target, total)
+            st.target = new_target
+            self._reconcile(st, wait=False)
+
+    # ------------------------------------------------------------ queries
+    def router_for(self, app_name: str, deployment: str):
+        with self.lock:
+            states = self.apps.get(app_name)
+            if not states or deployment not in states:
+                raise RayServeException(f"deployment {deployment!r} not found in application {app_name!r}")
+            return states[deployment].router
+
+    def get_app_handle(self, name: str) -> DeploymentHandle:
+        if name not in self.ingress:
+            raise RayServeException(f"application {name!r} not found")
+        return DeploymentHandle(self.ingress[name], name)
+
+    def get_deployment_handle(self, deployment: str, app_name: Optional[str] = None) -> DeploymentHandle:
+        if app_name is None:
+            matches = [a for a, s in self.apps.items() if deployment in s]
+            if len(matches) != 1:
+                raise RayServeException(f"deployment {deployment!r} is ambiguous or missing; pass app_name")
+            app_name = matches[0]
+        self.router_for(app_name, deployment)
+        return DeploymentHandle(deployment, app_name)
+
+    def status(self) -> Dict[str, Any]:
+        out = {"applications": {}}
+        with self.lock:
+            for app_name, states in self.apps.items():
+                deps = {}
+                for st in states.values():
+                    if st.mode == "local":
+                        reps = [r.stats() for r in st.local_replicas]
+                        healthy = sum(1 for r in st.local_replicas if not r.dead)
+                    else:
+                        job = self.jobs[app_name]
+                        reps = []
+                        for r in st.proc_replicas:
+                            s = job.replica_stats(r.slot)
+                            s.update(slot=r.slot, draining=r.draining, queue=job.queue_stats(r.slot))
+                            reps.append(s)
+                        healthy = sum(1 for r in st.proc_replicas if r.ready and not r.draining)
+                    status = "HEALTHY" if healthy >= st.target else ("UPDATING" if healthy > 0 else "UNHEALTHY")
+                    deps[st.name] = dict(status=status, target_replicas=st.target, running_replicas=healthy,
+                                         mode=st.mode, replicas=reps)
+                out["applications"][app_name] = dict(status="RUNNING", ingress=self.ingress[app_name],
+                                                     deployments=deps)
+        return out
+
+    # ------------------------------------------------------------ teardown
+    def delete_application(self, name: str) -> None:
+        with self.lock:
+            states = self.apps.pop(name, None)
+            self.ingress.pop(name, None)
+            if not states:
+                return
+            for st in states.values():
+                for r in st.local_replicas:
+                    r.shutdown(st.config.graceful_shutdown_timeout_s)
+                for rep in st.proc_replicas:
+                    if rep.proc is not None and rep.proc.poll() is None:
+                        rep.proc.terminate()
+                for rep in st.proc_replicas:
+                    if rep.proc is not None:
+                        try:
+                            rep.proc.wait(10)
+                        except subprocess.TimeoutExpired:
+                            rep.proc.kill()
+                    self.allocator.release(f"{st.app_name}#{st.name}#{rep.slot}")
+            job = self.jobs.pop(name, None)
+            if job is not None:
+                from .router import ShmRouter
+
+                hub = ShmRouter._clients.pop(job.info()["name"], None)
+                job.set_shutdown(True)
+                if hub is not None:
+                    hub.close()
+                job.close()
+            self._checkpoint()
+
+    def shutdown(self) -> None:
+        global _CONTROLLER
+        for name in list(self.apps):
+            try:
+                self.delete_application(name)
+            except Exception:  # pragma: no cover
+                logger.error("error deleting %s:\n%s", name, traceback.format_exc())
+        self._stop.set()
+        with _CTRL_LOCK:
+            if _CONTROLLER is self:
+                _CONTROLLER = None
+
+    # ------------------------------------------------------------ checkpoint
+    def _checkpoint(self) -> None:
+        """Persist the applied config (reference: controller KV checkpoint)."""
+        data = {}
+        for app_name, states in self.apps.items():
+            data[app_name] = dict(ingress=self.ingress.get(app_name),
+                                  deployments={n: st.config.model_dump(mode="json") for n, st in states.items()})
+        try:
+            tmp = self.kv_path + ".tmp"
+            with open(tmp, "w") as f:
+                json.dump(dict(version=1, time=time.time(), applications=data), f, default=str)
+            os.replace(tmp, self.kv_path)
+        except OSError:  # pragma: no cover
+            pass
+
+
+def _codec_for_servable(sv) -> Any:
+    """Build the tensor codec from the model's declared I/O (cheap: metadata only)."""
+    from .servable import TensorCodec
+
+    spec = getattr(sv["factory"], "io_spec", None)
+    if spec is None:
+        return None
+    return TensorCodec(*spec)
+
+
+def _torch_dtype_name(np_dtype) -> str:
+    import numpy as np
+
+    return {np.int32: "int32", np.int64: "int64", np.float32: "float32", np.float16: "float16",
+            np.uint8: "uint8"}[np_dtype]

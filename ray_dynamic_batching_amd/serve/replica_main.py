@@ -1,0 +1,197 @@
+"""Entry point of a replica PROCESS (one per GPU slot), spawned by the controller.
+
+    python -m ray_dynamic_batching_amd.serve.replica_main --spec S --replica R --gpu G
+
+* servable-model deployments -> the native replica engine (no Python on the
+  request path);
+* any other deployment -> a Python worker: a reader thread pops requests from
+  the shm ring (GIL released while waiting), the user-code event loop runs the
+  calls (``@serve.batch`` batches them), results go back through the
+  completion ring.  Streaming methods send one completion per item.
+* a heartbeat thread refreshes the replica's shm heartbeat; the user's
+  ``check_health`` runs every ``health_check_period_s``; SIGTERM drains.
+"""
+from __future__ import annotations
+
+import argparse
+import asyncio
+import logging
+import os
+import signal
+import sys
+import threading
+import time
+import traceback
+
+logger = logging.getLogger("ray_dynamic_batching_amd.replica")
+
+KIND_TENSOR, KIND_PICKLE, KIND_STREAM_ITEM, KIND_STREAM_END = 0, 1, 2, 3
+ST_OK, ST_DROPPED, ST_ERROR = 0, 1, 2
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--spec", required=True)
+    ap.add_argument("--replica", type=int, required=True)
+    ap.add_argument("--gpu", default="")
+    a = ap.parse_args(argv)
+    logging.basicConfig(level=os.environ.get("RDB_LOG_LEVEL", "INFO"),
+                        format=f"%(asctime)s replica{a.replica} %(levelname)s %(message)s")
+    import cloudpickle
+
+    with open(a.spec, "rb") as f:
+        spec = cloudpickle.load(f)
+    from ..runtime import job as rjob
+    from .config import DeploymentConfig
+    from .context import ReplicaContext, _set_replica_context
+
+    cfg = DeploymentConfig(**spec["config"])
+    job = rjob.Job(spec["job"], create=False)
+    r = a.replica
+    gpu = int(a.gpu.split(",")[0]) if a.gpu else -1
+    job.set_replica_status(r, 1, gpu, os.getpid())
+    stop = threading.Event()
+
+    def _term(*_):
+        stop.set()
+    signal.signal(signal.SIGTERM, _term)
+
+    def heartbeat():
+        while not stop.is_set():
+            job.heartbeat(r)
+            time.sleep(0.25)
+    threading.Thread(target=heartbeat, daemon=True).start()
+
+    ctx = ReplicaContext(spec["app_name"], spec["deployment"], f"{spec['app_name']}#{spec['deployment']}#{r}", r,
+                         None, cfg.max_ongoing_requests, gpu)
+    _set_replica_context(ctx)
+    try:
+        if spec.get("servable"):
+            return _run_engine(spec, cfg, job, r, stop)
+        return _run_python(spec, cfg, job, r, stop, ctx)
+    except Exception:
+        logger.error("replica failed:\n%s", traceback.format_exc())
+        job.set_replica_status(r, 4, gpu, os.getpid())
+        return 1
+
+
+def _run_engine(spec, cfg, job, r, stop) -> int:
+    import torch
+
+    from ..runtime.engine import EngineRunner, SessionSpec
+
+    sv = spec["servable"]
+    torch.cuda.set_device(0)
+    factory = sv["factory"]
+    try:
+        model = factory(device="cuda")
+    except TypeError:
+        model = factory()
+    eng = cfg.engine
+    s = SessionSpec(model=model, queue=r, max_batch=sv["max_batch_size"], max_wait_s=sv["batch_wait_timeout_s"],
+                    buckets=eng.buckets, priority=cfg.priority, slo_ms=float(cfg.slo_ms or 0.0),
+                    drop_stale=cfg.drop_stale)
+    runner = EngineRunner(spec["job"], r, [s], pipeline_depth=eng.pipeline_depth, zero_copy=eng.zero_copy).build()
+    runner.start()   # sets the replica READY in shm
+    while not stop.is_set():
+        err = runner.error()
+        if err:
+            logger.error("engine error: %s", err)
+            return 2
+        stop.wait(0.2)
+    runner.stop()
+    return 0
+
+
+def _run_python(spec, cfg, job, r, stop, ctx) -> int:
+    import cloudpickle
+
+    from ..runtime import job as rjob
+    from .handle import RequestMeta
+    from .replica import UserCallable
+
+    loop = asyncio.new_event_loop()
+    asyncio.set_event_loop(loop)
+    user = UserCallable(spec["func_or_class"], spec["init_args"], spec["init_kwargs"], cfg.user_config)
+    ctx.servable_object = user.obj
+    cons = rjob.Consumer(job, [r])
+    inflight = [0]
+
+    async def handle(req):
+        rid, q, client, kind, t_sub, dl, payload = req
+        try:
+            method, args, kwargs, mux, stream, user_rid = cloudpickle.loads(payload)
+            meta = RequestMeta(user_rid, method, mux, stream, spec["app_name"], spec["deployment"])
+            if stream:
+                items = []
+
+                def emit(k, v):
+                    if k == "item":
+                        cons.complete(client, rid, q, ST_OK, t_sub, cloudpickle.dumps(v), KIND_STREAM_ITEM)
+                    elif k == "end":
+                        cons.complete(client, rid, q, ST_OK, t_sub, b"", KIND_STREAM_END)
+                    else:
+                        cons.complete(client, rid, q, ST_ERROR, t_sub, _dump_exc(v), KIND_PICKLE)
+                await user.call_stream(meta, args, kwargs, emit)
+            else:
+                res = await user.call(meta, args, kwargs)
+                if not cons.complete(client, rid, q, ST_OK, t_sub, cloudpickle.dumps(res), KIND_PICKLE):
+                    logger.error("result of request %d too large for the completion slot", rid)
+        except Exception as e:
+            cons.complete(client, rid, q, ST_ERROR, t_sub, _dump_exc(e), KIND_PICKLE)
+        finally:
+            inflight[0] -= 1
+
+    def reader():
+        while not stop.is_set():
+            try:
+                reqs = cons.pop(256, 50_000_000)
+            except Exception:  # pragma: no cover
+                break
+            if reqs:
+                inflight[0] += len(reqs)
+                for req in reqs:
+                    asyncio.run_coroutine_threadsafe(handle(req), loop)
+        loop.call_soon_threadsafe(loop.stop)
+
+    async def health():
+        fails = 0
+        while not stop.is_set():
+            await asyncio.sleep(cfg.health_check_period_s)
+            try:
+                await asyncio.wait_for(user.check_health(), cfg.health_check_timeout_s)
+                fails = 0
+            except Exception:
+                fails += 1
+                logger.warning("check_health failed (%d):\n%s", fails, traceback.format_exc())
+                if fails >= cfg.health_check_failure_threshold:
+                    job.set_replica_status(r, 4, ctx.gpu if ctx.gpu is not None else -1, os.getpid())
+                    stop.set()
+
+    t = threading.Thread(target=reader, daemon=True)
+    job.set_replica_status(r, 2, ctx.gpu if ctx.gpu is not None else -1, os.getpid())
+    t.start()
+    loop.create_task(health())
+    loop.run_forever()
+    t.join(5)
+    # graceful drain of in-flight requests
+    deadline = time.time() + cfg.graceful_shutdown_timeout_s
+    while inflight[0] > 0 and time.time() < deadline:
+        loop.run_until_complete(asyncio.sleep(0.01))
+    user.destroy()
+    return 0
+
+
+def _dump_exc(e: BaseException) -> bytes:
+    import cloudpickle
+
+    try:
+        return cloudpickle.dumps(e)
+    except Exception:
+        from .exceptions import RayServeException
+
+        return cloudpickle.dumps(RayServeException(f"{type(e).__name__}: {e}"))
+
+
+if __name__ == "__main__":
+    sys.exit(main())

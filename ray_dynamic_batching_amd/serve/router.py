@@ -1,0 +1,465 @@
+"""Request routers: power-of-two-choices by queue depth, FIFO pending queue,
+``max_ongoing_requests`` admission, ``max_queued_requests`` back-pressure,
+model-multiplexing affinity, retry on replica death.
+
+Reference: serve/_private/router.py:313-566 and
+replica_scheduler/pow_2_scheduler.py:346-835.  Differences by design:
+* the queue length of a replica is read from memory (local mode) or from two
+  shm atomics (process mode, via the native Client) -- there is no probe RPC,
+  no queue-length cache and no probe back-off to tune;
+* process-mode routing and submission are native (runtime.cpp Client).
+"""
+from __future__ import annotations
+
+import asyncio
+import collections
+import concurrent.futures
+import logging
+import queue as _queue
+import random
+import threading
+import time
+import traceback
+from typing import Any, Callable, Deque, Dict, List, Optional, Tuple
+
+from .exceptions import BackPressureError, DeploymentUnavailableError, RayServeException, ReplicaDiedError
+from .handle import DeploymentResponse, DeploymentResponseGenerator, RequestMeta
+
+logger = logging.getLogger("ray_dynamic_batching_amd.serve")
+
+
+def _has_response_args(args, kwargs) -> bool:
+    return any(isinstance(a, DeploymentResponse) for a in args) or any(
+        isinstance(v, DeploymentResponse) for v in kwargs.values())
+
+
+async def _resolve_args(args, kwargs):
+    """Composition: DeploymentResponse arguments are replaced by their values."""
+    if not _has_response_args(args, kwargs):
+        return args, kwargs
+    args = list(args)
+    for i, a in enumerate(args):
+        if isinstance(a, DeploymentResponse):
+            args[i] = await a
+    kwargs = dict(kwargs)
+    for k, v in kwargs.items():
+        if isinstance(v, DeploymentResponse):
+            kwargs[k] = await v
+    return tuple(args), kwargs
+
+
+class _LoopThread:
+    """A private asyncio loop on a daemon thread (Serve's router loop)."""
+
+    _shared: Optional["_LoopThread"] = None
+    _lock = threading.Lock()
+
+    def __init__(self, name="rdb-router"):
+        self.loop = asyncio.new_event_loop()
+        self.thread = threading.Thread(target=self._run, name=name, daemon=True)
+        self.thread.start()
+
+    def _run(self):
+        asyncio.set_event_loop(self.loop)
+        self.loop.run_forever()
+
+    @classmethod
+    def shared(cls) -> "_LoopThread":
+        with cls._lock:
+            if cls._shared is None or not cls._shared.thread.is_alive():
+                cls._shared = _LoopThread()
+            return cls._shared
+
+
+class RouterMetrics:
+    """serve_num_router_requests / serve_deployment_queued_queries equivalents."""
+
+    def __init__(self):
+        self.num_router_requests = 0
+        self.num_queued = 0
+        self.num_rejected_backpressure = 0
+        self.num_retries = 0
+
+
+class LocalRouter:
+    """Routes to in-process LocalReplica objects."""
+
+    def __init__(self, deployment: str, max_queued_requests: int = -1, seed: Optional[int] = None):
+        self.deployment = deployment
+        self.max_queued = max_queued_requests
+        self.replicas: List = []
+        self._lt = _LoopThread.shared()
+        self._waiters: Deque[asyncio.Future] = collections.deque()
+        self._rng = random.Random(seed)
+        self.metrics = RouterMetrics()
+        self._pending_count = 0
+
+    # replica set updates come from the controller thread
+    def update_replicas(self, replicas: List) -> None:
+        def _set():
+            self.replicas = [r for r in replicas if not r.dead]
+            self._wake()
+        self._lt.loop.call_soon_threadsafe(_set)
+
+    def set_max_queued_requests(self, v: int) -> None:
+        self.max_queued = v
+
+    def num_queued(self) -> int:
+        return self._pending_count
+
+    def total_ongoing(self) -> int:
+        return sum(r.ongoing for r in self.replicas) + self._pending_count
+
+    # --- replica choice (runs on the router loop) -------------------------
+    def _choose(self, meta: RequestMeta):
+        cands = [r for r in self.replicas if not r.dead and r.ongoing < r.max_ongoing]
+        if not cands:
+            return None
+        if meta.multiplexed_model_id:
+            with_model = [r for r in cands if meta.multiplexed_model_id in r.loaded_models]
+            if with_model:
+                cands = with_model
+        if len(cands) == 1:
+            return cands[0]
+        a, b = self._rng.sample(cands, 2)
+        return a if a.ongoing <= b.ongoing else b
+
+    def _wake(self) -> None:
+        while self._waiters:
+            w = self._waiters.popleft()
+            if not w.done():
+                w.set_result(None)
+                return
+
+    async def _acquire(self, meta: RequestMeta):
+        r = self._choose(meta)
+        if r is not None and not self._waiters:
+            return r
+        self._pending_count += 1
+        self.metrics.num_queued += 1
+        try:
+            while True:
+                w = self._lt.loop.create_future()
+                self._waiters.append(w)
+                await w
+                r = self._choose(meta)
+                if r is not None:
+                    if self._waiters:  # keep the FIFO moving
+                        self._lt.loop.call_soon(self._wake)
+                    return r
+        finally:
+            self._pending_count -= 1
+
+    async def _assign(self, meta: RequestMeta, args, kwargs, attempt: int = 0):
+        args, kwargs = await _resolve_args(args, kwargs)
+        r = await self._acquire(meta)
+        r.ongoing += 1
+        try:
+            if r.dead:
+                raise ReplicaDiedError(r.replica_id)
+            return await asyncio.wrap_future(r.call(meta, args, kwargs))
+        except ReplicaDiedError:
+            if attempt < 3:
+                self.metrics.num_retries += 1
+                return await self._assign(meta, args, kwargs, attempt + 1)
+            raise
+        finally:
+            r.ongoing -= 1
+            self._wake()
+
+    async def _assign_stream(self, meta, args, kwargs, out_q: "_queue.Queue"):
+        try:
+            args, kwargs = await _resolve_args(args, kwargs)
+            r = await self._acquire(meta)
+        except Exception as e:
+            out_q.put(("error", e))
+            return
+        r.ongoing += 1
+        try:
+            src = r.call_stream(meta, args, kwargs)
+            loop = asyncio.get_running_loop()
+            while True:
+                kind, val = await loop.run_in_executor(None, src.get)
+                out_q.put((kind, val))
+                if kind != "item":
+                    break
+        finally:
+            r.ongoing -= 1
+            self._wake()
+
+    def _check_backpressure(self) -> None:
+        if self.max_queued != -1 and self._pending_count >= self.max_queued:
+            # only when no replica has capacity right now
+            if not any(not r.dead and r.ongoing < r.max_ongoing for r in self.replicas):
+                self.metrics.num_rejected_backpressure += 1
+                raise BackPressureError(self._pending_count, self.max_queued)
+
+    def assign(self, meta: RequestMeta, args, kwargs):
+        self.metrics.num_router_requests += 1
+        if meta.stream:
+            q: _queue.Queue = _queue.Queue()
+            try:
+                self._check_backpressure()
+            except BackPressureError as e:
+                q.put(("error", e))
+                return DeploymentResponseGenerator(q, meta)
+            asyncio.run_coroutine_threadsafe(self._assign_stream(meta, args, kwargs, q), self._lt.loop)
+            return DeploymentResponseGenerator(q, meta)
+        fut: concurrent.futures.Future
+        try:
+            self._check_backpressure()
+        except BackPressureError as e:
+            fut = concurrent.futures.Future()
+            fut.set_exception(e)
+            return DeploymentResponse(fut, meta)
+        fut = asyncio.run_coroutine_threadsafe(self._assign(meta, args, kwargs), self._lt.loop)
+        return DeploymentResponse(fut, meta, cancel_cb=lambda: self._lt.loop.call_soon_threadsafe(fut.cancel))
+
+
+# ---------------------------------------------------------------------------
+# Process mode: routing through the shared-memory job segment.
+# ---------------------------------------------------------------------------
+KIND_TENSOR = 0
+KIND_PICKLE = 1
+KIND_STREAM_ITEM = 2
+KIND_STREAM_END = 3
+
+
+class ShmRouter:
+    """Routes to replica processes of one deployment (model id) through the
+    job segment.  One instance per (process, job, deployment); a single
+    dispatcher thread drains this process's completion ring for all routers
+    sharing the client."""
+
+    _clients: Dict[str, "_ShmClientHub"] = {}
+    _clients_lock = threading.Lock()
+
+    def __init__(self, job_name: str, model_id: int, deployment: str, max_queued_requests: int = -1,
+                 tensor_codec=None, max_retries: int = 3):
+        self.job_name = job_name
+        self.model_id = model_id
+        self.deployment = deployment
+        self.max_queued = max_queued_requests
+        self.codec = tensor_codec
+        self.max_retries = max_retries
+        self.metrics = RouterMetrics()
+        with ShmRouter._clients_lock:
+            hub = ShmRouter._clients.get(job_name)
+            if hub is None or hub.closed:
+                hub = _ShmClientHub(job_name)
+                ShmRouter._clients[job_name] = hub
+        self.hub = hub
+
+    def num_queued(self) -> int:
+        return self.hub.pending_for(self.model_id)
+
+    def set_max_queued_requests(self, v: int) -> None:
+        self.max_queued = v
+
+    def update_replicas(self, replicas) -> None:  # replica set lives in shm
+        self.hub.kick()
+
+    def assign(self, meta: RequestMeta, args, kwargs):
+        self.metrics.num_router_requests += 1
+        if self.max_queued != -1 and self.hub.pending_for(self.model_id) >= self.max_queued:
+            self.metrics.num_rejected_backpressure += 1
+            err = BackPressureError(self.hub.pending_for(self.model_id), self.max_queued)
+            if meta.stream:
+                q = _queue.Queue()
+                q.put(("error", err))
+                return DeploymentResponseGenerator(q, meta)
+            f = concurrent.futures.Future()
+            f.set_exception(err)
+            return DeploymentResponse(f, meta)
+        if self.codec is not None and not meta.stream and meta.method_name == "__call__" and len(args) == 1 \
+                and not kwargs and self.codec.accepts(args[0]):
+            payload, kind = self.codec.encode(args[0]), KIND_TENSOR
+        else:
+            if _has_response_args(args, kwargs):
+                # composition: resolve upstream responses on a helper thread
+                fut = concurrent.futures.Future()
+
+                def _later():
+                    try:
+                        a = tuple(x.result(_skip_asyncio_check=True) if isinstance(x, DeploymentResponse) else x for x in args)
+                        k = {kk: (v.result(_skip_asyncio_check=True) if isinstance(v, DeploymentResponse) else v)
+                             for kk, v in kwargs.items()}
+                        inner = self.assign(meta, a, k)
+                        fut.set_result(inner.result(_skip_asyncio_check=True))
+                    except BaseException as e:
+                        fut.set_exception(e)
+                threading.Thread(target=_later, daemon=True).start()
+                return DeploymentResponse(fut, meta)
+            import cloudpickle
+
+            payload = cloudpickle.dumps((meta.method_name, args, kwargs, meta.multiplexed_model_id, meta.stream,
+                                         meta.request_id))
+            kind = KIND_PICKLE
+        if meta.stream:
+            q = _queue.Queue()
+            self.hub.submit(self.model_id, payload, kind, ("stream", q), self.codec, self.max_retries)
+            return DeploymentResponseGenerator(q, meta)
+        fut = concurrent.futures.Future()
+        self.hub.submit(self.model_id, payload, kind, ("unary", fut), self.codec, self.max_retries)
+        return DeploymentResponse(fut, meta)
+
+
+class _ShmClientHub:
+    """Per-process native Client + dispatcher thread for one job segment."""
+
+    def __init__(self, job_name: str):
+        from ..runtime import job as rjob
+        from ..runtime.job import Status
+
+        self.Status = Status
+        self.job = rjob.Job(job_name, create=False)
+        self.client = rjob.Client(self.job)
+        self.lock = threading.Lock()
+        self.inflight: Dict[int, Tuple] = {}
+        self.pending: Deque[Tuple] = collections.deque()
+        self.closed = False
+        self._pending_by_model: Dict[int, int] = collections.Counter()
+        self.thread = threading.Thread(target=self._run, name=f"rdb-dispatch-{job_name}", daemon=True)
+        self.thread.start()
+
+    def pending_for(self, model_id: int) -> int:
+        return self._pending_by_model[model_id]
+
+    def kick(self) -> None:
+        with self.lock:
+            self._drain_pending()
+
+    def submit(self, model_id, payload, kind, sink, codec, retries_left) -> None:
+        with self.lock:
+            if self.pending:
+                self.pending.append((model_id, payload, kind, sink, codec, retries_left))
+                self._pending_by_model[model_id] += 1
+                self._drain_pending()
+                return
+            if not self._try_submit(model_id, payload, kind, sink, codec, retries_left):
+                self.pending.append((model_id, payload, kind, sink, codec, retries_left))
+                self._pending_by_model[model_id] += 1
+
+    def _try_submit(self, model_id, payload, kind, sink, codec, retries_left) -> bool:
+        q = self.client.choose_queue(model_id)
+        if q == -2:
+            self._fail(sink, DeploymentUnavailableError(f"no replica serves model id {model_id}"))
+            return True
+        if q < 0:
+            return False
+        rid = self.client.submit(q, payload, kind)
+        if rid == -3:
+            self._fail(sink, RayServeException("request payload larger than the ring slot "
+                                               "(raise engine.request_slot_bytes)"))
+            return True
+        if rid < 0:
+            return False
+        rep = self.job.queue_replica(q)
+        self.inflight[rid] = (model_id, payload, kind, sink, codec, retries_left, q, rep,
+                              self.job.replica_generation(rep))
+        return True
+
+    def _drain_pending(self) -> None:
+        while self.pending:
+            item = self.pending[0]
+            if not self._try_submit(*item):
+                break
+            self.pending.popleft()
+            self._pending_by_model[item[0]] -= 1
+
+    @staticmethod
+    def _fail(sink, exc) -> None:
+        kind, obj = sink
+        if kind == "unary":
+            if not obj.done():
+                obj.set_exception(exc)
+        else:
+            obj.put(("error", exc))
+
+    def _run(self) -> None:
+        import cloudpickle
+
+        St = self.Status
+        last_check = time.time()
+        while not self.closed:
+            try:
+                comps = self.client.poll(1024, 0.05)
+            except Exception:  # pragma: no cover - job torn down
+                break
+            if time.time() - last_check > 0.1:
+                last_check = time.time()
+                with self.lock:
+                    self._reap_lost()
+            if not comps:
+                if self.pending:
+                    with self.lock:
+                        self._drain_pending()
+                continue
+            with self.lock:
+                for rid, st, q, ts, td, tr, kind, payload in comps:
+                    entry = self.inflight.get(rid)
+                    if entry is None:
+                        continue
+                    model_id, req_payload, req_kind, sink, codec, retries = entry[:6]
+                    if kind == KIND_STREAM_ITEM and st == St.OK:
+                        sink[1].put(("item", cloudpickle.loads(payload)))
+                        continue
+                    del self.inflight[rid]
+                    try:
+                        if st == St.OK:
+                            if sink[0] == "stream":
+                                sink[1].put(("end", None))
+                            elif kind == KIND_TENSOR:
+                                sink[1].set_result(codec.decode(payload))
+                            else:
+                                sink[1].set_result(cloudpickle.loads(payload) if payload else None)
+                        elif st == St.ERROR:
+                            exc = cloudpickle.loads(payload) if payload else RayServeException("replica error")
+                            self._fail(sink, exc)
+                        elif st == St.DROPPED_STALE:
+                            from .exceptions import RequestDroppedError
+
+                            self._fail(sink, RequestDroppedError("request dropped: its SLO deadline could not be met"))
+                        elif st in (St.REPLICA_DIED, St.SHUTDOWN) and retries > 0:
+                            self.pending.appendleft((model_id, req_payload, req_kind, sink, codec, retries - 1))
+                            self._pending_by_model[model_id] += 1
+                        elif st == St.TOO_LARGE:
+                            self._fail(sink, RayServeException("result larger than the completion slot"))
+                        else:
+                            self._fail(sink, ReplicaDiedError(f"request failed with status {int(st)}"))
+                    except Exception as e:  # pragma: no cover - decode failure
+                        self._fail(sink, e)
+                self._drain_pending()
+
+    def _reap_lost(self) -> None:
+        """Requests a replica popped but never answered because it died (its
+        generation changed or it is DEAD) are re-dispatched (idempotent forward)."""
+        lost = []
+        for rid, e in self.inflight.items():
+            rep, gen = e[7], e[8]
+            if self.job.replica_generation(rep) != gen or self.job.replica_status(rep) == 4:
+                lost.append(rid)
+        for rid in lost:
+            model_id, payload, kind, sink, codec, retries = self.inflight.pop(rid)[:6]
+            if retries > 0:
+                self.pending.appendleft((model_id, payload, kind, sink, codec, retries - 1))
+                self._pending_by_model[model_id] += 1
+            else:
+                self._fail(sink, ReplicaDiedError("replica died while processing the request"))
+        if lost:
+            self._drain_pending()
+
+    def close(self) -> None:
+        self.closed = True
+        if self.thread.is_alive() and self.thread is not threading.current_thread():
+            self.thread.join(2.0)
+
+
+def _close_all_hubs() -> None:
+    for hub in list(ShmRouter._clients.values()):
+        hub.close()
+
+
+import atexit as _atexit  # noqa: E402
+
+_atexit.register(_close_all_hubs)

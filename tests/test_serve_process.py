@@ -1,0 +1,81 @@
+"""Process-mode serving on CPU: replica processes + shm rings (no GPU needed)."""
+import os
+import signal
+import time
+
+import pytest
+
+from ray_dynamic_batching_amd import serve
+
+
+@pytest.fixture(autouse=True)
+def _shutdown():
+    yield
+    serve.shutdown()
+
+
+@serve.deployment(num_replicas=2, max_ongoing_requests=16)
+class Echo:
+    def __init__(self, k):
+        self.k = k
+
+    @serve.batch(max_batch_size=4, batch_wait_timeout_s=0.01)
+    async def __call__(self, xs):
+        return [x * self.k for x in xs]
+
+    def pid(self):
+        return os.getpid()
+
+    def stream(self, n):
+        for i in range(n):
+            yield i
+
+    def fail(self):
+        raise KeyError("nope")
+
+
+def test_process_mode_roundtrip_stream_errors():
+    h = serve.run(Echo.bind(7), mode="process")
+    rs = [h.remote(i) for i in range(50)]
+    assert [r.result(timeout_s=20) for r in rs] == [7 * i for i in range(50)]
+    pids = {h.pid.remote().result(timeout_s=10) for _ in range(20)}
+    assert len(pids) == 2 and os.getpid() not in pids
+    assert list(h.options(method_name="stream", stream=True).remote(5)) == [0, 1, 2, 3, 4]
+    with pytest.raises(KeyError):
+        h.fail.remote().result(timeout_s=10)
+    st = serve.status()["applications"]["default"]["deployments"]["Echo"]
+    assert st["mode"] == "process" and st["running_replicas"] == 2
+    assert sum(r["queue"]["completed"] for r in st["replicas"]) >= 50
+
+
+@serve.deployment(num_replicas=1)
+class Down:
+    def __call__(self, x):
+        return x + 1
+
+
+@serve.deployment(num_replicas=1)
+class Up:
+    def __init__(self, down):
+        self.down = down
+
+    async def __call__(self, x):
+        return await self.down.remote(x) * 10
+
+
+def test_process_mode_composition_across_processes():
+    h = serve.run(Up.bind(Down.bind()), mode="process")
+    assert h.remote(4).result(timeout_s=20) == 50
+
+
+def test_replica_crash_is_restarted_and_requests_retried():
+    h = serve.run(Echo.options(num_replicas=1, health_check_timeout_s=2).bind(2), mode="process")
+    pid = h.pid.remote().result(timeout_s=10)
+    os.kill(pid, signal.SIGKILL)
+    t = time.time()
+    # a request sent while the replica is dead is retried after the restart
+    assert h.remote(21).result(timeout_s=60) == 42
+    new_pid = h.pid.remote().result(timeout_s=10)
+    assert new_pid != pid
+    st = serve.status()["applications"]["default"]["deployments"]["Echo"]
+    assert st["replicas"][0]["restarts"] >= 1
