@@ -1,0 +1,371 @@
+"""SLO-aware multi-model scheduler runtime (the fork's NexusScheduler + GPUWorker,
+293-project/src/scheduler.py:374-930, re-designed on the shm data plane).
+
+* Per-model request queues: the job segment has one queue per (GPU, model);
+  a queue is ACTIVE only on the GPUs the current plan places that model on,
+  so the native router's power-of-two choice follows the plan automatically
+  (no per-request RPC, no RayQueue actors).
+* Executors, one per GPU:
+    - ``DutyCycleExecutor`` (Python; CPU tests and arbitrary torch models):
+      the fork's duty-cycle loop -- for each (session, occupancy) take up to
+      ``batch`` requests, drop stale ones, run, then wait out the time slice
+      (scheduler.py:525-588, without its inverted end-of-cycle sleep);
+    - the native engine (GPU): same sessions handed to ops/csrc/engine.cpp,
+      which serves them EDF/priority-first with stale dropping in C++.
+* Monitoring: request rates from RateTrackers; a model triggers re-planning
+  when it is new or its rate moved by more than ``rate_change_threshold``
+  (2x that threshold for decreases), as in scheduler.py:773-819.  The new
+  plan is placed on GPU slots with minimal model moves (Hungarian assignment)
+  and applied at batch boundaries (models loaded/unloaded by the executor).
+"""
+from __future__ import annotations
+
+import copy
+import logging
+import math
+import threading
+import time
+from dataclasses import dataclass, field
+from typing import Any, Callable, Dict, List, Optional
+
+import numpy as np
+
+from ..runtime import job as rjob
+from .nexus import Node, Plan, Session, SquishyPlanner, assign_to_slots, total_transfers
+from .rates import RateTracker
+
+logger = logging.getLogger("ray_dynamic_batching_amd.planner")
+
+
+@dataclass
+class ScheduleChange:
+    time: float
+    reason: Dict[str, float]
+    nodes: List[List[tuple]]
+    transfers: int
+
+
+class DutyCycleExecutor(threading.Thread):
+    """One GPU worker (CPU-capable): serves the sessions of its plan node."""
+
+    def __init__(self, sched: "SLOScheduler", gpu: int):
+        super().__init__(name=f"executor-{gpu}", daemon=True)
+        self.sched = sched
+        self.gpu = gpu
+        self.node: Optional[Node] = None
+        self._new: Optional[Node] = None
+        self._lock = threading.Lock()
+        self.models: Dict[str, Any] = {}
+        self.stop_flag = threading.Event()
+        self.stats = dict(processed_batches=0, total_requests=0, dropped=0, processing_ms=[])
+        self.consumers: Dict[str, Any] = {}
+
+    def update(self, node: Optional[Node]) -> None:
+        with self._lock:
+            self._new = node if node is not None else Node([], 1.0)
+
+    def _apply_update(self) -> None:
+        with self._lock:
+            new, self._new = self._new, None
+        if new is None:
+            return
+        new_models = set(new.models())
+        for m in list(self.models):
+            if m not in new_models:           # unload (fork: .cpu(); del; empty_cache)
+                del self.models[m]
+                self.consumers.pop(m, None)
+        for m in new_models:
+            if m not in self.models:          # load
+                self.models[m] = self.sched.model_factories[m]()
+                q = self.sched.queue_id(self.gpu, m)
+                self.consumers[m] = rjob.Consumer(self.sched.job, [q])
+        self.node = new
+
+    def run(self) -> None:
+        S = self.sched
+        while not self.stop_flag.is_set():
+            self._apply_update()
+            node = self.node
+            if node is None or not node.sessions:
+                time.sleep(0.01)
+                continue
+            cycle_start = time.perf_counter()
+            for s, occ in node.sessions:
+                slice_s = node.duty_cycle * occ / 1000.0
+                t0 = time.perf_counter()
+                self._serve(s)
+                spent = time.perf_counter() - t0
+                if spent < slice_s:
+                    time.sleep(min(slice_s - spent, 0.25))
+                if self.stop_flag.is_set() or self._new is not None:
+                    break
+            # end of duty cycle: idle out the remainder (the fork's sign-inverted sleep, fixed)
+            rem = node.duty_cycle / 1000.0 - (time.perf_counter() - cycle_start)
+            if rem > 0 and self._new is None:
+                self.stop_flag.wait(min(rem, 0.25))
+
+    def _serve(self, s: Session) -> None:
+        S = self.sched
+        cons = self.consumers.get(s.model_name)
+        model = self.models.get(s.model_name)
+        if cons is None or model is None:
+            return
+        reqs = cons.pop(max(1, s.batch_size), 0)
+        if not reqs:
+            return
+        est_ms = S.latency_ms(s.model_name, len(reqs))
+        from ..utils.native import load_runtime
+
+        now = load_runtime().now_ns()
+        keep, xs = [], []
+        for r in reqs:
+            rid, q, client, kind, t_sub, dl, payload = r
+            deadline = dl or (t_sub + int(S.slos[s.model_name] * 1e6))
+            if S.drop_stale and now + est_ms * 1e6 > deadline:
+                cons.complete(client, rid, q, int(rjob.Status.DROPPED_STALE), t_sub, b"", 0)
+                self.stats["dropped"] += 1
+                continue
+            keep.append(r)
+            xs.append(np.frombuffer(payload, dtype=S.codecs[s.model_name].in_np).reshape(S.codecs[s.model_name].input_shape))
+        if not keep:
+            return
+        import torch
+
+        t0 = time.perf_counter()
+        with torch.no_grad():
+            y = model.forward(torch.from_numpy(np.stack(xs)))
+        y = y.cpu().numpy()
+        dt = (time.perf_counter() - t0) * 1e3
+        for r, out in zip(keep, y):
+            rid, q, client, kind, t_sub, dl, payload = r
+            cons.complete(client, rid, q, 0, t_sub, np.ascontiguousarray(out, dtype=S.codecs[s.model_name].out_np).tobytes(), 0)
+        self.stats["processed_batches"] += 1
+        self.stats["total_requests"] += len(keep)
+        self.stats["processing_ms"] = (self.stats["processing_ms"] + [dt])[-100:]
+
+
+class SLOScheduler:
+    def __init__(self, profiles: Dict[str, Dict[int, Dict[str, float]]], slos_ms: Dict[str, float],
+                 model_factories: Dict[str, Callable[[], Any]], codecs: Dict[str, Any], num_gpus: int = 2,
+                 monitoring_interval: float = 1.0, rate_change_threshold: float = 0.05, rate_window_s: float = 1.0,
+                 compat: bool = False, slo_divisor: float = 1.0, drop_stale: bool = True,
+                 gpu_mem_gb: Optional[float] = None, queue_capacity: int = 2048, job_name: Optional[str] = None):
+        self.profiles = profiles
+        self.slos = dict(slos_ms)
+        self.model_factories = model_factories
+        self.codecs = codecs
+        self.models = sorted(slos_ms)
+        self.num_gpus = num_gpus
+        self.monitoring_interval = monitoring_interval
+        self.threshold = rate_change_threshold
+        self.slo_divisor = slo_divisor
+        self.drop_stale = drop_stale
+        self.planner = SquishyPlanner(profiles, gpu_mem_gb=gpu_mem_gb, compat=compat)
+        self.trackers = {m: RateTracker(rate_window_s) for m in self.models}
+        self.sessions: Dict[str, Session] = {}
+        self.slots: List[Optional[Node]] = [None] * num_gpus
+        self.changes: List[ScheduleChange] = []
+        self.unplaced_nodes = 0
+        slot_bytes = max(c.in_bytes for c in codecs.values())
+        cmp_bytes = max(c.out_bytes for c in codecs.values())
+        self.job_name = job_name or rjob.unique_job_name("sched")
+        self.job = rjob.Job(self.job_name, create=True, n_replicas=num_gpus, n_queues=num_gpus * len(self.models),
+                            n_clients=8, req_capacity=queue_capacity, req_slot_bytes=slot_bytes,
+                            cmp_capacity=max(4096, queue_capacity * 2), cmp_slot_bytes=cmp_bytes)
+        for g in range(num_gpus):
+            self.job.set_replica_status(g, 2, g, 0)
+            for m in self.models:
+                self.job.configure_queue(self.queue_id(g, m), g, self.model_id(m), 0,
+                                         float(self.slos[m]), False)
+        self.client = rjob.Client(self.job)
+        self._client_lock = threading.Lock()
+        self._backlog: List[tuple] = []
+        self._backlog_ids = 0
+        self.executors = [DutyCycleExecutor(self, g) for g in range(num_gpus)]
+        for e in self.executors:
+            e.start()
+        self._monitor: Optional[threading.Thread] = None
+        self._stop = threading.Event()
+        self.lock = threading.Lock()
+
+    # --------------------------------------------------------------- ids
+    def model_id(self, m: str) -> int:
+        return self.models.index(m)
+
+    def queue_id(self, gpu: int, m: str) -> int:
+        return gpu * len(self.models) + self.model_id(m)
+
+    def latency_ms(self, model: str, b: int) -> float:
+        rows = self.profiles[model]
+        ks = [k for k in rows if k >= b]
+        return rows[min(ks) if ks else max(rows)]["avg_latency_ms"]
+
+    # ------------------------------------------------------------ ingress
+    def submit_request(self, model_name: str, request_id: Any = None, input_tensor=None) -> bool:
+        """Fork API (scheduler.py:734-751): enqueue one request; False if dropped."""
+        return self.submit(model_name, input_tensor) > 0
+
+    def submit(self, model_name: str, x, deadline_s: float = 0.0) -> int:
+        if model_name not in self.trackers:
+            return -2
+        self.trackers[model_name].record()
+        payload = self.codecs[model_name].encode(x)
+        with self._client_lock:
+            q = self.client.choose_queue(self.model_id(model_name))
+            if q == -2:
+                # model not placed yet: hold the request until the next plan places it
+                rid = self._next_backlog_id()
+                self._backlog.append((model_name, payload, deadline_s, rid))
+                return rid
+            if q < 0:
+                q = self._least_loaded_active(model_name)
+            return self.client.submit(q, payload, 0, deadline_s)
+
+    def _least_loaded_active(self, model_name: str) -> int:
+        qs = [self.queue_id(g, model_name) for g in range(self.num_gpus)
+              if self.slots[g] is not None and model_name in self.slots[g].models()]
+        return min(qs, key=self.job.queue_depth) if qs else self.queue_id(0, model_name)
+
+    def _next_backlog_id(self) -> int:
+        self._backlog_ids += 1
+        return 1 << 62 | self._backlog_ids
+
+    def _flush_backlog(self) -> None:
+        with self._client_lock:
+            keep = []
+            for model_name, payload, dl, rid in self._backlog:
+                q = self.client.choose_queue(self.model_id(model_name))
+                if q == -2:
+                    keep.append((model_name, payload, dl, rid))
+                    continue
+                if q < 0:
+                    q = self._least_loaded_active(model_name)
+                self.client.submit(q, payload, 0, dl, rid)
+            self._backlog = keep
+
+    def poll(self, max_n: int = 1024, timeout_s: float = 0.0):
+        with self._client_lock:
+            return self.client.poll(max_n, timeout_s)
+
+    # ----------------------------------------------------------- planning
+    def start_monitoring(self) -> None:
+        if self._monitor is not None:
+            return
+        self._stop.clear()
+        self._monitor = threading.Thread(target=self._monitor_loop, name="rate-monitor", daemon=True)
+        self._monitor.start()
+
+    def stop_monitoring(self) -> None:
+        self._stop.set()
+        if self._monitor is not None:
+            self._monitor.join()
+            self._monitor = None
+
+    def _monitor_loop(self) -> None:
+        while not self._stop.wait(self.monitoring_interval):
+            try:
+                self.check_and_update()
+            except Exception:  # pragma: no cover
+                logger.exception("monitor error")
+
+    def check_and_update(self, rates: Optional[Dict[str, float]] = None) -> bool:
+        rates = rates or {m: t.rate() for m, t in self.trackers.items()}
+        update = {}
+        with self.lock:
+            for m, r in rates.items():
+                if r <= 0:
+                    continue
+                if m not in self.sessions:
+                    update[m] = r
+                    continue
+                prev = self.sessions[m].request_rate
+                diff = r - prev
+                thr = self.threshold * (2 if diff < 0 else 1)
+                if prev > 0 and abs(diff) / prev > thr:
+                    update[m] = r
+        if update:
+            self.replan(update)
+            return True
+        return False
+
+    def replan(self, update: Dict[str, float]) -> Plan:
+        with self.lock:
+            sessions = []
+            for m, s in self.sessions.items():
+                ns = copy.copy(s)
+                if m in update:
+                    ns.request_rate = update[m]
+                if ns.request_rate > 0:
+                    sessions.append(ns)
+            for m, r in update.items():
+                if m not in self.sessions and r > 0:
+                    sessions.append(Session(m, self.slos[m] / self.slo_divisor, r))
+            plan = self.planner.plan(sessions)
+            nodes = plan.nodes
+            if len(nodes) > self.num_gpus:
+                # more GPUs needed than the node has: keep the most loaded ones (the fork
+                # silently ignored the shortage, scheduler.py:927-929; we count it)
+                self.unplaced_nodes = len(nodes) - self.num_gpus
+                nodes = sorted(nodes, key=lambda n: n.occupancy(), reverse=True)[: self.num_gpus]
+            else:
+                self.unplaced_nodes = 0
+            placed = assign_to_slots(self.slots, nodes)[: self.num_gpus]
+            placed += [None] * (self.num_gpus - len(placed))
+            transfers = total_transfers(self.slots, placed)
+            self.sessions = {s.model_name: s for s in sessions}
+            self.slots = placed
+            self._apply(placed)
+            self._flush_backlog()
+            self.changes.append(ScheduleChange(time.time(), dict(update),
+                                               [n.as_tuples() if n else [] for n in placed], transfers))
+            logger.info("new schedule (%d transfers):\n%s", transfers,
+                        "\n".join(n.describe() if n else "(idle)" for n in placed))
+            return plan
+
+    def _apply(self, placed: List[Optional[Node]]) -> None:
+        for g, node in enumerate(placed):
+            models = set(node.models()) if node else set()
+            for m in self.models:
+                batch = 0
+                if node:
+                    batch = max((s.batch_size for s, _ in node.sessions if s.model_name == m), default=0)
+                self.job.configure_queue(self.queue_id(g, m), g, self.model_id(m), 0, float(self.slos[m]),
+                                         m in models)
+            self.executors[g].update(node)
+        # requests parked on queues that are no longer active stay there until a
+        # plan re-activates them; move them forward by re-submitting is unnecessary
+        # because every model keeps at least one active queue while its rate > 0.
+
+    # ------------------------------------------------------------- metrics
+    def get_stats(self) -> Dict[str, Dict[str, Any]]:
+        """Per-model stats with the fork's metrics.json keys (scheduler.py:343-372)."""
+        out = {}
+        for m in self.models:
+            tot = dict(total_requests=0, dropped_requests=0, slo_violations=0, queue_size=0, completed=0)
+            lat_p = []
+            for g in range(self.num_gpus):
+                st = self.job.queue_stats(self.queue_id(g, m))
+                tot["total_requests"] += st["submitted"]
+                tot["dropped_requests"] += st["dropped"]
+                tot["slo_violations"] += st["slo_violations"]
+                tot["queue_size"] += st["ring_depth"]
+                tot["completed"] += st["completed"]
+                if st["e2e"]["count"]:
+                    lat_p.append(st["e2e"])
+            n = sum(h["count"] for h in lat_p)
+            tot["avg_latency"] = sum(h["mean_ms"] * h["count"] for h in lat_p) / n if n else 0.0
+            tot["p95_latency"] = max((h["p95_ms"] for h in lat_p), default=0.0)
+            tot["p99_latency"] = max((h["p99_ms"] for h in lat_p), default=0.0)
+            tot["request_rate"] = self.trackers[m].rate()
+            tot["slo_ms"] = self.slos[m]
+            out[m] = tot
+        return out
+
+    def shutdown(self) -> None:
+        self.stop_monitoring()
+        for e in self.executors:
+            e.stop_flag.set()
+        for e in self.executors:
+            e.join(2)
+        self.job.set_shutdown(True)
+        self.job.close()
