@@ -1,0 +1,41 @@
+import os
+import subprocess
+import sys
+
+import pytest
+import torch
+
+from ray_dynamic_batching_amd import serve
+from ray_dynamic_batching_amd.serve.schema import ServeDeploySchema, build_application, deploy_config
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(autouse=True)
+def _shutdown():
+    yield
+    serve.shutdown()
+
+
+def test_yaml_deploy_applies_overrides():
+    sys.path.insert(0, ROOT)
+    sch = ServeDeploySchema.from_yaml(os.path.join(ROOT, "configs", "mlp_local.yaml"))
+    app = build_application(sch.applications[0])
+    assert app.deployment.config.num_replicas == 2 and app.deployment.config.max_ongoing_requests == 16
+    h = deploy_config(sch)["mlp"]
+    y = h.remote(torch.zeros(32)).result(timeout_s=10)
+    assert tuple(y.shape) == (8,)
+    assert serve.status()["applications"]["mlp"]["deployments"]["MLPDeployment"]["running_replicas"] == 2
+
+
+def test_cli_build_and_run():
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    out = subprocess.run([sys.executable, "-m", "ray_dynamic_batching_amd.serve.cli", "build", "examples.mlp_app:app"],
+                         capture_output=True, text=True, env=env, cwd=ROOT, timeout=120)
+    assert out.returncode == 0, out.stderr
+    assert "import_path: examples.mlp_app:app" in out.stdout and "num_replicas: 2" in out.stdout
+    out = subprocess.run([sys.executable, "-m", "ray_dynamic_batching_amd.serve.cli", "run", "examples.mlp_app:app",
+                          "--mode", "local", "--duration", "0.5"], capture_output=True, text=True, env=env, cwd=ROOT,
+                         timeout=120)
+    assert out.returncode == 0, out.stderr
+    assert "HEALTHY" in out.stdout
