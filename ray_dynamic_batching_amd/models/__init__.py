@@ -56,3 +56,25 @@ def _bert(device="cuda", backend="hip", seq_len=128, layers=12, **kw):
     from .bert import BertConfig, BertForSequenceClassification
 
     return BertForSequenceClassification(BertConfig(seq_len=seq_len, layers=layers), device=device, backend=backend, **kw)
+
+
+@register("resnet50")
+def _resnet(device="cuda", backend="hip", **kw):
+    from .resnet import ResNet50
+
+    return ResNet50(device=device, backend=backend, **kw)
+
+
+@register("llama3-8b")
+def _llama(device="cuda", backend="hip", tp_rank=0, tp_size=1, group_name=None, seq_len=512, layers=32, **kw):
+    from .llama import LlamaConfig, LlamaTP
+
+    return LlamaTP(LlamaConfig(seq_len=seq_len, layers=layers), tp_rank, tp_size, group_name, device=device,
+                   backend=backend, **kw)
+
+
+@register("vit-b16")
+def _vit(device="cuda", backend="hip", **kw):
+    from .vit import ViT, ViTConfig
+
+    return ViT(ViTConfig.b16(), device=device, backend=backend, **kw)

@@ -1,0 +1,60 @@
+"""Picklable model factories for servable deployments (shipped to replica
+processes), each with the per-request I/O spec the router's codec needs."""
+from __future__ import annotations
+
+import functools
+
+import torch
+
+
+class Factory:
+    """Callable factory with an ``io_spec`` (input_shape, input_dtype, output_shape, output_dtype)."""
+
+    def __init__(self, fn, io_spec, **kw):
+        self.fn = fn
+        self.kw = kw
+        self.io_spec = io_spec
+
+    def __call__(self, device="cuda"):
+        return self.fn(device=device, **self.kw)
+
+
+def _bert(device, layers=12, seq_len=128, backend="hip"):
+    from .bert import BertConfig, BertForSequenceClassification
+
+    return BertForSequenceClassification(BertConfig(layers=layers, seq_len=seq_len), device=device, backend=backend)
+
+
+def _resnet(device, backend="hip"):
+    from .resnet import ResNet50
+
+    return ResNet50(device=device, backend=backend)
+
+
+def _vit(device, backend="hip"):
+    from .vit import ViT, ViTConfig
+
+    return ViT(ViTConfig.b16(), device=device, backend=backend)
+
+
+def _mlp(device, **kw):
+    from .mlp import MLP
+
+    return MLP(device=device, **kw)
+
+
+def bert_base(layers: int = 12, seq_len: int = 128, backend: str = "hip") -> Factory:
+    return Factory(_bert, ((seq_len,), torch.int32, (2,), torch.float32), layers=layers, seq_len=seq_len,
+                   backend=backend)
+
+
+def resnet50(backend: str = "hip") -> Factory:
+    return Factory(_resnet, ((224, 224, 3), torch.uint8, (10,), torch.float32), backend=backend)
+
+
+def vit_b16(backend: str = "hip") -> Factory:
+    return Factory(_vit, ((224, 224, 3), torch.uint8, (10,), torch.float32), backend=backend)
+
+
+def mlp(d_in: int = 32, d_out: int = 8) -> Factory:
+    return Factory(_mlp, ((d_in,), torch.float32, (d_out,), torch.float32), d_in=d_in, d_out=d_out)

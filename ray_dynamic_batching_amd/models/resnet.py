@@ -1,0 +1,145 @@
+"""ResNet-50 (random init) on the NHWC f16 implicit-GEMM conv kernels.
+
+The fork's main profiled model (scheduler.py:43; resnet50_* profile) and
+BASELINE config 2 (ResNet-50 fp16, 1 replica, dyn-batch <= 32 / 5 ms).
+
+Serving contract: one request = one uint8 RGB image [224, 224, 3] (what a
+client actually sends; half the PCIe bytes of f16 NCHW); one response =
+top-5 (probability, class id) as 10 float32 (softmax + top-k fused kernel --
+the Serve ResNet workload's softmax + argmax).
+
+Forward (all on gfx950 kernels, hipGraph-captured by the replica engine):
+  image_to_nhwc (normalise, C 3 -> 8) -> conv7x7/2 (+BN folded +ReLU) ->
+  maxpool3x3/2 -> 16 bottlenecks [conv1x1+ReLU, conv3x3(/s)+ReLU,
+  conv1x1 + (downsample conv) residual + ReLU fused in the epilogue] ->
+  global avgpool -> FC GEMM (f32 logits) -> softmax_topk(5)
+BatchNorm is folded into (W, b) at load time.
+"""
+from __future__ import annotations
+
+import math
+from typing import List
+
+import torch
+import torch.nn.functional as F
+
+from .. import ops
+
+STAGES = [(64, 3, 1), (128, 4, 2), (256, 6, 2), (512, 3, 2)]   # (width, blocks, stride)
+
+
+class ResNet50:
+    def __init__(self, device="cuda", dtype=torch.float16, backend: str = "hip", num_classes: int = 1000, seed: int = 0,
+                 image_size: int = 224, topk: int = 5):
+        self.device = torch.device(device)
+        self.dtype = dtype
+        self.backend = backend
+        self.num_classes = num_classes
+        self.image_size = image_size
+        self.topk = topk
+        g = torch.Generator(device="cpu").manual_seed(seed)
+
+        def conv(cin, cout, k, gamma=1.0):
+            w = torch.randn(cout, k, k, cin, generator=g) * math.sqrt(2.0 / (k * k * cin))
+            # folded BN: y = gamma * (conv - mean) / sqrt(var + eps) + beta, with
+            # random running stats
+            mean = torch.randn(cout, generator=g) * 0.01
+            var = 1.0 + torch.rand(cout, generator=g) * 0.1
+            beta = torch.randn(cout, generator=g) * 0.01
+            scale = gamma / torch.sqrt(var + 1e-5)
+            wf = w * scale[:, None, None, None]
+            bf = beta - mean * scale
+            return wf.to(self.device, dtype).contiguous(), bf.to(self.device, dtype).contiguous()
+
+        w, b = conv(3, 64, 7)
+        self.stem_w = torch.zeros(64, 7, 7, 8, device=self.device, dtype=dtype)   # C padded 3 -> 8
+        self.stem_w[..., :3] = w
+        self.stem_b = b
+        self.blocks: List[dict] = []
+        cin = 64
+        for width, n, stride in STAGES:
+            for i in range(n):
+                s = stride if i == 0 else 1
+                blk = dict(stride=s)
+                blk["w1"], blk["b1"] = conv(cin, width, 1)
+                blk["w2"], blk["b2"] = conv(width, width, 3)
+                blk["w3"], blk["b3"] = conv(width, width * 4, 1, gamma=0.2)   # small last-BN gamma keeps f16 stable
+                if s != 1 or cin != width * 4:
+                    blk["wd"], blk["bd"] = conv(cin, width * 4, 1)
+                self.blocks.append(blk)
+                cin = width * 4
+        self.fc_w = (torch.randn(num_classes, 2048, generator=g) * 0.01).to(self.device, dtype).contiguous()
+        self.fc_b = torch.zeros(num_classes, device=self.device, dtype=dtype)
+
+    # -- serving contract
+    @property
+    def input_shape(self):
+        return (self.image_size, self.image_size, 3)
+
+    input_dtype = torch.uint8
+
+    @property
+    def output_shape(self):
+        return (2 * self.topk,)
+
+    output_dtype = torch.float32
+
+    def __call__(self, x):
+        return self.forward(x)
+
+    @torch.no_grad()
+    def forward(self, img: torch.Tensor) -> torch.Tensor:
+        """img uint8 [B, H, W, 3] -> [B, 2k] f32 = (top-k probs, top-k class ids)."""
+        logits = self.logits(img)
+        if self.backend == "hip":
+            p, i = ops.softmax_topk(logits, self.topk)
+        else:
+            p, i = ops.softmax_topk_ref(logits, self.topk)
+        return torch.cat([p, i.float()], dim=1).contiguous()
+
+    def logits(self, img: torch.Tensor) -> torch.Tensor:
+        if self.backend == "hip":
+            return self._logits_hip(img)
+        return self._logits_torch(img)
+
+    def _logits_hip(self, img):
+        x = ops.image_to_nhwc(img, 8)
+        x = ops.conv2d_nhwc(x, self.stem_w, self.stem_b, stride=2, pad=3, act="relu")
+        x = ops.maxpool_nhwc(x, 3, 2, 1)
+        for blk in self.blocks:
+            s = blk["stride"]
+            h = ops.conv2d_nhwc(x, blk["w1"], blk["b1"], act="relu")
+            h = ops.conv2d_nhwc(h, blk["w2"], blk["b2"], stride=s, pad=1, act="relu")
+            sc = ops.conv2d_nhwc(x, blk["wd"], blk["bd"], stride=s) if "wd" in blk else x
+            x = ops.conv2d_nhwc(h, blk["w3"], blk["b3"], act="relu", residual=sc)
+        pooled = ops.avgpool_nhwc(x)
+        return ops.linear(pooled, self.fc_w, self.fc_b, out_dtype=torch.float32)
+
+    def _logits_torch(self, img):
+        """Eager PyTorch baseline (NCHW via channels_last, same folded weights)."""
+        dt = self.dtype if self.device.type == "cuda" else torch.float32
+        mean = torch.tensor([0.485, 0.456, 0.406], device=img.device)
+        std = torch.tensor([0.229, 0.224, 0.225], device=img.device)
+        x = ((img.float() / 255.0 - mean) / std).permute(0, 3, 1, 2).to(dt)
+
+        def cv(x, w, b, s=1, p=0):
+            return F.conv2d(x, w.permute(0, 3, 1, 2).to(dt), b.to(dt), stride=s, padding=p)
+
+        x = F.relu(cv(x, self.stem_w[..., :3], self.stem_b, 2, 3))
+        x = F.max_pool2d(x, 3, 2, 1)
+        for blk in self.blocks:
+            s = blk["stride"]
+            h = F.relu(cv(x, blk["w1"], blk["b1"]))
+            h = F.relu(cv(h, blk["w2"], blk["b2"], s, 1))
+            sc = cv(x, blk["wd"], blk["bd"], s) if "wd" in blk else x
+            x = F.relu(cv(h, blk["w3"], blk["b3"]) + sc)
+        pooled = x.float().mean(dim=(2, 3))
+        return (pooled @ self.fc_w.float().t() + self.fc_b.float()).float()
+
+    def example_input(self, batch: int, seed: int = 0, device=None) -> torch.Tensor:
+        g = torch.Generator(device="cpu").manual_seed(seed)
+        return torch.randint(0, 256, (batch,) + self.input_shape, generator=g, dtype=torch.uint8).to(
+            device or self.device)
+
+    def flops_per_image(self) -> float:
+        return 2 * 4.1e9  # ~4.1 GMACs at 224x224

@@ -231,7 +231,8 @@ def attention(qkv: torch.Tensor, B: int, S: int, H: int, Hkv: int, D: int, lens:
               causal: bool = False, scale: Optional[float] = None, out: Optional[torch.Tensor] = None,
               q_off: int = 0, k_off: Optional[int] = None, v_off: Optional[int] = None) -> torch.Tensor:
     """Fused MHA / GQA on the packed projection output qkv [B*S, ld] (q | k | v)."""
-    _check(qkv.is_cuda and qkv.dtype == torch.bfloat16 and qkv.dim() == 2 and qkv.stride(1) == 1, "attention: bad qkv")
+    _check(qkv.is_cuda and qkv.dtype in (torch.bfloat16, torch.float16) and qkv.dim() == 2 and qkv.stride(1) == 1,
+           "attention: bad qkv")
     _check(qkv.shape[0] == B * S, "attention: qkv rows must be B*S")
     _check(D in (64, 128), "attention: head dim must be 64 or 128")
     _check(H % Hkv == 0, "attention: H % Hkv")
@@ -246,7 +247,7 @@ def attention(qkv: torch.Tensor, B: int, S: int, H: int, Hkv: int, D: int, lens:
         out = torch.empty(B * S, H * D, device=qkv.device, dtype=qkv.dtype)
     _check(out.is_contiguous() and out.shape == (B * S, H * D), "attention: bad out")
     scale = 1.0 / math.sqrt(D) if scale is None else scale
-    _ops().attn_fwd(qkv.data_ptr(), ld, q_off, k_off, v_off, B, H, Hkv, S, D, _ptr(lens), int(causal),
+    _ops().attn_fwd(DTYPE_CODE[qkv.dtype], qkv.data_ptr(), ld, q_off, k_off, v_off, B, H, Hkv, S, D, _ptr(lens), int(causal),
                     out.data_ptr(), H * D, float(scale), _stream())
     return out
 

@@ -32,25 +32,39 @@ struct AttnCfg {
   static constexpr int V_BYTES = D * VT_LD * 2;
 };
 
+template <typename T>
+__device__ __forceinline__ f32x4 mma16(
+    T __attribute__((ext_vector_type(8))) a, T __attribute__((ext_vector_type(8))) b, f32x4 c);
+template <>
+__device__ __forceinline__ f32x4 mma16<bf16>(bf16x8 a, bf16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+template <>
+__device__ __forceinline__ f32x4 mma16<f16>(f16x8 a, f16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
+
 template <int CPR>
 __device__ __forceinline__ int kswz(int row, int chunk) {
   if constexpr (CPR == 8) return row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4);
   else return row * (CPR * 16) + ((chunk ^ (row & 15)) << 4);
 }
 
-template <int D>
+template <typename T, int D>
 __global__ void __launch_bounds__(256, 2)
-attn_fwd_kernel(const bf16* __restrict__ qkv, int ld_qkv, int q_off, int k_off, int v_off,
+attn_fwd_kernel(const T* __restrict__ qkv, int ld_qkv, int q_off, int k_off, int v_off,
                 int H, int Hkv, int S, const int* __restrict__ lens, int causal,
-                bf16* __restrict__ out, int ld_out, float scale_log2e) {
+                T* __restrict__ out, int ld_out, float scale_log2e) {
   typedef AttnCfg<D> C;
+  typedef T frag8 __attribute__((ext_vector_type(8)));
+  typedef T frag4 __attribute__((ext_vector_type(4)));
   constexpr int KB = C::KB;
   constexpr int NKT = KB / 16;       // key tiles per block
   constexpr int NKS = D / 32;        // k-steps for S = K.Q^T
   constexpr int NDT = D / 16;        // d tiles of O^T
   __shared__ __attribute__((aligned(16))) char smem[C::K_BYTES + C::V_BYTES];
   char* Ks = smem;
-  bf16* Vt = reinterpret_cast<bf16*>(smem + C::K_BYTES);
+  T* Vt = reinterpret_cast<T*>(smem + C::K_BYTES);
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int fr = lane & 15, fg = lane >> 4;
@@ -62,17 +76,17 @@ attn_fwd_kernel(const bf16* __restrict__ qkv, int ld_qkv, int q_off, int k_off, 
   kv_len = kv_len > S ? S : kv_len;
 
   // Q fragments (B operand): lane holds Q[q][ks*32 + 8*fg + j].
-  bf16x8 qf[2][NKS];
+  frag8 qf[2][NKS];
 #pragma unroll
   for (int qt = 0; qt < 2; ++qt) {
     const int q = q0 + qt * 16 + fr;
 #pragma unroll
     for (int ks = 0; ks < NKS; ++ks) {
       if (q < S)
-        qf[qt][ks] = *reinterpret_cast<const bf16x8*>(qkv + (tok0 + q) * ld_qkv + q_off + h * D +
+        qf[qt][ks] = *reinterpret_cast<const frag8*>(qkv + (tok0 + q) * ld_qkv + q_off + h * D +
                                                         ks * 32 + fg * 8);
       else
-        qf[qt][ks] = bf16x8{};
+        qf[qt][ks] = frag8{};
     }
   }
 
@@ -106,8 +120,8 @@ attn_fwd_kernel(const bf16* __restrict__ qkv, int ld_qkv, int q_off, int k_off, 
     for (int i = 0; i < KB * C::CPR / 256; ++i) {
       const int qd = tid + 256 * i, row = qd & (KB - 1), c = qd / KB;
       const int key = key0 + row;
-      bf16x8 v = bf16x8{};
-      if (key < S) v = *reinterpret_cast<const bf16x8*>(qkv + (tok0 + key) * ld_qkv + v_off + hk * D + c * 8);
+      frag8 v = frag8{};
+      if (key < S) v = *reinterpret_cast<const frag8*>(qkv + (tok0 + key) * ld_qkv + v_off + hk * D + c * 8);
 #pragma unroll
       for (int j = 0; j < 8; ++j) Vt[(c * 8 + j) * C::VT_LD + row] = v[j];
     }
@@ -120,9 +134,9 @@ attn_fwd_kernel(const bf16* __restrict__ qkv, int ld_qkv, int q_off, int k_off, 
       s[kt][0] = s[kt][1] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int ks = 0; ks < NKS; ++ks) {
-        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(Ks + kswz<C::CPR>(kt * 16 + fr, ks * 4 + fg));
-        s[kt][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[0][ks], s[kt][0], 0, 0, 0);
-        s[kt][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[1][ks], s[kt][1], 0, 0, 0);
+        const frag8 kf = *reinterpret_cast<const frag8*>(Ks + kswz<C::CPR>(kt * 16 + fr, ks * 4 + fg));
+        s[kt][0] = mma16<T>(kf, qf[0][ks], s[kt][0]);
+        s[kt][1] = mma16<T>(kf, qf[1][ks], s[kt][1]);
       }
     }
 
@@ -166,23 +180,23 @@ attn_fwd_kernel(const bf16* __restrict__ qkv, int ld_qkv, int q_off, int k_off, 
     // ---- O^T += V^T . P^T over 4 chunks of 32 keys ----
 #pragma unroll
     for (int c = 0; c < KB / 32; ++c) {
-      bf16x8 pf[2];
+      frag8 pf[2];
 #pragma unroll
       for (int qt = 0; qt < 2; ++qt) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          pf[qt][e] = (bf16)s[2 * c][qt][e];
-          pf[qt][4 + e] = (bf16)s[2 * c + 1][qt][e];
+          pf[qt][e] = (T)s[2 * c][qt][e];
+          pf[qt][4 + e] = (T)s[2 * c + 1][qt][e];
         }
       }
 #pragma unroll
       for (int dt = 0; dt < NDT; ++dt) {
-        const bf16* vr = Vt + (dt * 16 + fr) * C::VT_LD + c * 32 + fg * 4;
-        const bf16x4 lo = *reinterpret_cast<const bf16x4*>(vr);
-        const bf16x4 hi = *reinterpret_cast<const bf16x4*>(vr + 16);
-        const bf16x8 vf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        o[dt][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[0], o[dt][0], 0, 0, 0);
-        o[dt][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[1], o[dt][1], 0, 0, 0);
+        const T* vr = Vt + (dt * 16 + fr) * C::VT_LD + c * 32 + fg * 4;
+        const frag4 lo = *reinterpret_cast<const frag4*>(vr);
+        const frag4 hi = *reinterpret_cast<const frag4*>(vr + 16);
+        const frag8 vf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        o[dt][0] = mma16<T>(vf, pf[0], o[dt][0]);
+        o[dt][1] = mma16<T>(vf, pf[1], o[dt][1]);
       }
     }
   }
@@ -196,17 +210,17 @@ attn_fwd_kernel(const bf16* __restrict__ qkv, int ld_qkv, int q_off, int k_off, 
     const float inv = l > 0.f ? 1.f / l : 0.f;
     const int q = q0 + qt * 16 + fr;
     if (q >= S) continue;
-    bf16* op = out + (tok0 + q) * ld_out + h * D;
+    T* op = out + (tok0 + q) * ld_out + h * D;
 #pragma unroll
     for (int dt = 0; dt < NDT; ++dt) {
-      const bf16x4 v = {(bf16)(o[dt][qt][0] * inv), (bf16)(o[dt][qt][1] * inv),
-                        (bf16)(o[dt][qt][2] * inv), (bf16)(o[dt][qt][3] * inv)};
-      *reinterpret_cast<bf16x4*>(op + dt * 16 + fg * 4) = v;
+      const frag4 v = {(T)(o[dt][qt][0] * inv), (T)(o[dt][qt][1] * inv),
+                       (T)(o[dt][qt][2] * inv), (T)(o[dt][qt][3] * inv)};
+      *reinterpret_cast<frag4*>(op + dt * 16 + fg * 4) = v;
     }
   }
 }
 
-void attn_fwd(uintptr_t qkv, int ld_qkv, int q_off, int k_off, int v_off, int B, int H, int Hkv,
+void attn_fwd(int dtype, uintptr_t qkv, int ld_qkv, int q_off, int k_off, int v_off, int B, int H, int Hkv,
               int S, int D, uintptr_t lens, int causal, uintptr_t out, int ld_out, float scale,
               uintptr_t stream) {
   if (H % Hkv != 0) throw std::invalid_argument("attn: H must be a multiple of Hkv");
@@ -216,14 +230,14 @@ void attn_fwd(uintptr_t qkv, int ld_qkv, int q_off, int k_off, int v_off, int B,
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   dim3 grid((S + 127) / 128, H, B), blk(256);
   const float sl2e = scale * 1.4426950408889634f;
-  if (D == 64)
-    hipLaunchKernelGGL((attn_fwd_kernel<64>), grid, blk, 0, s, (const bf16*)qkv, ld_qkv, q_off, k_off,
-                       v_off, H, Hkv, S, (const int*)lens, causal, (bf16*)out, ld_out, sl2e);
-  else if (D == 128)
-    hipLaunchKernelGGL((attn_fwd_kernel<128>), grid, blk, 0, s, (const bf16*)qkv, ld_qkv, q_off, k_off,
-                       v_off, H, Hkv, S, (const int*)lens, causal, (bf16*)out, ld_out, sl2e);
-  else
-    throw std::invalid_argument("attn: head dim must be 64 or 128");
+#define RDB_ATTN(T, DD)                                                                          \
+  hipLaunchKernelGGL((attn_fwd_kernel<T, DD>), grid, blk, 0, s, (const T*)qkv, ld_qkv, q_off, k_off, \
+                     v_off, H, Hkv, S, (const int*)lens, causal, (T*)out, ld_out, sl2e)
+  if (D != 64 && D != 128) throw std::invalid_argument("attn: head dim must be 64 or 128");
+  if (dtype == 0) { if (D == 64) RDB_ATTN(bf16, 64); else RDB_ATTN(bf16, 128); }
+  else if (dtype == 1) { if (D == 64) RDB_ATTN(f16, 64); else RDB_ATTN(f16, 128); }
+  else throw std::invalid_argument("attn: dtype must be bf16 or f16");
+#undef RDB_ATTN
   RDB_HIP_CHECK(hipGetLastError());
 }
 

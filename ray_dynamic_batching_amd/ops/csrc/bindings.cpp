@@ -18,7 +18,7 @@ void norm_fwd(int dtype, int mode, uintptr_t x, uintptr_t res, uintptr_t res_out
 void embed_ln_fwd(int dtype, uintptr_t ids, uintptr_t types, uintptr_t word, uintptr_t pos,
                   uintptr_t typ, uintptr_t gamma, uintptr_t beta, uintptr_t y, int tokens, int S,
                   int D, int vocab, float eps, uintptr_t stream);
-void attn_fwd(uintptr_t qkv, int ld_qkv, int q_off, int k_off, int v_off, int B, int H, int Hkv,
+void attn_fwd(int dtype, uintptr_t qkv, int ld_qkv, int q_off, int k_off, int v_off, int B, int H, int Hkv,
               int S, int D, uintptr_t lens, int causal, uintptr_t out, int ld_out, float scale,
               uintptr_t stream);
 void softmax_topk(uintptr_t x, int rows, int C, int k, uintptr_t probs, uintptr_t idx, uintptr_t stream);

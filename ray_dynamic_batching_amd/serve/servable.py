@@ -99,13 +99,21 @@ def _accepts_device(f) -> bool:
 
 
 def model_deployment(factory: Callable, name: str, *, max_batch_size: int = 32, batch_wait_timeout_s: float = 0.005,
-                     buckets: Optional[Sequence[int]] = None, pipeline_depth: int = 2, **deployment_options) -> Deployment:
+                     buckets: Optional[Sequence[int]] = None, pipeline_depth: int = 2, io_spec=None,
+                     **deployment_options) -> Deployment:
     """Declare a GPU servable-model deployment.  ``factory(device=...)`` returns a
     model exposing ``input_shape/input_dtype/output_shape/output_dtype`` and
-    ``forward(x[B, ...])``."""
+    ``forward(x[B, ...])``; ``io_spec`` (or ``factory.io_spec``) =
+    (input_shape, input_dtype, output_shape, output_dtype) lets the router encode
+    requests without instantiating the model (see models/factories.py)."""
+    if io_spec is not None:
+        factory.io_spec = tuple(io_spec)
     eng = dict(deployment_options.pop("engine", {}) or {})
     eng.setdefault("buckets", list(buckets) if buckets else None)
     eng.setdefault("pipeline_depth", pipeline_depth)
+    spec = getattr(factory, "io_spec", None)
+    if spec is not None and not eng.get("request_slot_bytes"):
+        eng["request_slot_bytes"] = TensorCodec(*spec).in_bytes
     d = deployment(_EagerServable, name=name, engine=eng, **deployment_options)
     d.servable = dict(factory=factory, max_batch_size=max_batch_size, batch_wait_timeout_s=batch_wait_timeout_s)
     return d
