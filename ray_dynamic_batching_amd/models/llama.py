@@ -156,6 +156,8 @@ class LlamaTP:
         x = self.hidden_states(ids)
         return self._next_token(x, ids.shape[0], ids.shape[1])
 
+    __call__ = forward
+
     def hidden_states(self, ids: torch.Tensor) -> torch.Tensor:
         if self.backend == "hip":
             return self._layers_hip(ids)
