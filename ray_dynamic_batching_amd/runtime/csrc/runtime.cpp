@@ -22,6 +22,7 @@
 #include <deque>
 #include <map>
 #include <random>
+#include <thread>
 #include <vector>
 
 namespace py = pybind11;
@@ -480,6 +481,97 @@ class LoadGen {
 // ---------------------------------------------------------------------------
 // Consumer: request side of a Python replica (generic @serve.batch path).
 // ---------------------------------------------------------------------------
+// Native fake replica: one thread per served queue pops up to `max_batch`
+// requests, optionally "computes" for service_us (+ per_item_us per request),
+// and completes each with the first `out_bytes` of its payload.  Used as the
+// FakeReplicaWrapper-style stand-in in router tests and to measure the
+// runtime's own request overhead without a GPU (bench/runtime_microbench.py).
+class EchoServer {
+ public:
+  EchoServer(JobHandle& jh, uint32_t replica, std::vector<uint32_t> queues, uint32_t max_batch,
+             double service_us, double per_item_us, uint32_t out_bytes)
+      : job_(jh.job()), replica_(replica), queues_(std::move(queues)), max_batch_(max_batch),
+        service_ns_((int64_t)(service_us * 1e3)), per_item_ns_((int64_t)(per_item_us * 1e3)),
+        out_bytes_(out_bytes) {}
+  ~EchoServer() { stop(); }
+  void start() {
+    if (!threads_.empty()) return;
+    stop_.store(false);
+    job_.replica(replica_)->status.store(RS_READY);
+    for (uint32_t q : queues_) threads_.emplace_back([this, q] { serve(q); });
+  }
+  void stop() {
+    stop_.store(true);
+    for (auto& t : threads_)
+      if (t.joinable()) t.join();
+    threads_.clear();
+  }
+  uint64_t served() const { return served_.load(); }
+
+ private:
+  void serve(uint32_t q) {
+    Ring r = job_.req_ring(q);
+    uint64_t pos = r.h->tail.load();
+    ReplicaState* rs = job_.replica(replica_);
+    QueueState* qs = job_.queue(q);
+    std::vector<SlotHeader*> batch;
+    while (!stop_.load(std::memory_order_relaxed) && !job_.hdr()->shutdown.load()) {
+      rs->heartbeat_ns.store(now_ns(), std::memory_order_relaxed);
+      batch.clear();
+      while (batch.size() < max_batch_) {
+        SlotHeader* s = r.peek(pos + batch.size());
+        if (!s) break;
+        batch.push_back(s);
+      }
+      if (batch.empty()) {
+        r.wait_for(pos, 1000000, 200);
+        continue;
+      }
+      const int64_t t0 = now_ns();
+      const int64_t work = service_ns_ + per_item_ns_ * (int64_t)batch.size();
+      while (work > 0 && now_ns() - t0 < work) {}
+      for (SlotHeader* s : batch) {
+        Ring c = job_.cmp_ring(s->client);
+        uint64_t cpos;
+        SlotHeader* o;
+        while ((o = c.reserve(&cpos)) == nullptr) {
+          if (stop_.load() || job_.hdr()->shutdown.load()) return;
+          std::this_thread::yield();
+        }
+        const uint32_t n = std::min<uint32_t>({s->len, out_bytes_, c.max_payload()});
+        o->req_id = s->req_id;
+        o->t_submit_ns = s->t_submit_ns;
+        o->deadline_ns = 0;
+        o->len = n;
+        o->kind = 0;
+        o->client = s->client;
+        o->queue = q;
+        o->status = ST_OK;
+        o->t_aux_ns = now_ns();
+        if (n) memcpy(c.payload(o), r.payload(s), n);
+        qs->completed.fetch_add(1, std::memory_order_relaxed);
+        qs->hist_e2e.record((uint64_t)std::max<int64_t>(0, o->t_aux_ns - s->t_submit_ns));
+        c.publish(o, cpos);
+      }
+      pos += batch.size();
+      r.commit(pos);
+      rs->batches.fetch_add(1, std::memory_order_relaxed);
+      rs->batch_items.fetch_add(batch.size(), std::memory_order_relaxed);
+      rs->hist_batch_size.record(batch.size());
+      served_.fetch_add(batch.size(), std::memory_order_relaxed);
+    }
+  }
+  Job& job_;
+  uint32_t replica_;
+  std::vector<uint32_t> queues_;
+  uint32_t max_batch_;
+  int64_t service_ns_, per_item_ns_;
+  uint32_t out_bytes_;
+  std::atomic<bool> stop_{false};
+  std::atomic<uint64_t> served_{0};
+  std::vector<std::thread> threads_;
+};
+
 class Consumer {
  public:
   Consumer(JobHandle& jh, std::vector<uint32_t> queues) : job_(jh.job()), queues_(std::move(queues)) {
@@ -628,6 +720,15 @@ PYBIND11_MODULE(_rdb_runtime, m) {
       .def("info", &JobHandle::info)
       .def("base", &JobHandle::base)
       .def("request_region", &JobHandle::request_region);
+
+  py::class_<EchoServer>(m, "EchoServer")
+      .def(py::init<JobHandle&, uint32_t, std::vector<uint32_t>, uint32_t, double, double, uint32_t>(),
+           py::arg("job"), py::arg("replica"), py::arg("queues"), py::arg("max_batch") = 32,
+           py::arg("service_us") = 0.0, py::arg("per_item_us") = 0.0, py::arg("out_bytes") = 8,
+           py::keep_alive<1, 2>())
+      .def("start", &EchoServer::start)
+      .def("stop", &EchoServer::stop, py::call_guard<py::gil_scoped_release>())
+      .def("served", &EchoServer::served);
 
   py::class_<Client>(m, "Client")
       .def(py::init<JobHandle&, int, uint64_t>(), py::arg("job"), py::arg("client_id") = -1,

@@ -47,3 +47,10 @@ def LoadGen(client, model: int, payloads):
 
 def Consumer(job, queues):
     return load_runtime().Consumer(job, list(queues))
+
+
+def EchoServer(job, replica: int, queues, max_batch: int = 32, service_us: float = 0.0, per_item_us: float = 0.0,
+               out_bytes: int = 8):
+    """Native fake replica (C++ threads): batches up to ``max_batch`` requests per
+    queue, busy-waits ``service_us + per_item_us*B`` and echoes ``out_bytes``."""
+    return load_runtime().EchoServer(job, replica, list(queues), max_batch, service_us, per_item_us, out_bytes)

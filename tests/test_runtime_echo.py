@@ -1,0 +1,77 @@
+"""Native fake replicas (EchoServer) driving the C++ router/load generator:
+pow-2 routing by shm queue depth, batching under load, and the runtime
+microbenchmark (request-path overhead without a GPU)."""
+import os
+import subprocess
+import sys
+
+from ray_dynamic_batching_amd.runtime import job as rjob
+
+
+def _job(nq, **kw):
+    j = rjob.Job(rjob.unique_job_name("echo"), create=True, n_replicas=nq, n_queues=nq, n_clients=2,
+                 req_capacity=1024, req_slot_bytes=256, cmp_capacity=2048, cmp_slot_bytes=64, **kw)
+    for q in range(nq):
+        j.configure_queue(q, q, 0, 1024, 0.0, True)
+    return j
+
+
+def test_echo_roundtrip_payload():
+    j = _job(1)
+    s = rjob.EchoServer(j, 0, [0], max_batch=8, out_bytes=16)
+    s.start()
+    try:
+        c = rjob.Client(j, 0)
+        rids = {c.submit(0, bytes([i]) * 32): i for i in range(50)}
+        got = {}
+        while len(got) < 50:
+            for rid, st, q, ts, td, tr, kind, payload in c.poll(64, 1.0):
+                assert st == 0
+                got[rids[rid]] = payload
+        assert all(got[i] == bytes([i]) * 16 for i in range(50))
+        assert s.served() == 50
+    finally:
+        s.stop()
+        j.close()
+
+
+def test_pow2_routing_prefers_less_loaded_replica():
+    j = _job(2)
+    fast = rjob.EchoServer(j, 0, [0], max_batch=16, service_us=50.0)
+    slow = rjob.EchoServer(j, 1, [1], max_batch=16, service_us=3000.0)
+    fast.start()
+    slow.start()
+    try:
+        c = rjob.Client(j, 0)
+        lg = rjob.LoadGen(c, 0, [b"x" * 64])
+        res = lg.run(4000, 64, 0.0, 0.0, True, 60.0)
+        assert res["ok"] == 4000
+        assert fast.served() > 3 * slow.served(), (fast.served(), slow.served())
+    finally:
+        fast.stop()
+        slow.stop()
+        j.close()
+
+
+def test_batches_form_under_load():
+    j = _job(1)
+    s = rjob.EchoServer(j, 0, [0], max_batch=32, service_us=500.0)
+    s.start()
+    try:
+        c = rjob.Client(j, 0)
+        lg = rjob.LoadGen(c, 0, [b"y" * 64])
+        res = lg.run(3000, 128, 0.0, 0.0, True, 60.0)
+        assert res["ok"] == 3000
+        st = j.replica_stats(0)
+        assert st["batch_items"] / st["batches"] > 16
+    finally:
+        s.stop()
+        j.close()
+
+
+def test_runtime_microbench_runs():
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = subprocess.run([sys.executable, os.path.join(root, "bench", "runtime_microbench.py"), "--total", "5000",
+                          "--queues", "2"], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    assert "1:1 sync" in out.stdout and "serve path" in out.stdout
