@@ -43,6 +43,7 @@ def parse():
     ap.add_argument("--seq", type=int, default=128)
     ap.add_argument("--backend", default="hip", choices=["hip", "torch"])
     ap.add_argument("--pipeline-depth", type=int, default=2)
+    ap.add_argument("--compute-streams", type=int, default=1, help="batches executing concurrently per GPU")
     ap.add_argument("--layers", type=int, default=12)
     ap.add_argument("--json-out", default="")
     return ap.parse_args()
@@ -85,7 +86,8 @@ def main():
     cfg = BertConfig(seq_len=args.seq, layers=args.layers)
     model = BertForSequenceClassification(cfg, device="cuda", backend=args.backend)
     spec = SessionSpec(model=model, queue=rank, max_batch=args.max_batch, max_wait_s=args.max_wait_ms / 1e3)
-    runner = EngineRunner(name, rank, [spec], pipeline_depth=args.pipeline_depth).build()
+    runner = EngineRunner(name, rank, [spec], pipeline_depth=args.pipeline_depth,
+                          compute_streams=args.compute_streams).build()
     runner.start()
     barrier()
 

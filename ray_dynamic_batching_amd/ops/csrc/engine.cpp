@@ -29,6 +29,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <deque>
 #include <mutex>
@@ -68,9 +69,23 @@ struct Session {
   std::vector<uintptr_t> in_dev;                     // [slot]
   Ring ring;
   uint64_t peek_pos = 0;                             // next unread position
-  // duty-cycle mode (Nexus): share of the cycle, ms
-  double duty_share = 0.0;
+  // duty-cycle mode (Nexus): GPU time this session may use per cycle
+  int64_t duty_share_ns = 0;
+  int64_t used_ns = 0;                               // charged in the current cycle
+  std::atomic<bool> active{true};                    // model loaded / unloaded by the planner
+  Session() = default;
+  Session(Session&& o) noexcept { *this = std::move(o); }
+  Session& operator=(Session&& o) noexcept {
+    queue = o.queue; max_batch = o.max_batch; max_wait_ns = o.max_wait_ns; buckets = std::move(o.buckets);
+    in_row_bytes = o.in_row_bytes; out_row_bytes = o.out_row_bytes; priority = o.priority; slo_ns = o.slo_ns;
+    drop_stale = o.drop_stale; est_ns = std::move(o.est_ns); graphs = std::move(o.graphs);
+    out_dev = std::move(o.out_dev); in_dev = std::move(o.in_dev); ring = o.ring; peek_pos = o.peek_pos;
+    duty_share_ns = o.duty_share_ns; used_ns = o.used_ns; active.store(o.active.load());
+    return *this;
+  }
 };
+
+enum Policy { POLICY_PRIORITY_EDF = 0, POLICY_DUTY_CYCLE = 1 };
 
 struct InFlight {
   int session = -1;
@@ -85,15 +100,22 @@ struct InFlight {
 class Engine {
  public:
   Engine(const std::string& job_name, uint32_t replica, int pipeline_depth, bool zero_copy,
-         int device, int policy)
+         int device, int policy, int compute_streams)
       : replica_(replica), depth_(std::max(1, pipeline_depth)), zero_copy_(zero_copy),
         device_(device), policy_(policy) {
+    if (policy != POLICY_PRIORITY_EDF && policy != POLICY_DUTY_CYCLE)
+      throw std::invalid_argument("policy must be 0 (priority/EDF) or 1 (duty cycle)");
+    const int ns = std::max(1, std::min(compute_streams, depth_));
     job_.attach(job_name, 30000000000LL);
     job_.set_unlink_on_close(false);
     if (replica_ >= job_.hdr()->n_replicas) throw std::out_of_range("replica index");
     ENG_CHECK(hipSetDevice(device_));
     ENG_CHECK(hipStreamCreateWithFlags(&copy_stream_, hipStreamNonBlocking));
-    ENG_CHECK(hipStreamCreateWithFlags(&compute_stream_, hipStreamNonBlocking));
+    for (int i = 0; i < ns; ++i) {
+      hipStream_t st;
+      ENG_CHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+      compute_streams_.push_back(st);
+    }
     if (zero_copy_) {
       auto reg = job_.request_region();
       host_base_ = reg.first;
@@ -123,7 +145,7 @@ class Engine {
     for (auto p : host_out_) hipHostFree(p);
     if (registered_) hipHostUnregister(job_.request_region().first);
     if (copy_stream_) hipStreamDestroy(copy_stream_);
-    if (compute_stream_) hipStreamDestroy(compute_stream_);
+    for (auto st : compute_streams_) hipStreamDestroy(st);
   }
 
   int add_session(uint32_t queue, int max_batch, double max_wait_s, std::vector<int> buckets,
@@ -172,7 +194,12 @@ class Engine {
     s.out_dev.at(bucket_idx).at(slot) = out_dev;
   }
   void set_latency_estimate(int sid, int bucket_idx, double ms) { sess(sid).est_ns.at(bucket_idx) = ms * 1e6; }
-  void set_duty_share(int sid, double ms) { sess(sid).duty_share = ms; }
+  // Nexus duty cycle (policy 1): every `cycle_ms` each session may use `share_ms`
+  // of GPU time (= occupancy x duty cycle); budgets reset at the cycle boundary.
+  void set_duty_share(int sid, double ms) { sess(sid).duty_share_ns = (int64_t)(ms * 1e6); }
+  void set_duty_cycle(double ms) { duty_cycle_ns_.store((int64_t)(ms * 1e6)); }
+  void set_session_active(int sid, bool on) { sess(sid).active.store(on); }
+  int compute_streams() const { return (int)compute_streams_.size(); }
   void set_max_batch(int sid, int b) {
     Session& s = sess(sid);
     if (b < 1 || b > s.buckets.back()) throw std::invalid_argument("max_batch out of range");
@@ -244,10 +271,12 @@ class Engine {
   }
   // Session choice: highest priority with work; ties -> earliest head deadline (EDF).
   int pick_session() {
+    if (policy_ == POLICY_DUTY_CYCLE) return pick_duty_cycle();
     int best = -1;
     int best_pri = INT32_MIN;
     int64_t best_dl = INT64_MAX;
     for (size_t i = 0; i < sessions_.size(); ++i) {
+      if (!sessions_[i].active.load(std::memory_order_relaxed)) continue;
       const int64_t dl = head_deadline(sessions_[i]);
       if (dl == INT64_MAX) continue;
       const int pri = sessions_[i].priority;
@@ -258,6 +287,38 @@ class Engine {
       }
     }
     return best;
+  }
+  // Duty-cycle policy (fork GPUWorker.execute_schedule, scheduler.py:525-588, with
+  // the cycle-end sleep sign fixed): round-robin over the active sessions; a
+  // session may launch while its charged GPU time in this cycle is below its
+  // share; once every session with work is out of budget the launcher idles to
+  // the cycle boundary, where budgets reset.  Sessions without a share
+  // (duty_share 0) are unconstrained (work-conserving fill).
+  int pick_duty_cycle() {
+    const int64_t cyc = duty_cycle_ns_.load(std::memory_order_relaxed);
+    const int64_t now = now_ns();
+    if (cyc > 0 && now - cycle_start_ns_ >= cyc) {
+      cycle_start_ns_ = cyc > 0 && now - cycle_start_ns_ < 2 * cyc ? cycle_start_ns_ + cyc : now;
+      for (auto& s : sessions_) s.used_ns = 0;
+    }
+    const size_t n = sessions_.size();
+    bool starved = false;
+    for (size_t k = 0; k < n; ++k) {
+      const size_t i = (rr_next_ + k) % n;
+      Session& s = sessions_[i];
+      if (!s.active.load(std::memory_order_relaxed) || !s.ring.peek(s.peek_pos)) continue;
+      if (cyc > 0 && s.duty_share_ns > 0 && s.used_ns >= s.duty_share_ns) {
+        starved = true;
+        continue;
+      }
+      rr_next_ = (i + 1) % n;
+      return (int)i;
+    }
+    if (starved) {  // everyone with work is out of budget: idle until the cycle boundary
+      const int64_t wait = cycle_start_ns_ + cyc - now_ns();
+      if (wait > 0) std::this_thread::sleep_for(std::chrono::nanoseconds(std::min<int64_t>(wait, 2000000)));
+    }
+    return -1;
   }
   void set_error(const std::string& e) {
     std::lock_guard<std::mutex> lk(mu_);
@@ -382,14 +443,16 @@ class Engine {
               ENG_CHECK(hipMemsetAsync(reinterpret_cast<char*>(in) + (size_t)n * s.in_row_bytes, 0,
                                        (size_t)(rows - n) * s.in_row_bytes, copy_stream_));
           }
+          hipStream_t cs = compute_streams_[slot % compute_streams_.size()];
           ENG_CHECK(hipEventRecord(ev_copy_[slot], copy_stream_));
-          ENG_CHECK(hipStreamWaitEvent(compute_stream_, ev_copy_[slot], 0));
-          ENG_CHECK(hipEventRecord(ev_start_[slot], compute_stream_));
-          ENG_CHECK(hipGraphLaunch(s.graphs[bi][slot], compute_stream_));
+          ENG_CHECK(hipStreamWaitEvent(cs, ev_copy_[slot], 0));
+          ENG_CHECK(hipEventRecord(ev_start_[slot], cs));
+          ENG_CHECK(hipGraphLaunch(s.graphs[bi][slot], cs));
           ENG_CHECK(hipMemcpyAsync(host_out_[sid * depth_ + slot],
                                    reinterpret_cast<void*>(s.out_dev[bi][slot]),
-                                   (size_t)n * s.out_row_bytes, hipMemcpyDeviceToHost, compute_stream_));
-          ENG_CHECK(hipEventRecord(ev_done_[slot], compute_stream_));
+                                   (size_t)n * s.out_row_bytes, hipMemcpyDeviceToHost, cs));
+          ENG_CHECK(hipEventRecord(ev_done_[slot], cs));
+          s.used_ns += (int64_t)s.est_ns[bi];
           padded_.fetch_add(rows - n, std::memory_order_relaxed);
         }
         f.t_launch = now_ns();
@@ -481,7 +544,11 @@ class Engine {
   bool registered_ = false;
   char* host_base_ = nullptr;
   char* dev_base_ = nullptr;
-  hipStream_t copy_stream_ = nullptr, compute_stream_ = nullptr;
+  hipStream_t copy_stream_ = nullptr;
+  std::vector<hipStream_t> compute_streams_;
+  std::atomic<int64_t> duty_cycle_ns_{0};
+  int64_t cycle_start_ns_ = 0;
+  size_t rr_next_ = 0;
   std::vector<hipEvent_t> ev_copy_, ev_start_, ev_done_;
   std::vector<void*> host_ptrs_, host_out_;
   std::vector<Session> sessions_;
@@ -501,9 +568,9 @@ class Engine {
 
 void register_engine(py::module_& m) {
   py::class_<Engine>(m, "Engine")
-      .def(py::init<const std::string&, uint32_t, int, bool, int, int>(), py::arg("job_name"),
+      .def(py::init<const std::string&, uint32_t, int, bool, int, int, int>(), py::arg("job_name"),
            py::arg("replica"), py::arg("pipeline_depth") = 2, py::arg("zero_copy") = true,
-           py::arg("device") = 0, py::arg("policy") = 0)
+           py::arg("device") = 0, py::arg("policy") = 0, py::arg("compute_streams") = 1)
       .def("add_session", &Engine::add_session, py::arg("queue"), py::arg("max_batch"),
            py::arg("max_wait_s"), py::arg("buckets"), py::arg("in_row_bytes"),
            py::arg("out_row_bytes"), py::arg("priority") = 0, py::arg("slo_ms") = 0.0,
@@ -512,6 +579,9 @@ void register_engine(py::module_& m) {
       .def("set_graph", &Engine::set_graph)
       .def("set_latency_estimate", &Engine::set_latency_estimate)
       .def("set_duty_share", &Engine::set_duty_share)
+      .def("set_duty_cycle", &Engine::set_duty_cycle)
+      .def("set_session_active", &Engine::set_session_active)
+      .def("compute_streams", &Engine::compute_streams)
       .def("set_max_batch", &Engine::set_max_batch)
       .def("set_max_wait", &Engine::set_max_wait)
       .def("start", &Engine::start, py::call_guard<py::gil_scoped_release>())

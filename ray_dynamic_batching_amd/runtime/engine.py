@@ -46,16 +46,27 @@ class SessionSpec:
 
 
 class EngineRunner:
+    POLICY_PRIORITY_EDF = 0
+    POLICY_DUTY_CYCLE = 1
+
     def __init__(self, job_name: str, replica: int, sessions: Sequence[SessionSpec], pipeline_depth: int = 2,
-                 zero_copy: bool = True, device: Optional[int] = None, warmup_iters: int = 2):
+                 zero_copy: bool = True, device: Optional[int] = None, warmup_iters: int = 2, policy: int = 0,
+                 compute_streams: int = 1):
+        """``policy``: 0 = priority then earliest-deadline-first across sessions
+        (co-located models, config 5); 1 = Nexus duty cycle (``set_duty_cycle`` +
+        per-session ``set_duty_share``).  ``compute_streams`` > 1 runs that many
+        batches concurrently (one hipGraph per pipeline slot, slot i on stream
+        i % n, separate graph memory pools per stream so they never alias)."""
         self.ops = require_gpu_ops()
         self.device = torch.cuda.current_device() if device is None else device
         self.job_name = job_name
         self.replica = replica
         self.depth = pipeline_depth
         self.sessions = list(sessions)
-        self.engine = self.ops.Engine(job_name, replica, pipeline_depth, zero_copy, self.device, 0)
-        self.pool = None
+        self.compute_streams = max(1, min(compute_streams, pipeline_depth))
+        self.engine = self.ops.Engine(job_name, replica, pipeline_depth, zero_copy, self.device, policy,
+                                      self.compute_streams)
+        self.pools = []
         self.capture_s = 0.0
         self.warmup_iters = warmup_iters
 
@@ -68,7 +79,7 @@ class EngineRunner:
     def build(self) -> "EngineRunner":
         t0 = time.perf_counter()
         dev = torch.device("cuda", self.device)
-        self.pool = torch.cuda.graph_pool_handle()
+        self.pools = [torch.cuda.graph_pool_handle() for _ in range(self.compute_streams)]
         for s in self.sessions:
             m = s.model
             buckets = sorted(set(s.buckets or default_buckets(s.max_batch)))
@@ -100,7 +111,7 @@ class EngineRunner:
             for bi, b in enumerate(buckets):
                 for slot in range(self.depth):
                     g = torch.cuda.CUDAGraph()
-                    with torch.cuda.graph(g, pool=self.pool):
+                    with torch.cuda.graph(g, pool=self.pools[slot % self.compute_streams]):
                         y = m.forward(s.inputs[slot][:b])
                     if not y.is_contiguous():
                         raise RuntimeError("servable model output must be contiguous")
@@ -124,6 +135,16 @@ class EngineRunner:
     def start(self):
         self.engine.start()
         return self
+
+    def set_duty_cycle(self, cycle_ms: float, shares_ms: Optional[Sequence[float]] = None):
+        """Nexus plan -> engine: duty cycle and per-session GPU-time shares (ms)."""
+        self.engine.set_duty_cycle(cycle_ms)
+        for s, share in zip(self.sessions, shares_ms or []):
+            self.engine.set_duty_share(s.sid, share)
+
+    def set_active(self, session: int, on: bool):
+        """Load/unload a model at a batch boundary (planner re-placement)."""
+        self.engine.set_session_active(self.sessions[session].sid, on)
 
     def stop(self):
         self.engine.stop()

@@ -84,3 +84,121 @@ def test_engine_stale_drop_with_deadline():
     finally:
         runner.stop()
         j.close()
+
+
+def _serve_all(c, rjob, q, payloads):
+    rids = {c.submit(q, p): i for i, p in enumerate(payloads)}
+    got = {}
+    while len(got) < len(rids):
+        for rid, st, qq, ts, td, tr, kind, payload in c.poll(256, 1.0):
+            assert st == 0, st
+            got[rids[rid]] = payload
+    return got
+
+
+def test_engine_concurrent_streams_match_single_stream():
+    from ray_dynamic_batching_amd.models.bert import BertConfig, BertForSequenceClassification
+    from ray_dynamic_batching_amd.runtime import job as rjob
+    from ray_dynamic_batching_amd.runtime.engine import EngineRunner, SessionSpec
+
+    m = BertForSequenceClassification(BertConfig.tiny(seq_len=64), device="cuda", backend="hip", seed=5)
+    name = rjob.unique_job_name("eng2s")
+    j = rjob.Job(name, create=True, n_replicas=1, n_queues=1, n_clients=1, req_slot_bytes=64 * 4, cmp_slot_bytes=64)
+    j.configure_queue(0, 0, 0, 1024, 0.0, True)
+    runner = EngineRunner(name, 0, [SessionSpec(model=m, queue=0, max_batch=8, max_wait_s=0.0005)],
+                          pipeline_depth=4, compute_streams=2).build()
+    assert runner.engine.compute_streams() == 2
+    runner.start()
+    try:
+        c = rjob.Client(j)
+        ids = m.example_input(200, seed=11).cpu()
+        got = _serve_all(c, rjob, 0, [ids[i].numpy().tobytes() for i in range(200)])
+        ref = m(ids.cuda()).cpu()
+        out = torch.stack([torch.tensor(struct.unpack("<2f", got[i])) for i in range(200)])
+        assert torch.allclose(out, ref, atol=2e-2, rtol=2e-2), (out - ref).abs().max()
+        assert runner.error() == ""
+    finally:
+        runner.stop()
+        j.close()
+
+
+def test_engine_colocated_sessions_duty_cycle_shares():
+    """Config 5 in miniature: two models on one GPU with per-model queues.  Under
+    the duty-cycle policy GPU time splits by the planned shares (15 vs 2 ms of
+    a 20 ms cycle), so the favoured queue drains while the other is throttled."""
+    from ray_dynamic_batching_amd.models.bert import BertConfig, BertForSequenceClassification
+    from ray_dynamic_batching_amd.runtime import job as rjob
+    from ray_dynamic_batching_amd.runtime.engine import EngineRunner, SessionSpec
+
+    ma = BertForSequenceClassification(BertConfig.tiny(seq_len=64), device="cuda", backend="hip", seed=1)
+    mb = BertForSequenceClassification(BertConfig.tiny(seq_len=64), device="cuda", backend="hip", seed=2)
+    name = rjob.unique_job_name("coloc")
+    n = 3000
+    j = rjob.Job(name, create=True, n_replicas=1, n_queues=2, n_clients=1, req_capacity=4096,
+                 req_slot_bytes=64 * 4, cmp_capacity=8192, cmp_slot_bytes=64)
+    j.configure_queue(0, 0, 0, 4096, 0.0, True)
+    j.configure_queue(1, 0, 1, 4096, 0.0, True)
+    runner = EngineRunner(name, 0, [SessionSpec(model=ma, queue=0, max_batch=16, max_wait_s=0.001),
+                                    SessionSpec(model=mb, queue=1, max_batch=16, max_wait_s=0.001)],
+                          policy=EngineRunner.POLICY_DUTY_CYCLE).build()
+    runner.set_duty_cycle(20.0, [15.0, 2.0])
+    try:
+        c = rjob.Client(j)
+        ids = ma.example_input(64, seed=3).cpu()
+        for i in range(n):
+            c.submit(0, ids[i % 64].numpy().tobytes())
+            c.submit(1, ids[i % 64].numpy().tobytes())
+        runner.start()
+        import time
+        seen = {0: 0, 1: 0}
+        qb_at_a_done = None
+        t_end = time.time() + 120
+        while seen[0] + seen[1] < 2 * n and time.time() < t_end:
+            for rid, st, q, ts, td, tr, kind, payload in c.poll(512, 0.5):
+                assert st == 0
+                seen[q] += 1
+            if qb_at_a_done is None and seen[0] == n:
+                qb_at_a_done = seen[1]
+        assert seen == {0: n, 1: n}
+        assert qb_at_a_done is not None and qb_at_a_done < n // 2, qb_at_a_done
+        assert runner.error() == ""
+    finally:
+        runner.stop()
+        j.close()
+
+
+def test_engine_priority_policy_prefers_high_priority_session():
+    from ray_dynamic_batching_amd.models.bert import BertConfig, BertForSequenceClassification
+    from ray_dynamic_batching_amd.runtime import job as rjob
+    from ray_dynamic_batching_amd.runtime.engine import EngineRunner, SessionSpec
+
+    m = BertForSequenceClassification(BertConfig.tiny(seq_len=64), device="cuda", backend="hip", seed=1)
+    name = rjob.unique_job_name("prio")
+    n = 2000
+    j = rjob.Job(name, create=True, n_replicas=1, n_queues=2, n_clients=1, req_capacity=4096,
+                 req_slot_bytes=64 * 4, cmp_capacity=8192, cmp_slot_bytes=64)
+    j.configure_queue(0, 0, 0, 4096, 0.0, True)
+    j.configure_queue(1, 0, 1, 4096, 0.0, True)
+    runner = EngineRunner(name, 0, [SessionSpec(model=m, queue=0, max_batch=16, max_wait_s=0.001, priority=0),
+                                    SessionSpec(model=m, queue=1, max_batch=16, max_wait_s=0.001, priority=5)]).build()
+    try:
+        c = rjob.Client(j)
+        ids = m.example_input(64, seed=3).cpu()
+        for i in range(n):
+            c.submit(0, ids[i % 64].numpy().tobytes())
+            c.submit(1, ids[i % 64].numpy().tobytes())
+        runner.start()
+        import time
+        seen = {0: 0, 1: 0}
+        low_at_high_done = None
+        t_end = time.time() + 120
+        while seen[0] + seen[1] < 2 * n and time.time() < t_end:
+            for rid, st, q, ts, td, tr, kind, payload in c.poll(512, 0.5):
+                seen[q] += 1
+            if low_at_high_done is None and seen[1] == n:
+                low_at_high_done = seen[0]
+        assert seen == {0: n, 1: n}
+        assert low_at_high_done is not None and low_at_high_done <= 64, low_at_high_done
+    finally:
+        runner.stop()
+        j.close()
