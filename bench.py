@@ -42,8 +42,8 @@ def parse():
     ap.add_argument("--rate", type=float, default=0.0, help="open-loop Poisson rate per GPU (req/s); 0 = closed loop")
     ap.add_argument("--seq", type=int, default=128)
     ap.add_argument("--backend", default="hip", choices=["hip", "torch"])
-    ap.add_argument("--pipeline-depth", type=int, default=2)
-    ap.add_argument("--compute-streams", type=int, default=1, help="batches executing concurrently per GPU")
+    ap.add_argument("--pipeline-depth", type=int, default=4)
+    ap.add_argument("--compute-streams", type=int, default=2, help="batches executing concurrently per GPU")
     ap.add_argument("--layers", type=int, default=12)
     ap.add_argument("--json-out", default="")
     return ap.parse_args()

@@ -81,6 +81,11 @@ def main(argv=None):
     done = loop.run_until_complete(run(a.requests, True))
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    pending = asyncio.all_tasks(loop)
+    for t in pending:
+        t.cancel()
+    loop.run_until_complete(asyncio.gather(*pending, return_exceptions=True))
+    loop.close()
     lat_ms = np.array(lat) * 1e3
     out = {"metric": "baseline req/s (1 GPU, Python @serve.batch + eager forward, no RPC)", "backend": a.backend,
            "value": round(done / dt, 2), "unit": "req/s", "p50_ms": float(np.percentile(lat_ms, 50)),

@@ -20,6 +20,7 @@
 // * Doorbells     : futex words in shm so an idle consumer sleeps and producers
 //                   wake it across processes (no busy polling when idle).
 #pragma once
+#include <algorithm>
 #include <atomic>
 #include <cerrno>
 #include <climits>
@@ -40,7 +41,8 @@ namespace rt {
 
 constexpr uint64_t kMagic = 0x3130424F4A424452ULL;  // "RDBJOB01"
 constexpr uint32_t kVersion = 3;
-constexpr int kHistBuckets = 320;
+constexpr int kHistSub = 32;       // sub-buckets per power of two (~3% wide)
+constexpr int kHistBuckets = 1280;  // covers values up to 2^44 ns
 
 inline int64_t now_ns() {
   timespec ts;
@@ -69,7 +71,7 @@ inline void futex_wake_all(std::atomic<uint32_t>* addr) {
 }
 
 // ---------------------------------------------------------------------------
-// Log-linear histogram: 8 sub-buckets per power of two of a nanosecond value
+// Log-linear histogram: 32 sub-buckets per power of two of a nanosecond value
 // (<= 12.5 % relative bucket width), range 1 ns .. ~2^40 ns.
 // ---------------------------------------------------------------------------
 struct Histogram {
@@ -79,18 +81,18 @@ struct Histogram {
   std::atomic<uint64_t> buckets[kHistBuckets];
 
   static int index(uint64_t v) {
-    if (v < 8) return (int)v;
-    const int e = 63 - __builtin_clzll(v);
-    int idx = (e - 2) * 8 + (int)((v >> (e - 3)) & 7);
+    if (v < (uint64_t)kHistSub) return (int)v;
+    const int e = 63 - __builtin_clzll(v);  // >= 5
+    int idx = (e - 4) * kHistSub + (int)((v >> (e - 5)) & (kHistSub - 1));
     return idx < kHistBuckets ? idx : kHistBuckets - 1;
   }
-  static double value_at(int idx) {  // bucket midpoint
-    if (idx < 8) return idx;
-    const int e = idx / 8 + 2, m = idx % 8;
-    const double lo = (double)(1ULL << e) * (1.0 + m / 8.0);
-    const double hi = (double)(1ULL << e) * (1.0 + (m + 1) / 8.0);
-    return 0.5 * (lo + hi);
+  static double lower(int idx) {
+    if (idx < kHistSub) return idx;
+    const int e = idx / kHistSub + 4, m = idx % kHistSub;
+    return (double)(1ULL << e) * (1.0 + (double)m / kHistSub);
   }
+  static double upper(int idx) { return idx < kHistSub ? idx + 1 : lower(idx + 1 < kHistBuckets ? idx + 1 : idx); }
+  static double value_at(int idx) { return 0.5 * (lower(idx) + upper(idx)); }
   void record(uint64_t v) {
     count.fetch_add(1, std::memory_order_relaxed);
     sum_ns.fetch_add(v, std::memory_order_relaxed);
@@ -110,8 +112,13 @@ struct Histogram {
     const double target = p / 100.0 * (double)n;
     uint64_t acc = 0;
     for (int i = 0; i < kHistBuckets; ++i) {
-      acc += buckets[i].load(std::memory_order_relaxed);
-      if ((double)acc >= target && acc > 0) return value_at(i);
+      const uint64_t c = buckets[i].load(std::memory_order_relaxed);
+      if (c && (double)(acc + c) >= target) {  // linear interpolation inside the bucket
+        const double f = std::min(1.0, std::max(0.0, (target - (double)acc) / (double)c));
+        const double v = lower(i) + f * (upper(i) - lower(i));
+        return std::min(v, (double)max_ns.load(std::memory_order_relaxed));
+      }
+      acc += c;
     }
     return (double)max_ns.load();
   }
