@@ -106,12 +106,14 @@ def build_ops(force: bool = False, jobs: int | None = None, verbose: bool = Fals
 
 def build_runtime(force: bool = False) -> Path:
     target = runtime_target()
-    srcs = [RT_SRC / "runtime.cpp"]
+    srcs = [RT_SRC / "runtime.cpp", RT_SRC / "node_agent.cpp"]
     if not force and not _stale(target, _deps(srcs, [RT_SRC])):
         return target
     cxx = os.environ.get("CXX", "g++")
     tmp = target.with_suffix(".tmp.so")
-    _run([cxx, "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", "-Wno-unused-function",
+    san = os.environ.get("RDB_SANITIZE", "")  # "address" / "thread" / "undefined" (host-code presets)
+    flags = ["-O1", "-g", "-fno-omit-frame-pointer", f"-fsanitize={san}"] if san else ["-O2"]
+    _run([cxx] + flags + ["-std=c++17", "-fPIC", "-shared", "-Wall", "-Wno-unused-function",
           "-fvisibility=hidden", f"-I{RT_SRC}"] + _pybind_includes() + [str(s) for s in srcs]
          + ["-o", str(tmp), "-lrt", "-pthread"])
     os.replace(tmp, target)

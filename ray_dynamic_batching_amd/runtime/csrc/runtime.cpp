@@ -173,32 +173,7 @@ class JobHandle {
   // are not left waiting (router then re-dispatches).
   uint64_t fail_queue(uint32_t q, uint32_t status) {
     check_q(q);
-    Ring ring = job_.req_ring(q);
-    QueueState* qs = job_.queue(q);
-    uint64_t pos = ring.h->tail.load();
-    uint64_t n = 0;
-    while (SlotHeader* s = ring.peek(pos)) {
-      Ring c = job_.cmp_ring(s->client);
-      uint64_t cpos;
-      SlotHeader* out = nullptr;
-      while ((out = c.reserve(&cpos)) == nullptr) usleep(100);
-      out->req_id = s->req_id;
-      out->t_submit_ns = s->t_submit_ns;
-      out->deadline_ns = s->deadline_ns;
-      out->len = 0;
-      out->kind = 0;
-      out->client = s->client;
-      out->queue = q;
-      out->status = status;
-      out->t_aux_ns = now_ns();
-      c.publish(out, cpos);
-      ++pos;
-      ++n;
-    }
-    ring.commit(pos);
-    qs->completed.fetch_add(n);
-    qs->errors.fetch_add(n);
-    return n;
+    return fail_pending(job_, q, status);
   }
   py::dict info() {
     JobHeader* h = job_.hdr();
@@ -675,6 +650,10 @@ class Consumer {
 
 }  // namespace
 
+namespace rdb {
+void register_node_agent(py::module_& m);
+}
+
 PYBIND11_MODULE(_rdb_runtime, m) {
   m.doc() = "ray_dynamic_batching_amd native host runtime (shm rings, router, load generator)";
   m.attr("ST_OK") = (int)ST_OK;
@@ -786,4 +765,5 @@ PYBIND11_MODULE(_rdb_runtime, m) {
       .def("complete", &Consumer::complete, py::arg("client"), py::arg("req_id"), py::arg("queue"),
            py::arg("status"), py::arg("t_submit_ns"), py::arg("payload"), py::arg("kind") = 0)
       .def("record_batch", &Consumer::record_batch);
+  rdb::register_node_agent(m);
 }

@@ -461,5 +461,38 @@ class Job {
   bool unlink_on_close_ = true;
 };
 
+// Complete every request still in queue q's ring (unconsumed, or consumed but
+// not yet committed by a replica that died) with `status`, so its clients can
+// retry elsewhere.  Used by the router on drain and by the node agent when a
+// replica process dies or stops heart-beating.
+inline uint64_t fail_pending(Job& job, uint32_t q, uint32_t status) {
+  Ring ring = job.req_ring(q);
+  QueueState* qs = job.queue(q);
+  uint64_t pos = ring.h->tail.load();
+  uint64_t n = 0;
+  while (SlotHeader* s = ring.peek(pos)) {
+    Ring c = job.cmp_ring(s->client);
+    uint64_t cpos;
+    SlotHeader* out = nullptr;
+    while ((out = c.reserve(&cpos)) == nullptr) usleep(100);
+    out->req_id = s->req_id;
+    out->t_submit_ns = s->t_submit_ns;
+    out->deadline_ns = s->deadline_ns;
+    out->len = 0;
+    out->kind = 0;
+    out->client = s->client;
+    out->queue = q;
+    out->status = status;
+    out->t_aux_ns = now_ns();
+    c.publish(out, cpos);
+    ++pos;
+    ++n;
+  }
+  ring.commit(pos);
+  qs->completed.fetch_add(n);
+  qs->errors.fetch_add(n);
+  return n;
+}
+
 }  // namespace rt
 }  // namespace rdb

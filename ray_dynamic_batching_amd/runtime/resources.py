@@ -112,6 +112,10 @@ def detect_num_gpus() -> int:
 
 def visible_devices_env(gpus: List[int]) -> Dict[str, str]:
     """Environment that pins a replica process to its GPUs (reference:
-    _private/accelerators/amd_gpu.py:99-107 sets ROCR_VISIBLE_DEVICES)."""
+    _private/accelerators/amd_gpu.py:99-107 sets ROCR_VISIBLE_DEVICES).  The
+    native node agent (runtime/csrc/node_agent.cpp) owns the live allocator;
+    the Python GpuAllocator above is the reference model its tests pin."""
+    # Only HIP_VISIBLE_DEVICES: it indexes the devices ROCR already exposes, so an
+    # inherited ROCR_VISIBLE_DEVICES (e.g. from a cluster scheduler) keeps working.
     v = ",".join(str(g) for g in gpus)
-    return {"HIP_VISIBLE_DEVICES": v, "ROCR_VISIBLE_DEVICES": v} if gpus else {"HIP_VISIBLE_DEVICES": "", "RDB_NO_GPU": "1"}
+    return {"HIP_VISIBLE_DEVICES": v} if gpus else {"HIP_VISIBLE_DEVICES": "", "RDB_NO_GPU": "1"}

@@ -35,6 +35,36 @@ def _serve_until(duration: float) -> None:
         api.shutdown()
 
 
+def _status(sock: str, kv: str) -> dict:
+    """Live status from the node agent's control socket (processes, GPU slots,
+    last checkpointed config); falls back to a checkpoint file."""
+    import os
+
+    from .controller import discovery_file
+
+    if not sock and not kv:
+        try:
+            with open(discovery_file()) as f:
+                sock = json.load(f).get("socket", "")
+        except (OSError, ValueError):
+            sock = ""
+    if sock and os.path.exists(sock):
+        from ..runtime import agent as ragent
+
+        try:
+            st = ragent.status(sock)
+            ck = ragent.request(sock, "KV_GET serve/checkpoint")
+            st["checkpoint"] = json.loads(ck[3:]) if ck.startswith("OK ") else None
+            return st
+        except (RuntimeError, ValueError):
+            pass
+    try:
+        with open(kv or "serve_kv.json") as f:
+            return json.load(f)
+    except (OSError, ValueError):
+        return {"applications": {}}
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser(prog="serve")
     sub = ap.add_subparsers(dest="cmd", required=True)
@@ -52,7 +82,8 @@ def main(argv=None) -> int:
     c = sub.add_parser("config")
     c.add_argument("config")
     s = sub.add_parser("status")
-    s.add_argument("--kv", default="serve_kv.json")
+    s.add_argument("--kv", default="", help="checkpoint file (default: ask the running node agent)")
+    s.add_argument("--socket", default="", help="node agent control socket (default: discovered)")
     a = ap.parse_args(argv)
 
     from .schema import ServeApplicationSchema, ServeDeploySchema, build_application, deploy_config, import_attr
@@ -85,10 +116,7 @@ def main(argv=None) -> int:
         sch = ServeDeploySchema.from_yaml(a.config)
         print(yaml.safe_dump(sch.model_dump(mode="json"), sort_keys=False))
     elif a.cmd == "status":
-        try:
-            print(open(a.kv).read())
-        except OSError:
-            print(json.dumps({"applications": {}}))
+        print(json.dumps(_status(a.socket, a.kv), indent=1))
     return 0
 
 

@@ -125,3 +125,10 @@ class DeploymentConfig(BaseModel):
     @property
     def num_gpus(self) -> float:
         return float(self.ray_actor_options.get("num_gpus", 0) or 0)
+
+    @property
+    def hbm_gb(self) -> float:
+        """HBM the replica reserves on its GPU(s) for placement (ray_actor_options
+        ``memory_gb`` / ``hbm_gb``; 0 = unconstrained)."""
+        o = self.ray_actor_options
+        return float(o.get("hbm_gb", o.get("memory_gb", 0)) or 0)

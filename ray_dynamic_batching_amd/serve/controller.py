@@ -5,13 +5,16 @@ Reference parity:
   deployment state update, health checks, autoscaling;
 * DeploymentState replica state machine (deployment_state.py): start, health-check,
   restart dead replicas, scale up/down, graceful drain;
-* raylet worker pool + GPU allocation (node_manager / worker_pool /
-  resource_instance_set.cc): replica PROCESSES pinned to GPUs with
-  HIP_VISIBLE_DEVICES, GPU slots from runtime.resources.GpuAllocator;
-* GCS health checks / actor restarts (gcs_health_check_manager.cc): heartbeats
-  in the shm job segment, exponential restart back-off;
+* raylet worker pool + GPU allocation + GCS health checks / actor restarts
+  (node_manager / worker_pool / resource_instance_set.cc /
+  gcs_health_check_manager.cc / gcs_actor_manager.cc) are the NATIVE node agent
+  (runtime/csrc/node_agent.cpp): it owns the GPU slots, spawns the replica
+  PROCESSES pinned with HIP_VISIBLE_DEVICES, watches exit status + shm
+  heartbeats, fails a dead replica's pending requests, bumps its generation and
+  restarts it with exponential back-off;
 * config checkpoint (controller.py:510-563 KV): the last applied application
-  config is written to a JSON KV file and can be restored.
+  config is written to the agent's persistent KV (and a JSON file for the CLI);
+  the agent also answers PING/STATUS/KV_* on a Unix socket.
 """
 from __future__ import annotations
 
@@ -19,7 +22,6 @@ import atexit
 import json
 import logging
 import os
-import subprocess
 import sys
 import tempfile
 import threading
@@ -40,6 +42,10 @@ logger = logging.getLogger("ray_dynamic_batching_amd.serve")
 
 _CONTROLLER: Optional["ServeController"] = None
 _CTRL_LOCK = threading.Lock()
+
+
+def discovery_file() -> str:
+    return os.environ.get("RDB_SERVE_DISCOVERY", os.path.join(tempfile.gettempdir(), f"rdb_serve_{os.getuid()}.json"))
 
 
 def get_controller(create: bool = True) -> Optional["ServeController"]:
@@ -78,7 +84,7 @@ def lookup_router(app_name: str, deployment: str):
 @dataclass
 class ProcReplica:
     slot: int                 # replica index in the job segment (== queue id)
-    proc: Optional[subprocess.Popen] = None
+    proc_id: int = -1         # node-agent process handle
     alloc: Any = None
     started_at: float = 0.0
     ready: bool = False
@@ -112,15 +118,23 @@ class DeploymentState:
 
 class ServeController:
     def __init__(self):
-        from ..runtime.resources import GpuAllocator
+        from ..runtime import agent as ragent
+        from ..runtime.resources import detect_num_gpus
 
         self.apps: Dict[str, Dict[str, DeploymentState]] = {}
         self.ingress: Dict[str, str] = {}
         self.jobs: Dict[str, Any] = {}            # app -> job segment handle (process mode)
-        self.allocator = GpuAllocator()
         self.lock = threading.RLock()
         self.workdir = tempfile.mkdtemp(prefix="rdb_serve_")
         self.kv_path = os.environ.get("RDB_SERVE_KV", os.path.join(self.workdir, "serve_kv.json"))
+        self.agent = ragent.NodeAgent(detect_num_gpus(), 0.0, os.path.join(self.workdir, "agent_kv.bin"))
+        self.agent_socket = os.path.join(self.workdir, "agent.sock")
+        try:
+            self.agent.serve(self.agent_socket)
+            with open(discovery_file(), "w") as f:   # lets `serve status` find the live agent
+                json.dump(dict(pid=os.getpid(), socket=self.agent_socket, kv=self.kv_path), f)
+        except (RuntimeError, OSError):  # pragma: no cover - control RPC is optional
+            self.agent_socket = ""
         self.default_mode = os.environ.get("RDB_SERVE_MODE", "auto")
         self._stop = threading.Event()
         self._thread = threading.Thread(target=self._control_loop, name="rdb-serve-controller", daemon=True)
@@ -237,26 +251,27 @@ class ServeController:
         from ..runtime.resources import visible_devices_env
 
         owner = f"{st.app_name}#{st.name}#{rep.slot}"
-        self.allocator.release(owner)
-        alloc = self.allocator.allocate(owner, st.config.num_gpus)
+        self.agent.release(owner)
+        alloc = self.agent.allocate(owner, float(st.config.num_gpus), float(st.config.hbm_gb or 0.0))
         if alloc is None:
             logger.warning("no GPU capacity for %s (num_gpus=%s)", owner, st.config.num_gpus)
             return False
         rep.alloc = alloc
+        gpus = list(alloc["gpus"])
         job = self.jobs[st.app_name]
         job.configure_queue(rep.slot, rep.slot, st.model_id, st.config.max_ongoing_requests,
                             float(st.config.slo_ms or 0.0), True)
-        job.set_replica_status(rep.slot, 1, alloc.gpus[0] if alloc.gpus else -1, 0)
-        env = dict(os.environ)
-        env.update(visible_devices_env(alloc.gpus))
+        job.set_replica_status(rep.slot, 1, gpus[0] if gpus else -1, 0)
+        env = dict(visible_devices_env(gpus))
         env["RDB_ROUTING_TABLE"] = self._routes_path
-        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
         pkg_root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-        env["PYTHONPATH"] = pkg_root + os.pathsep + env.get("PYTHONPATH", "")
+        env["PYTHONPATH"] = pkg_root + os.pathsep + os.environ.get("PYTHONPATH", "")
         cmd = [sys.executable, "-m", "ray_dynamic_batching_amd.serve.replica_main", "--spec", st.spec_path,
-               "--replica", str(rep.slot), "--gpu", ",".join(map(str, alloc.gpus))]
-        log = open(os.path.join(self.workdir, f"{owner.replace('#', '.')}.log"), "ab")
-        rep.proc = subprocess.Popen(cmd, env=env, stdout=log, stderr=subprocess.STDOUT)
+               "--replica", str(rep.slot), "--gpu", ",".join(map(str, gpus))]
+        log = os.path.join(self.workdir, f"{owner.replace('#', '.')}.log")
+        rep.proc_id = self.agent.spawn(owner, cmd, env, log, job.info()["name"], rep.slot, [rep.slot],
+                                       float(st.config.health_check_timeout_s), -1, 0.5, 30.0)
         rep.started_at = time.time()
         rep.ready = False
         rep.health_failures = 0
@@ -311,9 +326,11 @@ class ServeController:
                     if job.replica_status(rep.slot) == 2:
                         rep.ready = True
                         break
-                    if rep.proc is not None and rep.proc.poll() is not None:
-                        raise RayServeException(f"replica {st.name}#{rep.slot} exited during startup "
-                                                f"(code {rep.proc.returncode}); log: {self.workdir}")
+                    if rep.proc_id >= 0:
+                        info = self.agent.info(rep.proc_id)
+                        if info["restarts"] > 0 or info["state"] in ("EXITED", "STOPPED"):
+                            raise RayServeException(f"replica {st.name}#{rep.slot} exited during startup "
+                                                    f"({info['last_exit']}); log: {self.workdir}")
                     time.sleep(0.02)
                 else:
                     raise RayServeException(f"replica {st.name}#{rep.slot} did not become ready")
@@ -329,15 +346,12 @@ class ServeController:
             deadline = time.time() + st.config.graceful_shutdown_timeout_s
             while time.time() < deadline and job.queue_depth(rep.slot) > 0:
                 time.sleep(st.config.graceful_shutdown_wait_loop_s / 20)
-            if rep.proc is not None and rep.proc.poll() is None:
-                rep.proc.terminate()
-                try:
-                    rep.proc.wait(5)
-                except subprocess.TimeoutExpired:
-                    rep.proc.kill()
+            if rep.proc_id >= 0:
+                self.agent.terminate(rep.proc_id, 5.0)
+                self.agent.forget(rep.proc_id)
             job.fail_queue(rep.slot, 6)
             job.set_replica_status(rep.slot, 4, -1, 0)
-            self.allocator.release(f"{st.app_name}#{st.name}#{rep.slot}")
+            self.agent.release(f"{st.app_name}#{st.name}#{rep.slot}")
             with self.lock:
                 if rep in st.proc_replicas:
                     st.proc_replicas.remove(rep)
@@ -380,30 +394,17 @@ class ServeController:
         job = self.jobs.get(st.app_name)
         if job is None:
             return
+        # the native agent restarts dead / silent replicas itself; here we only
+        # track readiness and surface its events in the log
         for rep in list(st.proc_replicas):
-            if rep.draining:
+            if rep.draining or rep.proc_id < 0:
                 continue
-            status = job.replica_status(rep.slot)
-            if status == 2:
-                rep.ready = True
-            died = rep.proc is not None and rep.proc.poll() is not None
-            stale = rep.ready and job.heartbeat_age_s(rep.slot) > st.config.health_check_timeout_s
-            if died or stale or status == 4:
-                if rep.next_restart_at == 0.0:
-                    logger.warning("replica %s#%d %s; restarting", st.name, rep.slot,
-                                   "died" if died else "missed heartbeats")
-                    if rep.proc is not None and rep.proc.poll() is None:
-                        rep.proc.kill()
-                    job.set_replica_status(rep.slot, 4, -1, 0)
-                    job.fail_queue(rep.slot, 6)   # REPLICA_DIED -> clients retry elsewhere
-                    job.bump_restarts(rep.slot)
-                    rep.restarts += 1
-                    backoff = min(30.0, 0.5 * (2 ** min(rep.restarts - 1, 6)))
-                    rep.next_restart_at = now + backoff
-                    rep.ready = False
-                elif now >= rep.next_restart_at:
-                    rep.next_restart_at = 0.0
-                    self._spawn(st, rep)
+            info = self.agent.info(rep.proc_id)
+            rep.restarts = info["restarts"]
+            rep.ready = job.replica_status(rep.slot) == 2 and info["state"] in ("STARTING", "RUNNING")
+        for pid, kind, msg in self.agent.events():
+            if kind in ("died", "exited", "spawn_failed"):
+                logger.warning("replica process %d %s: %s", pid, kind, msg)
 
     def _autoscale_tick(self, st: DeploymentState) -> None:
         if st.autoscaler is None:
@@ -479,15 +480,10 @@ class ServeController:
                 for r in st.local_replicas:
                     r.shutdown(st.config.graceful_shutdown_timeout_s)
                 for rep in st.proc_replicas:
-                    if rep.proc is not None and rep.proc.poll() is None:
-                        rep.proc.terminate()
-                for rep in st.proc_replicas:
-                    if rep.proc is not None:
-                        try:
-                            rep.proc.wait(10)
-                        except subprocess.TimeoutExpired:
-                            rep.proc.kill()
-                    self.allocator.release(f"{st.app_name}#{st.name}#{rep.slot}")
+                    if rep.proc_id >= 0:
+                        self.agent.terminate(rep.proc_id, 10.0)
+                        self.agent.forget(rep.proc_id)
+                    self.agent.release(f"{st.app_name}#{st.name}#{rep.slot}")
             job = self.jobs.pop(name, None)
             if job is not None:
                 from .router import ShmRouter
@@ -507,6 +503,12 @@ class ServeController:
             except Exception:  # pragma: no cover
                 logger.error("error deleting %s:\n%s", name, traceback.format_exc())
         self._stop.set()
+        if self._thread.is_alive() and threading.current_thread() is not self._thread:
+            self._thread.join(5.0)
+        try:
+            self.agent.shutdown(5.0)
+        except Exception:  # pragma: no cover
+            pass
         with _CTRL_LOCK:
             if _CONTROLLER is self:
                 _CONTROLLER = None
@@ -518,10 +520,12 @@ class ServeController:
         for app_name, states in self.apps.items():
             data[app_name] = dict(ingress=self.ingress.get(app_name),
                                   deployments={n: st.config.model_dump(mode="json") for n, st in states.items()})
+        blob = json.dumps(dict(version=1, time=time.time(), applications=data), default=str)
         try:
+            self.agent.kv_put("serve/checkpoint", blob.encode())
             tmp = self.kv_path + ".tmp"
             with open(tmp, "w") as f:
-                json.dump(dict(version=1, time=time.time(), applications=data), f, default=str)
+                f.write(blob)
             os.replace(tmp, self.kv_path)
         except OSError:  # pragma: no cover
             pass

@@ -196,6 +196,13 @@ class LocalReplica:
 
         async def _stop():
             self.user.destroy()
+            # cancel the @batch queue loops (and any other background tasks) so the
+            # loop stops with nothing pending
+            me = asyncio.current_task()
+            rest = [t for t in asyncio.all_tasks() if t is not me]
+            for t in rest:
+                t.cancel()
+            await asyncio.gather(*rest, return_exceptions=True)
         try:
             asyncio.run_coroutine_threadsafe(_stop(), self._loop).result(2)
         except Exception:  # pragma: no cover

@@ -39,3 +39,21 @@ def test_cli_build_and_run():
                          timeout=120)
     assert out.returncode == 0, out.stderr
     assert "HEALTHY" in out.stdout
+
+
+def test_cli_status_queries_live_node_agent(tmp_path):
+    from ray_dynamic_batching_amd import serve
+    from ray_dynamic_batching_amd.serve.cli import _status
+
+    disc = tmp_path / "disc.json"
+    os.environ["RDB_SERVE_DISCOVERY"] = str(disc)
+    try:
+        from examples.mlp_app import app
+
+        serve.run(app, mode="local")
+        st = _status("", "")
+        assert "procs" in st and "gpus" in st
+        assert "default" in st["checkpoint"]["applications"]
+    finally:
+        serve.shutdown()
+        os.environ.pop("RDB_SERVE_DISCOVERY", None)
