@@ -126,6 +126,11 @@ class Engine {
       registered_ = true;
     }
     slot_busy_.assign(depth_, false);
+    // fault-injection knobs (same variables as utils/faults.py)
+    auto knob = [](const char* n) { const char* v = getenv(n); return v ? atoll(v) : 0LL; };
+    fault_drop_every_ = knob("RDB_FAULT_DROP_EVERY");
+    fault_delay_batch_us_ = knob("RDB_FAULT_DELAY_BATCH_US");
+    fault_kill_after_ = knob("RDB_FAULT_KILL_AFTER_BATCHES");
     for (int s = 0; s < depth_; ++s) {
       hipEvent_t a, b, c;
       ENG_CHECK(hipEventCreateWithFlags(&a, hipEventDisableTiming));
@@ -413,6 +418,11 @@ class Engine {
               continue;
             }
           }
+          if (fault_drop_every_ > 0 && ++fault_req_count_ % fault_drop_every_ == 0) {
+            write_completion(h, s.queue, ST_REPLICA_DIED, nullptr, 0, now_ns());  // injected loss
+            ++s.peek_pos;
+            continue;
+          }
           if (h->len != (uint32_t)s.in_row_bytes) {
             write_completion(h, s.queue, ST_ERROR, nullptr, 0, now_ns());
             ++s.peek_pos;
@@ -425,6 +435,9 @@ class Engine {
           ++s.peek_pos;
         }
         f.pos_end = s.peek_pos;
+        if (n > 0 && fault_delay_batch_us_ > 0)
+          std::this_thread::sleep_for(std::chrono::microseconds(fault_delay_batch_us_));
+        if (n > 0 && fault_kill_after_ > 0 && ++fault_batch_count_ > fault_kill_after_) _exit(137);
         if (n > 0) {
           const int bi = bucket_for(s, n);
           const int rows = s.buckets[bi];
@@ -547,6 +560,8 @@ class Engine {
   hipStream_t copy_stream_ = nullptr;
   std::vector<hipStream_t> compute_streams_;
   std::atomic<int64_t> duty_cycle_ns_{0};
+  long long fault_drop_every_ = 0, fault_delay_batch_us_ = 0, fault_kill_after_ = 0;
+  long long fault_req_count_ = 0, fault_batch_count_ = 0;
   int64_t cycle_start_ns_ = 0;
   size_t rr_next_ = 0;
   std::vector<hipEvent_t> ev_copy_, ev_start_, ev_done_;

@@ -691,7 +691,10 @@ class NodeAgent {
       ReplicaState* rs = p.job->replica(p.replica);
       rs->status.store(RS_DEAD);
       for (uint32_t q : p.queues)
-        if (q < p.job->hdr()->n_queues) fail_pending(*p.job, q, ST_REPLICA_DIED);
+        if (q < p.job->hdr()->n_queues) {
+          fail_pending(*p.job, q, ST_REPLICA_DIED);
+          forget_inflight(*p.job, q);
+        }
       rs->restarts.fetch_add(1);  // generation bump: routers reap requests lost in flight
     }
     if (!p.restart || stopped_.load()) {

@@ -494,5 +494,15 @@ inline uint64_t fail_pending(Job& job, uint32_t q, uint32_t status) {
   return n;
 }
 
+// After a replica died: requests it had already consumed will never complete
+// (routers re-dispatch them on the generation bump), so stop counting them as
+// ongoing -- otherwise the restarted replica looks saturated forever.
+inline void forget_inflight(Job& job, uint32_t q) {
+  QueueState* qs = job.queue(q);
+  const uint64_t sub = qs->submitted.load();
+  uint64_t done = qs->completed.load();
+  while (done < sub && !qs->completed.compare_exchange_weak(done, sub)) {}
+}
+
 }  // namespace rt
 }  // namespace rdb

@@ -116,9 +116,16 @@ def _run_python(spec, cfg, job, r, stop, ctx) -> int:
     ctx.servable_object = user.obj
     cons = rjob.Consumer(job, [r])
     inflight = [0]
+    from ..utils.faults import injector
+
+    faults = injector()
 
     async def handle(req):
         rid, q, client, kind, t_sub, dl, payload = req
+        if faults.drop_request():   # injected message loss: the router re-dispatches
+            cons.complete(client, rid, q, int(rjob.Status.REPLICA_DIED), t_sub, b"", KIND_PICKLE)
+            inflight[0] -= 1
+            return
         try:
             method, args, kwargs, mux, stream, user_rid = cloudpickle.loads(payload)
             meta = RequestMeta(user_rid, method, mux, stream, spec["app_name"], spec["deployment"])
@@ -149,6 +156,7 @@ def _run_python(spec, cfg, job, r, stop, ctx) -> int:
             except Exception:  # pragma: no cover
                 break
             if reqs:
+                faults.before_batch()
                 inflight[0] += len(reqs)
                 for req in reqs:
                     asyncio.run_coroutine_threadsafe(handle(req), loop)

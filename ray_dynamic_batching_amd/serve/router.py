@@ -319,6 +319,9 @@ class _ShmClientHub:
         self.pending: Deque[Tuple] = collections.deque()
         self.closed = False
         self._pending_by_model: Dict[int, int] = collections.Counter()
+        from ..utils.faults import injector
+
+        self.faults = injector()
         self.thread = threading.Thread(target=self._run, name=f"rdb-dispatch-{job_name}", daemon=True)
         self.thread.start()
 
@@ -346,6 +349,8 @@ class _ShmClientHub:
             self._fail(sink, DeploymentUnavailableError(f"no replica serves model id {model_id}"))
             return True
         if q < 0:
+            return False
+        if self.faults.reject_submit():   # injected rejection: exercises the pending/retry path
             return False
         rid = self.client.submit(q, payload, kind)
         if rid == -3:

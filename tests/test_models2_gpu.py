@@ -65,3 +65,53 @@ def test_serve_model_deployment_bert_on_gpu():
         assert st["replicas"][0]["batches"] >= 3
     finally:
         serve.shutdown()
+
+
+def test_serve_gpu_replica_killer_restart(monkeypatch):
+    """Chaos on the GPU path: the engine replica exits after 5 batches; the node
+    agent restarts it (graph re-capture) and the router re-dispatches."""
+    from ray_dynamic_batching_amd import serve
+    from ray_dynamic_batching_amd.models import factories
+    from ray_dynamic_batching_amd.serve.controller import get_controller
+
+    monkeypatch.setenv("RDB_FAULT_KILL_AFTER_BATCHES", "5")
+    fac = factories.bert_base(layers=2)
+    d = serve.model_deployment(fac, "bert", max_batch_size=8, batch_wait_timeout_s=0.002,
+                               ray_actor_options={"num_gpus": 1}, max_ongoing_requests=16,
+                               health_check_timeout_s=60)
+    try:
+        h = serve.run(d.bind(), mode="process")
+        ids = np.random.default_rng(0).integers(1, 30000, size=(120, 128)).astype(np.int32)
+        outs = [h.remote(ids[i]) for i in range(120)]
+        got = [o.result(timeout_s=300) for o in outs]
+        assert all(g.shape == (2,) for g in got)
+        assert sum(p["restarts"] for p in get_controller().agent.list()) >= 1
+    finally:
+        serve.shutdown()
+
+
+def test_engine_fault_drop_knob(monkeypatch):
+    from ray_dynamic_batching_amd.models.bert import BertConfig, BertForSequenceClassification
+    from ray_dynamic_batching_amd.runtime import job as rjob
+    from ray_dynamic_batching_amd.runtime.engine import EngineRunner, SessionSpec
+
+    monkeypatch.setenv("RDB_FAULT_DROP_EVERY", "4")
+    m = BertForSequenceClassification(BertConfig.tiny(seq_len=64), device="cuda", backend="hip")
+    name = rjob.unique_job_name("fdrop")
+    j = rjob.Job(name, create=True, n_replicas=1, n_queues=1, n_clients=1, req_slot_bytes=64 * 4, cmp_slot_bytes=64)
+    j.configure_queue(0, 0, 0, 1024, 0.0, True)
+    runner = EngineRunner(name, 0, [SessionSpec(model=m, queue=0, max_batch=8, max_wait_s=0.001)]).build().start()
+    try:
+        c = rjob.Client(j)
+        ids = m.example_input(100, seed=1).cpu()
+        for i in range(100):
+            c.submit(0, ids[i].numpy().tobytes())
+        st = []
+        import time
+        t_end = time.time() + 60
+        while len(st) < 100 and time.time() < t_end:
+            st += [x[1] for x in c.poll(128, 0.5)]
+        assert len(st) == 100 and st.count(int(rjob.Status.REPLICA_DIED)) == 25
+    finally:
+        runner.stop()
+        j.close()
