@@ -86,9 +86,12 @@ def build_ops(force: bool = False, jobs: int | None = None, verbose: bool = Fals
               f"-I{OPS_SRC}", f"-I{RT_SRC}"] + _pybind_includes()
     objs = []
     cmds = []
+    hdr_mtime = max((h.stat().st_mtime for d in (OPS_SRC, RT_SRC) for h in d.glob("*.h")), default=0.0)
     for s in srcs:
         o = BUILD / (s.name + ".o")
         objs.append(o)
+        if not force and o.exists() and o.stat().st_mtime >= max(s.stat().st_mtime, hdr_mtime):
+            continue  # object up to date
         lang = ["-x", "hip"] if s.suffix == ".hip" else []
         cmds.append([cc] + common + lang + ["-c", str(s), "-o", str(o)])
     jobs = jobs or min(8, os.cpu_count() or 4, 16)
@@ -99,7 +102,7 @@ def build_ops(force: bool = False, jobs: int | None = None, verbose: bool = Fals
         list(ex.map(_run, cmds))
     tmp = target.with_suffix(".tmp.so")
     _run([cc, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", str(tmp)] + [str(o) for o in objs]
-         + [f"-L{ROCM}/lib", "-lamdhip64"])
+         + [f"-L{ROCM}/lib", "-lamdhip64", "-lrocprofiler-sdk-roctx", f"-Wl,-rpath,{ROCM}/lib"])
     os.replace(tmp, target)
     return target
 

@@ -24,6 +24,7 @@
 //                     request-ring slots and updates shm metrics.
 // No Python runs in steady state.
 #include <hip/hip_runtime.h>
+#include <rocprofiler-sdk-roctx/roctx.h>
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
@@ -390,6 +391,7 @@ class Engine {
         }
         job_.replica(replica_)->heartbeat_ns.store(now_ns(), std::memory_order_relaxed);
         Session& s = sessions_[sid];
+        roctxRangePushA("rdb:form_batch");
         InFlight f;
         f.session = sid;
         f.slot = slot;
@@ -435,6 +437,8 @@ class Engine {
           ++s.peek_pos;
         }
         f.pos_end = s.peek_pos;
+        roctxRangePop();
+        if (n > 0) roctxRangePushA("rdb:launch");
         if (n > 0 && fault_delay_batch_us_ > 0)
           std::this_thread::sleep_for(std::chrono::microseconds(fault_delay_batch_us_));
         if (n > 0 && fault_kill_after_ > 0 && ++fault_batch_count_ > fault_kill_after_) _exit(137);
@@ -467,6 +471,7 @@ class Engine {
           ENG_CHECK(hipEventRecord(ev_done_[slot], cs));
           s.used_ns += (int64_t)s.est_ns[bi];
           padded_.fetch_add(rows - n, std::memory_order_relaxed);
+          roctxRangePop();
         }
         f.t_launch = now_ns();
         {
@@ -508,6 +513,8 @@ class Engine {
             if (q != hipErrorNotReady) ENG_CHECK(q);
             std::this_thread::yield();
           }
+          const int64_t t_obs = now_ns();
+          roctxRangePushA("rdb:complete");
           float ms = 0.f;
           if (hipEventElapsedTime(&ms, ev_start_[f.slot], ev_done_[f.slot]) == hipSuccess) {
             gpu_busy_ms_.store(gpu_busy_ms_.load() + ms);
@@ -532,6 +539,12 @@ class Engine {
           rs->hist_service.record((uint64_t)(t_done - f.t_form_start));
           batches_.fetch_add(1, std::memory_order_relaxed);
           requests_.fetch_add(n, std::memory_order_relaxed);
+          TraceRing* tr = job_.trace(replica_);
+          const uint32_t rows = (uint32_t)s.buckets[f.bucket_idx];
+          tr->record(TK_FORM, f.t_form_start, f.t_launch, s.queue, n, rows);
+          tr->record(TK_GPU, t_obs - (int64_t)(ms * 1e6), t_obs, s.queue, n, rows);
+          tr->record(TK_COMPLETE, t_obs, now_ns(), s.queue, n, rows);
+          roctxRangePop();
         }
         s.ring.commit(f.pos_end);
         {

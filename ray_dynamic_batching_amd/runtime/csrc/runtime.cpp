@@ -171,6 +171,37 @@ class JobHandle {
   }
   // Fail every request still queued for a dead replica's queue so callers
   // are not left waiting (router then re-dispatches).
+  // -- seqlock snapshot (routing table / plan publication)
+  uint64_t publish(py::bytes b) {
+    std::string s = b;
+    return job_.snapshot()->publish(s.data(), (uint32_t)s.size());
+  }
+  py::tuple read_snapshot() {
+    std::string out;
+    const uint64_t v = job_.snapshot()->read(out);
+    return py::make_tuple(v, py::bytes(out));
+  }
+  uint64_t snapshot_version() { return job_.snapshot()->seq.load() / 2; }
+  // -- trace events of one replica: list of (kind, t0_ns, t1_ns, queue, n, bucket)
+  py::list trace_events(uint32_t r, uint64_t since) {
+    check_r(r);
+    TraceRing* tr = job_.trace(r);
+    const uint64_t head = tr->head.load(std::memory_order_acquire);
+    uint64_t start = head > kTraceCap ? head - kTraceCap : 0;
+    start = std::max(start, since);
+    py::list l;
+    for (uint64_t i = start; i < head; ++i) {
+      const TraceEvent& e = tr->ev[i & (kTraceCap - 1)];
+      if (e.seq.load(std::memory_order_acquire) != (uint32_t)(i + 1)) continue;
+      l.append(py::make_tuple(e.kind, e.t0, e.t1, e.queue, e.n, e.bucket));
+    }
+    return l;
+  }
+  uint64_t trace_head(uint32_t r) { check_r(r); return job_.trace(r)->head.load(); }
+  void trace_record(uint32_t r, uint32_t kind, int64_t t0, int64_t t1, uint32_t queue, uint32_t n, uint32_t bucket) {
+    check_r(r);
+    job_.trace(r)->record(kind, t0, t1, queue, n, bucket);
+  }
   uint64_t fail_queue(uint32_t q, uint32_t status) {
     check_q(q);
     return fail_pending(job_, q, status);
@@ -533,6 +564,7 @@ class EchoServer {
       rs->batches.fetch_add(1, std::memory_order_relaxed);
       rs->batch_items.fetch_add(batch.size(), std::memory_order_relaxed);
       rs->hist_batch_size.record(batch.size());
+      job_.trace(replica_)->record(TK_GPU, t0, now_ns(), q, (uint32_t)batch.size(), (uint32_t)batch.size());
       served_.fetch_add(batch.size(), std::memory_order_relaxed);
     }
   }
@@ -663,6 +695,11 @@ PYBIND11_MODULE(_rdb_runtime, m) {
   m.attr("ST_TOO_LARGE") = (int)ST_TOO_LARGE;
   m.attr("ST_SHUTDOWN") = (int)ST_SHUTDOWN;
   m.attr("ST_REPLICA_DIED") = (int)ST_REPLICA_DIED;
+  m.attr("TK_FORM") = (int)TK_FORM;
+  m.attr("TK_GPU") = (int)TK_GPU;
+  m.attr("TK_COMPLETE") = (int)TK_COMPLETE;
+  m.attr("TK_DROP") = (int)TK_DROP;
+  m.attr("TK_PY_BATCH") = (int)TK_PY_BATCH;
   m.attr("RS_UNUSED") = (int)RS_UNUSED;
   m.attr("RS_STARTING") = (int)RS_STARTING;
   m.attr("RS_READY") = (int)RS_READY;
@@ -696,6 +733,12 @@ PYBIND11_MODULE(_rdb_runtime, m) {
       .def("replica_stats", &JobHandle::replica_stats)
       .def("reset_stats", &JobHandle::reset_stats)
       .def("fail_queue", &JobHandle::fail_queue)
+      .def("publish", &JobHandle::publish)
+      .def("read_snapshot", &JobHandle::read_snapshot)
+      .def("snapshot_version", &JobHandle::snapshot_version)
+      .def("trace_events", &JobHandle::trace_events, py::arg("replica"), py::arg("since") = 0)
+      .def("trace_head", &JobHandle::trace_head)
+      .def("trace_record", &JobHandle::trace_record)
       .def("info", &JobHandle::info)
       .def("base", &JobHandle::base)
       .def("request_region", &JobHandle::request_region);

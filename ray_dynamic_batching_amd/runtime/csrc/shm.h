@@ -40,7 +40,9 @@ namespace rdb {
 namespace rt {
 
 constexpr uint64_t kMagic = 0x3130424F4A424452ULL;  // "RDBJOB01"
-constexpr uint32_t kVersion = 3;
+constexpr uint32_t kVersion = 4;
+constexpr uint32_t kTraceCap = 8192;          // trace events per replica (power of two)
+constexpr uint32_t kSnapshotBytes = 1 << 16;  // seqlock-published snapshot (routing table / plan)
 constexpr int kHistSub = 32;       // sub-buckets per power of two (~3% wide)
 constexpr int kHistBuckets = 1280;  // covers values up to 2^44 ns
 
@@ -292,6 +294,75 @@ struct alignas(64) QueueState {
   Histogram hist_e2e;                   // submit -> completion written
 };
 
+// Per-replica trace ring (chrome-trace export, utils/tracing.py): multi-writer,
+// overwrite-oldest.  Times are CLOCK_MONOTONIC ns like every other stamp here.
+enum TraceKind : uint32_t { TK_FORM = 1, TK_GPU = 2, TK_COMPLETE = 3, TK_DROP = 4, TK_PY_BATCH = 5 };
+struct TraceEvent {
+  int64_t t0, t1;
+  uint32_t kind;
+  uint16_t queue, n;
+  uint32_t bucket;
+  std::atomic<uint32_t> seq;  // publication stamp (event index + 1)
+};
+struct alignas(64) TraceRing {
+  std::atomic<uint64_t> head;
+  TraceEvent ev[kTraceCap];
+  void record(uint32_t kind, int64_t t0, int64_t t1, uint32_t queue, uint32_t n, uint32_t bucket) {
+    const uint64_t i = head.fetch_add(1, std::memory_order_relaxed);
+    TraceEvent& e = ev[i & (kTraceCap - 1)];
+    e.seq.store(0, std::memory_order_relaxed);
+    e.t0 = t0;
+    e.t1 = t1;
+    e.kind = kind;
+    e.queue = (uint16_t)queue;
+    e.n = (uint16_t)std::min<uint32_t>(n, 65535);
+    e.bucket = bucket;
+    e.seq.store((uint32_t)(i + 1), std::memory_order_release);
+  }
+};
+
+// Seqlock-versioned snapshot (replaces Ray's long-poll / pub-sub for the
+// routing table and the planner's placement: writers bump seq to odd, copy,
+// bump to even; readers retry while odd or changed).
+struct alignas(64) Snapshot {
+  std::atomic<uint64_t> seq;
+  std::atomic<uint32_t> len;
+  // payload as relaxed atomic words: the concurrent copy of a seqlock is then
+  // race-free in the C++ memory model (and clean under -fsanitize=thread)
+  std::atomic<uint64_t> words[kSnapshotBytes / 8];
+  uint64_t publish(const char* p, uint32_t n) {
+    if (n > kSnapshotBytes) throw std::length_error("snapshot too large");
+    uint64_t s = seq.load(std::memory_order_relaxed);
+    while (!(s % 2 == 0 && seq.compare_exchange_weak(s, s + 1, std::memory_order_acquire))) {
+      s = seq.load(std::memory_order_relaxed);
+    }
+    std::atomic_thread_fence(std::memory_order_release);
+    for (uint32_t i = 0; i < (n + 7) / 8; ++i) {
+      uint64_t w = 0;
+      memcpy(&w, p + 8 * i, std::min<uint32_t>(8, n - 8 * i));
+      words[i].store(w, std::memory_order_relaxed);
+    }
+    len.store(n, std::memory_order_relaxed);
+    seq.store(s + 2, std::memory_order_release);
+    return (s + 2) / 2;
+  }
+  // Returns the version (0 = never published) and fills out.
+  uint64_t read(std::string& out) const {
+    for (;;) {
+      const uint64_t s0 = seq.load(std::memory_order_acquire);
+      if (s0 & 1) continue;
+      const uint32_t n = std::min<uint32_t>(len.load(std::memory_order_relaxed), kSnapshotBytes);
+      out.resize(n);
+      for (uint32_t i = 0; i < (n + 7) / 8; ++i) {
+        const uint64_t w = words[i].load(std::memory_order_relaxed);
+        memcpy(&out[8 * i], &w, std::min<uint32_t>(8, n - 8 * i));
+      }
+      std::atomic_thread_fence(std::memory_order_acquire);
+      if (seq.load(std::memory_order_relaxed) == s0) return s0 / 2;
+    }
+  }
+};
+
 struct alignas(4096) JobHeader {
   std::atomic<uint64_t> magic;  // written last by the creator
   uint32_t version;
@@ -302,7 +373,7 @@ struct alignas(4096) JobHeader {
   uint32_t req_slot_bytes;
   uint32_t cmp_capacity;
   uint32_t cmp_slot_bytes;
-  uint64_t off_replicas, off_queues, off_req, off_cmp, total_bytes;
+  uint64_t off_replicas, off_queues, off_req, off_cmp, off_trace, off_snap, total_bytes;
   std::atomic<uint32_t> clients_registered;
   std::atomic<uint32_t> shutdown;
   std::atomic<uint64_t> next_req_id;
@@ -344,7 +415,9 @@ class Job {
     const uint64_t req_ring_sz = (Ring::bytes(cfg.req_capacity, cfg.req_slot_bytes) + 4095) & ~4095ULL;
     const uint64_t off_cmp = off_req + req_ring_sz * cfg.n_queues;
     const uint64_t cmp_ring_sz = (Ring::bytes(cfg.cmp_capacity, cfg.cmp_slot_bytes) + 4095) & ~4095ULL;
-    const uint64_t total = off_cmp + cmp_ring_sz * cfg.n_clients;
+    const uint64_t off_trace = off_cmp + cmp_ring_sz * cfg.n_clients;
+    const uint64_t off_snap = (off_trace + (uint64_t)cfg.n_replicas * sizeof(TraceRing) + 4095) & ~4095ULL;
+    const uint64_t total = (off_snap + sizeof(Snapshot) + 4095) & ~4095ULL;
     if (overwrite) shm_unlink(shm_path().c_str());
     int fd = shm_open(shm_path().c_str(), O_CREAT | O_EXCL | O_RDWR, 0600);
     if (fd < 0) throw std::runtime_error("shm_open(create) failed for " + name + ": " + strerror(errno));
@@ -367,6 +440,8 @@ class Job {
     h->off_queues = off_q;
     h->off_req = off_req;
     h->off_cmp = off_cmp;
+    h->off_trace = off_trace;
+    h->off_snap = off_snap;
     h->total_bytes = total;
     h->clients_registered.store(0);
     h->shutdown.store(0);
@@ -432,6 +507,8 @@ class Job {
     r.slots = p + sizeof(RingHeader);
     return r;
   }
+  TraceRing* trace(uint32_t r) const { return reinterpret_cast<TraceRing*>(base_ + hdr()->off_trace) + r; }
+  Snapshot* snapshot() const { return reinterpret_cast<Snapshot*>(base_ + hdr()->off_snap); }
   char* base() const { return base_; }
   size_t size() const { return size_; }
   const std::string& name() const { return name_; }

@@ -56,13 +56,32 @@ def get_controller(create: bool = True) -> Optional["ServeController"]:
         return _CONTROLLER
 
 
+_ROUTE_JOBS: Dict[str, Any] = {}
+
+
+def _read_routes(job_name: Optional[str], table: Optional[str]) -> Dict[str, Any]:
+    """Latest routing table: the seqlock snapshot the controller publishes in the
+    job segment (live updates), else the file written at spawn time."""
+    if job_name:
+        from ..runtime import job as rjob
+
+        j = _ROUTE_JOBS.get(job_name)
+        if j is None:
+            j = _ROUTE_JOBS[job_name] = rjob.Job(job_name, create=False)
+        version, blob = j.read_snapshot()
+        if version:
+            return json.loads(blob)
+    with open(table) as f:
+        return json.load(f)
+
+
 def lookup_router(app_name: str, deployment: str):
     """Router for a handle: the controller in the driver, the routing table in
     a replica process (handles shipped for composition)."""
     table = os.environ.get("RDB_ROUTING_TABLE")
-    if table and _CONTROLLER is None:
-        with open(table) as f:
-            routes = json.load(f)
+    job_name = os.environ.get("RDB_JOB")
+    if (table or job_name) and _CONTROLLER is None:
+        routes = _read_routes(job_name, table)
         r = routes.get(f"{app_name}/{deployment}")
         if r is None:
             raise RayServeException(f"no route for {app_name}/{deployment}")
@@ -246,6 +265,7 @@ class ServeController:
         with open(path, "w") as f:
             json.dump(routes, f)
         self._routes_path = path
+        self.jobs[app_name].publish(json.dumps(routes).encode())   # live copy for replicas
 
     def _spawn(self, st: DeploymentState, rep: ProcReplica) -> bool:
         from ..runtime.resources import visible_devices_env
@@ -264,6 +284,7 @@ class ServeController:
         job.set_replica_status(rep.slot, 1, gpus[0] if gpus else -1, 0)
         env = dict(visible_devices_env(gpus))
         env["RDB_ROUTING_TABLE"] = self._routes_path
+        env["RDB_JOB"] = job.info()["name"]
         env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
         pkg_root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
         env["PYTHONPATH"] = pkg_root + os.pathsep + os.environ.get("PYTHONPATH", "")

@@ -75,3 +75,40 @@ def test_runtime_microbench_runs():
                           "--queues", "2"], capture_output=True, text=True, timeout=120)
     assert out.returncode == 0, out.stderr
     assert "1:1 sync" in out.stdout and "serve path" in out.stdout
+
+
+def test_trace_ring_and_chrome_export(tmp_path):
+    import json
+
+    from ray_dynamic_batching_amd.utils import tracing
+
+    j = _job(2)
+    s = rjob.EchoServer(j, 1, [1], max_batch=8, service_us=100.0)
+    s.start()
+    try:
+        c = rjob.Client(j, 0)
+        lg = rjob.LoadGen(c, 0, [b"z" * 32])
+        lg.run(400, 32, 0.0, 0.0, False, 30.0)
+        j.trace_record(0, 1, 1000, 2000, 0, 3, 4)
+        ev = tracing.collect(j)
+        assert any(e["replica"] == 1 and e["kind"] == "gpu" for e in ev)
+        assert sum(e["n"] for e in ev if e["replica"] == 1) == 400
+        tr = tracing.export_chrome_trace(j, str(tmp_path / "t.json"))
+        assert json.load(open(tmp_path / "t.json"))["traceEvents"] == tr["traceEvents"]
+        assert tracing.summarize(ev)["gpu"]["mean_us"] >= 100.0
+    finally:
+        s.stop()
+        j.close()
+
+
+def test_seqlock_snapshot_publish_read():
+    j = _job(1)
+    try:
+        assert j.read_snapshot() == (0, b"")
+        assert j.publish(b'{"routes": 1}') == 1
+        assert j.publish(b'{"routes": 2}') == 2
+        other = rjob.Job(j.info()["name"], create=False)
+        assert other.read_snapshot() == (2, b'{"routes": 2}')
+        other.close()
+    finally:
+        j.close()
