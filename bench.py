@@ -46,6 +46,7 @@ def parse():
     ap.add_argument("--compute-streams", type=int, default=2, help="batches executing concurrently per GPU")
     ap.add_argument("--layers", type=int, default=12)
     ap.add_argument("--json-out", default="")
+    ap.add_argument("--trace-out", default="", help="write a Chrome trace of the replicas' batches")
     return ap.parse_args()
 
 
@@ -123,6 +124,11 @@ def main():
         t = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
+    if rank == 0 and args.trace_out:
+        from ray_dynamic_batching_amd.utils.tracing import collect, export_chrome_trace, summarize
+
+        export_chrome_trace(job, args.trace_out)
+        print(json.dumps({"trace_summary": summarize(collect(job))}), file=sys.stderr)
     if rank == 0:
         rep1 = [job.replica_stats(r) for r in range(n)]
         rep = [{k: rep1[i][k] - rep0[i][k] for k in ("batches", "batch_items", "busy_ms")} for i in range(n)]
