@@ -78,3 +78,17 @@ def _vit(device="cuda", backend="hip", **kw):
     from .vit import ViT, ViTConfig
 
     return ViT(ViTConfig.b16(), device=device, backend=backend, **kw)
+
+
+@register("shufflenet-v2")
+def _shufflenet(device="cuda", backend="hip", **kw):
+    from .shufflenet import ShuffleNetV2
+
+    return ShuffleNetV2(device=device, backend=backend, **kw)
+
+
+@register("efficientnet-v2s")
+def _efficientnet(device="cuda", backend="hip", **kw):
+    from .efficientnet import EfficientNetV2S
+
+    return EfficientNetV2S(device=device, backend=backend, **kw)

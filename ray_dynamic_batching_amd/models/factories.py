@@ -58,3 +58,23 @@ def vit_b16(backend: str = "hip") -> Factory:
 
 def mlp(d_in: int = 32, d_out: int = 8) -> Factory:
     return Factory(_mlp, ((d_in,), torch.float32, (d_out,), torch.float32), d_in=d_in, d_out=d_out)
+
+
+def _shufflenet(device, backend="hip"):
+    from .shufflenet import ShuffleNetV2
+
+    return ShuffleNetV2(device=device, backend=backend)
+
+
+def _efficientnet(device, backend="hip"):
+    from .efficientnet import EfficientNetV2S
+
+    return EfficientNetV2S(device=device, backend=backend)
+
+
+def shufflenet_v2(backend: str = "hip") -> Factory:
+    return Factory(_shufflenet, ((224, 224, 3), torch.uint8, (10,), torch.float32), backend=backend)
+
+
+def efficientnet_v2s(backend: str = "hip") -> Factory:
+    return Factory(_efficientnet, ((384, 384, 3), torch.uint8, (10,), torch.float32), backend=backend)

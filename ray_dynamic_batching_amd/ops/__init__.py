@@ -20,7 +20,7 @@ import torch.nn.functional as F
 from ..utils.native import require_gpu_ops
 
 DTYPE_CODE = {torch.bfloat16: 0, torch.float16: 1, torch.float32: 2}
-ACT_CODE = {"none": 0, "gelu": 1, "relu": 2, "tanh": 3, "silu": 4, "gelu_tanh": 5, "swiglu": 6}
+ACT_CODE = {"none": 0, "gelu": 1, "relu": 2, "tanh": 3, "silu": 4, "gelu_tanh": 5, "swiglu": 6, "sigmoid": 7}
 
 
 def _ops():
@@ -142,6 +142,8 @@ def _act_ref(y: torch.Tensor, act: str) -> torch.Tensor:
         return torch.tanh(y)
     if act == "silu":
         return F.silu(y)
+    if act == "sigmoid":
+        return torch.sigmoid(y)
     return y
 
 
@@ -436,3 +438,57 @@ def avgpool_nhwc(x):
 
 def avgpool_nhwc_ref(x):
     return x.float().mean(dim=(1, 2)).half()
+
+
+def shuffle_remap(a: torch.Tensor, b: torch.Tensor, ch: int, split: bool, ld1: int, ld2: int = 0):
+    """ShuffleNetV2 concat(a, b) + channel_shuffle(groups=2) [+ split] in one pass.
+
+    a, b: [..., >=ch] f16 (x1 / branch output, possibly channel-padded views with
+    unit stride in the last dim).  Returns one tensor [..., ld1] (``split=False``,
+    2*ch real channels) or two tensors [..., ld1], [..., ld2] (the next unit's
+    halves, ch real channels each); padded channels are zero."""
+    _check(a.is_cuda and a.dtype == torch.float16 and b.dtype == torch.float16, "shuffle_remap: f16 cuda tensors")
+    _check(a.stride(-1) == 1 and b.stride(-1) == 1 and a.shape[:-1] == b.shape[:-1], "shuffle_remap: bad views")
+    lead = a.shape[:-1]
+    pixels = 1
+    for d in lead:
+        pixels *= d
+    lda = a.stride(-2) if a.dim() > 1 else a.shape[-1]
+    ldb = b.stride(-2) if b.dim() > 1 else b.shape[-1]
+    _check(a.dim() < 2 or all(a.stride(i) == a.stride(i + 1) * a.shape[i + 1] for i in range(a.dim() - 2)),
+           "shuffle_remap: a must be a channel slice of a contiguous tensor")
+    _check(b.dim() < 2 or all(b.stride(i) == b.stride(i + 1) * b.shape[i + 1] for i in range(b.dim() - 2)),
+           "shuffle_remap: b must be a channel slice of a contiguous tensor")
+    o1 = torch.empty(*lead, ld1, device=a.device, dtype=torch.float16)
+    o2 = torch.empty(*lead, ld2, device=a.device, dtype=torch.float16) if split else None
+    _ops().shuffle_remap(a.data_ptr(), lda, b.data_ptr(), ldb, ch, pixels, o1.data_ptr(), ld1, _ptr(o2), ld2,
+                         int(split), _stream())
+    return (o1, o2) if split else o1
+
+
+def shuffle_remap_ref(a, b, ch, split, ld1, ld2=0):
+    cat = torch.cat([a[..., :ch], b[..., :ch]], dim=-1)
+    lead = cat.shape[:-1]
+    sh = cat.reshape(*lead, 2, ch).transpose(-1, -2).reshape(*lead, 2 * ch)
+
+    def pad(t, ld):
+        out = torch.zeros(*lead, ld, device=t.device, dtype=t.dtype)
+        out[..., :t.shape[-1]] = t
+        return out
+    if split:
+        return pad(sh[..., :ch], ld1), pad(sh[..., ch:], ld2)
+    return pad(sh, ld1)
+
+
+def se_scale(x: torch.Tensor, s: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Squeeze-excitation scaling: x [N, H, W, C] * s [N, C] (f16)."""
+    _check(x.is_cuda and x.dtype == torch.float16 and x.is_contiguous() and x.dim() == 4, "se_scale: bad x")
+    N, H, W, C = x.shape
+    _check(s.shape == (N, C) and s.is_contiguous() and s.dtype == torch.float16, "se_scale: bad s")
+    out = torch.empty_like(x) if out is None else out
+    _ops().se_scale(x.data_ptr(), s.data_ptr(), out.data_ptr(), N, H * W, C, _stream())
+    return out
+
+
+def se_scale_ref(x, s):
+    return (x.float() * s.float()[:, None, None, :]).to(torch.float16)

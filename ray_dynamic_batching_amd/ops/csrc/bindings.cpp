@@ -34,6 +34,9 @@ void maxpool_nhwc(uintptr_t x, uintptr_t y, int N, int H, int W, int C, int k, i
 void avgpool_nhwc(uintptr_t x, uintptr_t y, int N, int HW, int C, uintptr_t stream);
 void dwconv_nhwc(uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t y, int N, int H, int W, int C,
                  int R, int stride, int pad, int P, int Q, int act, uintptr_t stream);
+void shuffle_remap(uintptr_t A, int ldA, uintptr_t B, int ldB, int Ch, long pixels, uintptr_t O1, int ld1,
+                   uintptr_t O2, int ld2, int split, uintptr_t stream);
+void se_scale(uintptr_t x, uintptr_t s, uintptr_t y, int N, long HW, int C, uintptr_t stream);
 void register_engine(py::module_& m);
 }  // namespace rdb
 
@@ -55,6 +58,8 @@ PYBIND11_MODULE(_rdb_ops, m) {
   m.def("maxpool_nhwc", &rdb::maxpool_nhwc, py::call_guard<py::gil_scoped_release>());
   m.def("avgpool_nhwc", &rdb::avgpool_nhwc, py::call_guard<py::gil_scoped_release>());
   m.def("dwconv_nhwc", &rdb::dwconv_nhwc, py::call_guard<py::gil_scoped_release>());
+  m.def("shuffle_remap", &rdb::shuffle_remap, py::call_guard<py::gil_scoped_release>());
+  m.def("se_scale", &rdb::se_scale, py::call_guard<py::gil_scoped_release>());
 
   // Pinning of shared-memory regions so the device can read request payloads
   // in place (zero-copy H2D gather) -- the "pinned shm tensor arena".

@@ -39,7 +39,7 @@ __device__ __forceinline__ float wave_max(float v) {
 // Epilogue activations shared by GEMM / conv kernels.
 // ACT_SWIGLU is a GEMM-only pairing epilogue: W rows are interleaved (gate_j, up_j),
 // the output has N/2 columns and holds silu(gate_j) * up_j.
-enum Act : int { ACT_NONE = 0, ACT_GELU = 1, ACT_RELU = 2, ACT_TANH = 3, ACT_SILU = 4, ACT_GELU_TANH = 5, ACT_SWIGLU = 6 };
+enum Act : int { ACT_NONE = 0, ACT_GELU = 1, ACT_RELU = 2, ACT_TANH = 3, ACT_SILU = 4, ACT_GELU_TANH = 5, ACT_SWIGLU = 6, ACT_SIGMOID = 7 };
 
 template <int ACT>
 __device__ __forceinline__ float apply_act(float x) {
@@ -54,6 +54,8 @@ __device__ __forceinline__ float apply_act(float x) {
   } else if constexpr (ACT == ACT_GELU_TANH) {
     const float c = 0.7978845608028654f;
     return 0.5f * x * (1.0f + tanhf(c * (x + 0.044715f * x * x * x)));
+  } else if constexpr (ACT == ACT_SIGMOID) {
+    return 1.0f / (1.0f + __expf(-x));
   } else {
     return x;
   }

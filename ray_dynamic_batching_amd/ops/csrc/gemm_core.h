@@ -66,6 +66,7 @@ __device__ __forceinline__ float act_rt(int act, float x) {
     case ACT_TANH: return apply_act<ACT_TANH>(x);
     case ACT_SILU: return apply_act<ACT_SILU>(x);
     case ACT_GELU_TANH: return apply_act<ACT_GELU_TANH>(x);
+    case ACT_SIGMOID: return apply_act<ACT_SIGMOID>(x);
     default: return x;
   }
 }
@@ -356,6 +357,7 @@ mfma_gemm_kernel(typename LoaderT<T, BM * 8 / 256>::Params ap, const T* __restri
     case ACT_TANH: RDB_ACT_LOOP(ACT_TANH) break;
     case ACT_SILU: RDB_ACT_LOOP(ACT_SILU) break;
     case ACT_GELU_TANH: RDB_ACT_LOOP(ACT_GELU_TANH) break;
+    case ACT_SIGMOID: RDB_ACT_LOOP(ACT_SIGMOID) break;
     default: break;
   }
 #undef RDB_ACT_LOOP

@@ -115,3 +115,30 @@ def test_engine_fault_drop_knob(monkeypatch):
     finally:
         runner.stop()
         j.close()
+
+
+def _rel_err(a, b):
+    return ((a.float() - b.float()).abs().max() / b.float().abs().max().clamp_min(1e-6)).item()
+
+
+def test_shufflenet_hip_matches_torch():
+    from ray_dynamic_batching_amd.models.shufflenet import ShuffleNetV2
+
+    m = ShuffleNetV2(device="cuda", backend="hip")
+    x = m.example_input(4, seed=5)
+    lg = m._logits_hip(x)
+    ref = m._logits_torch(x)
+    assert lg.shape == (4, 1000)
+    assert _rel_err(lg, ref) < 3e-2, _rel_err(lg, ref)
+    assert m(x).shape == (4, 10)
+
+
+def test_efficientnet_v2s_hip_matches_torch():
+    from ray_dynamic_batching_amd.models.efficientnet import EfficientNetV2S
+
+    m = EfficientNetV2S(device="cuda", backend="hip")
+    x = m.example_input(2, seed=6)
+    lg = m._logits_hip(x)
+    ref = m._logits_torch(x)
+    assert lg.shape == (2, 1000)
+    assert _rel_err(lg, ref) < 5e-2, _rel_err(lg, ref)

@@ -221,3 +221,37 @@ def test_conv_all_tiles(cfg):
     b = torch.randn(200, device="cuda", dtype=torch.float16) * 0.1
     _close(ops.conv2d_nhwc(x, w, b, stride=1, pad=1, act="relu", tile_cfg=cfg),
            ops.conv2d_nhwc_ref(x, w, b, stride=1, pad=1, act="relu"), 2e-2, 2e-2)
+
+
+def test_shuffle_remap_split_and_full():
+    from ray_dynamic_batching_amd import ops
+
+    torch.manual_seed(0)
+    base_a = torch.randn(2, 7, 5, 64, device="cuda", dtype=torch.float16)
+    b = torch.randn(2, 7, 5, 64, device="cuda", dtype=torch.float16)
+    a = base_a[..., :64]
+    for ch in (58, 64):
+        o1, o2 = ops.shuffle_remap(a, b, ch, True, 64, 64)
+        r1, r2 = ops.shuffle_remap_ref(a, b, ch, True, 64, 64)
+        assert torch.equal(o1, r1) and torch.equal(o2, r2)
+        full = ops.shuffle_remap(a, b, ch, False, 128)
+        assert torch.equal(full, ops.shuffle_remap_ref(a, b, ch, False, 128))
+    # channel-slice view inputs (x1 = first half of a padded tensor)
+    x = torch.randn(3, 4, 4, 128, device="cuda", dtype=torch.float16)
+    o = ops.shuffle_remap(x[..., :64], x[..., 64:], 58, False, 120)
+    assert torch.equal(o, ops.shuffle_remap_ref(x[..., :64], x[..., 64:], 58, False, 120))
+
+
+def test_se_scale_and_sigmoid_gemm():
+    from ray_dynamic_batching_amd import ops
+
+    torch.manual_seed(1)
+    x = torch.randn(4, 9, 9, 96, device="cuda", dtype=torch.float16)
+    s = torch.rand(4, 96, device="cuda", dtype=torch.float16)
+    assert torch.allclose(ops.se_scale(x, s).float(), ops.se_scale_ref(x, s).float(), atol=1e-2)
+    a = torch.randn(8, 64, device="cuda", dtype=torch.float16)
+    w = torch.randn(96, 64, device="cuda", dtype=torch.float16) * 0.1
+    bias = torch.randn(96, device="cuda", dtype=torch.float16) * 0.1
+    y = ops.linear(a, w, bias, act="sigmoid")
+    r = ops.linear_ref(a, w, bias, act="sigmoid")
+    assert torch.allclose(y.float(), r.float(), atol=5e-3)
