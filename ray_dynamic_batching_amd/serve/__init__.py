@@ -10,13 +10,14 @@
     handle = serve.run(Model.bind())
     handle.remote(x).result()
 """
-from .api import Application, Deployment, delete, deployment, get_app_handle, get_deployment_handle, run, shutdown, \
-    start, status
+from .api import Application, Deployment, delete, deployment, get_app_handle, get_deployment_handle, http_port, \
+    run, shutdown, start, status
 from .batching import batch
 from .config import AutoscalingConfig, DeploymentConfig, EngineConfig
 from .context import get_replica_context
 from .exceptions import BackPressureError, RayServeException, RequestCancelledError, RequestDroppedError
 from .handle import DeploymentHandle, DeploymentResponse, DeploymentResponseGenerator
+from .http_proxy import HTTPRequest
 from .multiplex import get_multiplexed_model_id, multiplexed
 from .servable import TensorCodec, model_deployment
 
@@ -25,5 +26,5 @@ __all__ = [
     "get_app_handle", "get_deployment_handle", "get_replica_context", "multiplexed", "get_multiplexed_model_id",
     "DeploymentHandle", "DeploymentResponse", "DeploymentResponseGenerator", "AutoscalingConfig",
     "DeploymentConfig", "EngineConfig", "BackPressureError", "RayServeException", "RequestCancelledError",
-    "RequestDroppedError", "model_deployment", "TensorCodec",
+    "RequestDroppedError", "model_deployment", "TensorCodec", "HTTPRequest", "http_port",
 ]

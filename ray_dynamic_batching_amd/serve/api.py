@@ -155,9 +155,16 @@ def _controller(create: bool = True):
     return get_controller(create)
 
 
-def start(**kwargs) -> None:
-    """Start the (in-process) serve controller.  kwargs: mode="auto"|"local"|"process"."""
-    _controller().configure(**kwargs)
+def start(http_options: Optional[Dict[str, Any]] = None, **kwargs) -> None:
+    """Start the (in-process) serve controller.  kwargs: mode="auto"|"local"|"process";
+    ``http_options={"host": ..., "port": ...}`` also starts the HTTP proxy
+    (port 0 = pick a free port; see ``serve.http_port()``)."""
+    _controller().configure(http_options=http_options, **kwargs)
+
+
+def http_port() -> Optional[int]:
+    ctrl = _controller(create=False)
+    return ctrl.proxy.port if ctrl is not None and ctrl.proxy is not None else None
 
 
 def run(target: Application, blocking: bool = False, name: str = "default", route_prefix: Optional[str] = "/",

@@ -73,9 +73,11 @@ def main(argv=None) -> int:
     r.add_argument("--name", default="default")
     r.add_argument("--mode", default=None)
     r.add_argument("--duration", type=float, default=0)
+    r.add_argument("--http-port", type=int, default=-1, help="start the HTTP proxy on this port (-1 = off)")
     d = sub.add_parser("deploy")
     d.add_argument("config")
     d.add_argument("--duration", type=float, default=0)
+    d.add_argument("--http-port", type=int, default=-1)
     b = sub.add_parser("build")
     b.add_argument("import_path")
     b.add_argument("-o", "--output", default="-")
@@ -88,6 +90,10 @@ def main(argv=None) -> int:
 
     from .schema import ServeApplicationSchema, ServeDeploySchema, build_application, deploy_config, import_attr
 
+    if a.cmd in ("run", "deploy") and a.http_port >= 0:
+        from .api import start
+
+        start(http_options={"host": "127.0.0.1", "port": a.http_port})
     if a.cmd == "run":
         from .api import run
 

@@ -142,6 +142,8 @@ class ServeController:
 
         self.apps: Dict[str, Dict[str, DeploymentState]] = {}
         self.ingress: Dict[str, str] = {}
+        self.route_prefixes: Dict[str, Optional[str]] = {}
+        self.proxy = None
         self.jobs: Dict[str, Any] = {}            # app -> job segment handle (process mode)
         self.lock = threading.RLock()
         self.workdir = tempfile.mkdtemp(prefix="rdb_serve_")
@@ -160,9 +162,14 @@ class ServeController:
         self._thread.start()
         atexit.register(self.shutdown)
 
-    def configure(self, mode: str = None, **_):
+    def configure(self, mode: str = None, http_options: Optional[Dict[str, Any]] = None, **_):
         if mode:
             self.default_mode = mode
+        if http_options is not None and self.proxy is None:
+            from .http_proxy import HTTPProxy
+
+            self.proxy = HTTPProxy(self, http_options.get("host", "127.0.0.1"),
+                                   int(http_options.get("port", 8000))).start()
 
     # ------------------------------------------------------------------ deploy
     def _resolve_mode(self, app: Application, mode: Optional[str]) -> str:
@@ -185,6 +192,7 @@ class ServeController:
             states: Dict[str, DeploymentState] = {}
             self.apps[name] = states
             self.ingress[name] = app.deployment.name
+            self.route_prefixes[name] = route_prefix
             if mode == "process":
                 self._create_job(name, graph)
             for mid, a in enumerate(graph):
@@ -197,6 +205,11 @@ class ServeController:
                 # composition: bound Applications become handles
                 st.init_args = tuple(self._to_handle(name, x) for x in a.init_args)
                 st.init_kwargs = {k: self._to_handle(name, v) for k, v in a.init_kwargs.items()}
+                sv = getattr(d, "servable", None)
+                if sv is not None and mode == "local" and not st.init_args:
+                    # local mode runs the servable eagerly behind @serve.batch
+                    st.init_args = (sv["factory"], sv["max_batch_size"], sv["batch_wait_timeout_s"])
+                    st.init_kwargs = dict(device="cuda" if cfg.num_gpus > 0 else "cpu")
                 if mode == "local":
                     st.router = LocalRouter(d.name, cfg.max_queued_requests)
                 else:
@@ -495,6 +508,7 @@ class ServeController:
         with self.lock:
             states = self.apps.pop(name, None)
             self.ingress.pop(name, None)
+            self.route_prefixes.pop(name, None)
             if not states:
                 return
             for st in states.values():
@@ -523,6 +537,9 @@ class ServeController:
                 self.delete_application(name)
             except Exception:  # pragma: no cover
                 logger.error("error deleting %s:\n%s", name, traceback.format_exc())
+        if self.proxy is not None:
+            self.proxy.stop()
+            self.proxy = None
         self._stop.set()
         if self._thread.is_alive() and threading.current_thread() is not self._thread:
             self._thread.join(5.0)
