@@ -33,6 +33,7 @@
 #include <chrono>
 #include <condition_variable>
 #include <deque>
+#include <map>
 #include <mutex>
 #include <thread>
 #include <vector>
@@ -88,6 +89,16 @@ struct Session {
 
 enum Policy { POLICY_PRIORITY_EDF = 0, POLICY_DUTY_CYCLE = 1 };
 
+// process-wide refcount of pinned (hipHostRegister'ed) job request regions
+std::mutex& host_reg_mu() {
+  static std::mutex m;
+  return m;
+}
+std::map<void*, int>& host_reg_count() {
+  static std::map<void*, int> c;
+  return c;
+}
+
 struct InFlight {
   int session = -1;
   int slot = 0;
@@ -120,11 +131,19 @@ class Engine {
     if (zero_copy_) {
       auto reg = job_.request_region();
       host_base_ = reg.first;
-      ENG_CHECK(hipHostRegister(reg.first, reg.second, hipHostRegisterMapped));
+      // Portable: several engines (one per GPU) may live in one process (the
+      // SLO scheduler); only the first registers, the others reuse the mapping.
+      {
+        std::lock_guard<std::mutex> lk(host_reg_mu());
+        int& rc = host_reg_count()[reg.first];
+        if (rc == 0)
+          ENG_CHECK(hipHostRegister(reg.first, reg.second, hipHostRegisterMapped | hipHostRegisterPortable));
+        ++rc;
+        registered_ = true;
+      }
       void* dev = nullptr;
       ENG_CHECK(hipHostGetDevicePointer(&dev, reg.first, 0));
       dev_base_ = reinterpret_cast<char*>(dev);
-      registered_ = true;
     }
     slot_busy_.assign(depth_, false);
     // fault-injection knobs (same variables as utils/faults.py)
@@ -149,7 +168,14 @@ class Engine {
     for (auto e : ev_done_) hipEventDestroy(e);
     for (auto p : host_ptrs_) hipHostFree(p);
     for (auto p : host_out_) hipHostFree(p);
-    if (registered_) hipHostUnregister(job_.request_region().first);
+    if (registered_) {
+      std::lock_guard<std::mutex> lk(host_reg_mu());
+      void* base = job_.request_region().first;
+      if (--host_reg_count()[base] == 0) {
+        hipHostUnregister(base);
+        host_reg_count().erase(base);
+      }
+    }
     if (copy_stream_) hipStreamDestroy(copy_stream_);
     for (auto st : compute_streams_) hipStreamDestroy(st);
   }

@@ -144,12 +144,68 @@ class DutyCycleExecutor(threading.Thread):
         self.stats["processing_ms"] = (self.stats["processing_ms"] + [dt])[-100:]
 
 
+class EngineExecutor:
+    """GPU worker on the native replica engine (ops/csrc/engine.cpp) with the
+    Nexus duty-cycle policy in C++: every model of the scheduler is resident
+    and graph-captured on this GPU (288 GB HBM makes "load" an activation
+    flip instead of a weight copy + re-capture); a plan node activates its
+    sessions, sets their batch sizes and GPU-time shares (duty x occupancy) and
+    the engine enforces them per cycle, dropping stale requests natively."""
+
+    def __init__(self, sched: "SLOScheduler", gpu: int, device: int, max_batch: Dict[str, int]):
+        import torch
+
+        from ..runtime.engine import EngineRunner, SessionSpec
+
+        self.sched = sched
+        self.gpu = gpu
+        self.node: Optional[Node] = None
+        with torch.cuda.device(device):
+            self.models = {m: sched.model_factories[m](device=f"cuda:{device}") for m in sched.models}
+            specs = [SessionSpec(model=self.models[m], queue=sched.queue_id(gpu, m), max_batch=max_batch[m],
+                                 max_wait_s=0.0, slo_ms=float(sched.slos[m]), drop_stale=sched.drop_stale, name=m)
+                     for m in sched.models]
+            self.runner = EngineRunner(sched.job_name, gpu, specs, pipeline_depth=2, device=device,
+                                       policy=EngineRunner.POLICY_DUTY_CYCLE).build()
+        self.max_batch = dict(max_batch)
+        for i in range(len(specs)):
+            self.runner.set_active(i, False)
+        self.runner.start()
+
+    def update(self, node: Optional[Node]) -> None:
+        self.node = node
+        shares = []
+        for i, m in enumerate(self.sched.models):
+            sess = [(s, occ) for s, occ in (node.sessions if node else []) if s.model_name == m]
+            on = bool(sess)
+            if on:
+                b = max(1, min(self.max_batch[m], max(s.batch_size for s, _ in sess)))
+                self.runner.engine.set_max_batch(self.runner.sessions[i].sid, b)
+                shares.append(node.duty_cycle * sum(occ for _, occ in sess))
+            else:
+                shares.append(0.0)
+            self.runner.set_active(i, on)
+        self.runner.set_duty_cycle(node.duty_cycle if node else 0.0, shares)
+
+    @property
+    def stats(self) -> Dict[str, Any]:
+        return self.runner.stats()
+
+    def stop(self) -> None:
+        self.runner.stop()
+
+
 class SLOScheduler:
     def __init__(self, profiles: Dict[str, Dict[int, Dict[str, float]]], slos_ms: Dict[str, float],
                  model_factories: Dict[str, Callable[[], Any]], codecs: Dict[str, Any], num_gpus: int = 2,
                  monitoring_interval: float = 1.0, rate_change_threshold: float = 0.05, rate_window_s: float = 1.0,
                  compat: bool = False, slo_divisor: float = 1.0, drop_stale: bool = True,
-                 gpu_mem_gb: Optional[float] = None, queue_capacity: int = 2048, job_name: Optional[str] = None):
+                 gpu_mem_gb: Optional[float] = None, queue_capacity: int = 2048, job_name: Optional[str] = None,
+                 executor: str = "python", devices: Optional[List[int]] = None,
+                 max_batch: Optional[Dict[str, int]] = None):
+        """``executor``: "python" (DutyCycleExecutor threads; CPU / arbitrary torch
+        models) or "engine" (native GPU engines, one per entry of ``devices``;
+        ``max_batch`` = largest batch captured per model)."""
         self.profiles = profiles
         self.slos = dict(slos_ms)
         self.model_factories = model_factories
@@ -181,9 +237,14 @@ class SLOScheduler:
         self._client_lock = threading.Lock()
         self._backlog: List[tuple] = []
         self._backlog_ids = 0
-        self.executors = [DutyCycleExecutor(self, g) for g in range(num_gpus)]
-        for e in self.executors:
-            e.start()
+        if executor == "engine":
+            devices = list(devices if devices is not None else range(num_gpus))
+            mb = {m: (max_batch or {}).get(m, 32) for m in self.models}
+            self.executors = [EngineExecutor(self, g, devices[g], mb) for g in range(num_gpus)]
+        else:
+            self.executors = [DutyCycleExecutor(self, g) for g in range(num_gpus)]
+            for e in self.executors:
+                e.start()
         self._monitor: Optional[threading.Thread] = None
         self._stop = threading.Event()
         self.lock = threading.Lock()
@@ -364,8 +425,12 @@ class SLOScheduler:
     def shutdown(self) -> None:
         self.stop_monitoring()
         for e in self.executors:
-            e.stop_flag.set()
+            if isinstance(e, EngineExecutor):
+                e.stop()
+            else:
+                e.stop_flag.set()
         for e in self.executors:
-            e.join(2)
+            if not isinstance(e, EngineExecutor):
+                e.join(2)
         self.job.set_shutdown(True)
         self.job.close()

@@ -142,3 +142,51 @@ def test_efficientnet_v2s_hip_matches_torch():
     ref = m._logits_torch(x)
     assert lg.shape == (2, 1000)
     assert _rel_err(lg, ref) < 5e-2, _rel_err(lg, ref)
+
+
+def test_slo_scheduler_engine_executor_colocates_two_models():
+    """Config 5 in miniature through the planner: two models on one GPU, the
+    native engine executes the Nexus plan (duty cycle, shares, batch sizes)."""
+    import time
+
+    from ray_dynamic_batching_amd.models.bert import BertConfig, BertForSequenceClassification
+    from ray_dynamic_batching_amd.planner import synthetic_profile
+    from ray_dynamic_batching_amd.planner.scheduler import SLOScheduler
+    from ray_dynamic_batching_amd.serve.servable import TensorCodec
+
+    def fac(seed):
+        return lambda device: BertForSequenceClassification(BertConfig.tiny(seq_len=64), device=device,
+                                                             backend="hip", seed=seed)
+    m0 = fac(0)("cuda")
+    codec = TensorCodec.for_model(m0)
+    prof = {"a": synthetic_profile(0.3, 0.01, 50, 1, batches=(1, 2, 4, 8, 16)),
+            "b": synthetic_profile(0.3, 0.02, 50, 1, batches=(1, 2, 4, 8, 16))}
+    s = SLOScheduler(prof, {"a": 50.0, "b": 80.0}, {"a": fac(0), "b": fac(1)}, {"a": codec, "b": codec},
+                     num_gpus=1, executor="engine", devices=[0], max_batch={"a": 16, "b": 16})
+    try:
+        s.check_and_update({"a": 400.0, "b": 200.0})
+        node = s.slots[0]
+        assert node is not None and set(node.models()) == {"a", "b"}
+        ids = m0.example_input(8, seed=2).cpu()
+        rids = {}
+        for i in range(300):
+            name = "a" if i % 3 else "b"
+            rids[s.submit(name, ids[i % 8].numpy())] = (name, i % 8)
+            time.sleep(0.001)
+        got = {}
+        t_end = time.time() + 60
+        while len(got) < len(rids) and time.time() < t_end:
+            for c in s.poll(512, 0.2):
+                got[c[0]] = c
+        assert len(got) == len(rids)
+        ok = [c for c in got.values() if c[1] == 0]
+        assert len(ok) >= 0.95 * len(rids)
+        ref = m0(ids.cuda()).cpu().numpy()
+        for rid, c in got.items():
+            name, k = rids[rid]
+            if c[1] == 0 and name == "a":
+                assert np.allclose(np.frombuffer(c[7], dtype=np.float32), ref[k], atol=2e-2)
+        st = s.get_stats()
+        assert st["a"]["completed"] > 0 and st["b"]["completed"] > 0
+    finally:
+        s.shutdown()
