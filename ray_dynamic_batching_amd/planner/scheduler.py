@@ -305,8 +305,15 @@ class SLOScheduler:
             self._backlog = keep
 
     def poll(self, max_n: int = 1024, timeout_s: float = 0.0):
-        with self._client_lock:
-            return self.client.poll(max_n, timeout_s)
+        # never block while holding the client lock: submitters (ingress threads)
+        # would starve behind a waiting poller
+        deadline = time.perf_counter() + timeout_s
+        while True:
+            with self._client_lock:
+                out = self.client.poll(max_n, 0)
+            if out or time.perf_counter() >= deadline:
+                return out
+            time.sleep(0.0002)
 
     # ----------------------------------------------------------- planning
     def start_monitoring(self) -> None:
