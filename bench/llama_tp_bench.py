@@ -1,0 +1,109 @@
+"""BASELINE config 4: Llama-3-8B bf16, tensor parallel over the node's GPUs
+(one process per GPU, RCCL over xGMI), prefill of <= 8 prompts.
+
+Each rank holds a 1/TP shard (column-parallel QKV / gate-up, row-parallel O /
+down with an all-reduce each, vocab-parallel LM head + all-gathered argmax).
+The whole prefill (kernels + RCCL collectives) is captured in ONE hipGraph per
+batch bucket and replayed; rank 0 is the serving front: it batches prompts,
+broadcasts the token ids over RCCL and returns next-token ids.
+
+    python bench/llama_tp_bench.py                      # TP=1 on one GPU
+    torchrun --nproc-per-node 8 --master-addr 127.0.0.1 bench/llama_tp_bench.py
+Reports per-batch prefill latency (p50 over replays) and prompts/s for
+batches 1, 2, 4, 8 of --seq tokens.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--seq", type=int, default=128)
+    ap.add_argument("--layers", type=int, default=32)
+    ap.add_argument("--batches", default="1,2,4,8")
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--json-out", default="")
+    a = ap.parse_args(argv)
+
+    import torch
+    import torch.distributed as dist
+
+    from ray_dynamic_batching_amd.models.llama import LlamaConfig, LlamaTP
+    from ray_dynamic_batching_amd.parallel import collective as col
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        col.init_collective_group(world, rank, "nccl", "tp")
+    cfg = LlamaConfig.llama3_8b(seq_len=a.seq, layers=a.layers)
+    t0 = time.time()
+    m = LlamaTP(cfg, rank, world, "tp" if world > 1 else None, device=f"cuda:{local}", init="shard")
+    init_s = time.time() - t0
+    results = []
+    for b in [int(x) for x in a.batches.split(",")]:
+        ids = m.example_input(b, seed=b)
+        if world > 1:                      # rank 0 is the front end: it owns the prompts
+            col.broadcast(ids, 0, "tp")
+        with torch.no_grad():
+            for _ in range(2):
+                out = m(ids)
+            torch.cuda.synchronize()
+            if not a.no_graph:
+                side = torch.cuda.Stream()
+                side.wait_stream(torch.cuda.current_stream())
+                with torch.cuda.stream(side):
+                    m(ids)
+                torch.cuda.current_stream().wait_stream(side)
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    out = m(ids)
+                step = g.replay
+            else:
+                def step():
+                    m(ids)
+            if world > 1:
+                dist.barrier()
+            times = []
+            for _ in range(a.iters):
+                s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                s.record()
+                step()
+                e.record()
+                torch.cuda.synchronize()
+                times.append(s.elapsed_time(e))
+        times.sort()
+        p50 = times[len(times) // 2]
+        t = torch.tensor([p50], device="cuda")
+        if world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        p50 = t.item()
+        tokens = b * a.seq
+        flops = 2 * 8.0e9 * tokens * (a.layers / 32)
+        results.append(dict(batch=b, prefill_ms=round(p50, 3), prompts_per_s=round(b / p50 * 1e3, 1),
+                            tokens_per_s=round(tokens / p50 * 1e3, 1), tflops_whole_node=round(flops / p50 / 1e9, 1),
+                            next_token=int(out[0, 0].item())))
+    if rank == 0:
+        rep = dict(metric="Llama-3-8B bf16 TP prefill latency", tp=world, seq_len=a.seq, layers=a.layers,
+                   graph=not a.no_graph, init_s=round(init_s, 1), results=results,
+                   data="synthetic token ids, random-init weights")
+        print(json.dumps(rep), flush=True)
+        if a.json_out:
+            with open(a.json_out, "w") as f:
+                json.dump(rep, f, indent=1)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -92,3 +92,10 @@ def _efficientnet(device="cuda", backend="hip", **kw):
     from .efficientnet import EfficientNetV2S
 
     return EfficientNetV2S(device=device, backend=backend, **kw)
+
+
+@register("vit-g16")
+def _vit_g16(device="cuda", backend="hip", **kw):
+    from .vit import ViT, ViTConfig
+
+    return ViT(ViTConfig.g16(), device=device, backend=backend, **kw)

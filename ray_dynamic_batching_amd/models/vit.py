@@ -43,6 +43,12 @@ class ViTConfig:
         return ViTConfig(**d)
 
     @staticmethod
+    def g16(**kw):  # the fork's profiled "vit_g16" class (~1.85B params, vit_g16_*_report.txt:289-291)
+        d = dict(patch=16, hidden=1664, layers=48, heads=13, mlp=8192)
+        d.update(kw)
+        return ViTConfig(**d)
+
+    @staticmethod
     def tiny(**kw):
         d = dict(image=64, patch=16, hidden=256, layers=2, heads=4, mlp=512, classes=100)
         d.update(kw)
