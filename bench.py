@@ -41,13 +41,31 @@ def parse():
     ap.add_argument("--concurrency", type=int, default=96, help="closed-loop requests in flight per GPU")
     ap.add_argument("--rate", type=float, default=0.0, help="open-loop Poisson rate per GPU (req/s); 0 = closed loop")
     ap.add_argument("--seq", type=int, default=128)
-    ap.add_argument("--backend", default="hip", choices=["hip", "torch"])
+    ap.add_argument("--backend", default="hip", choices=["hip", "torch", "echo"],
+                    help="echo = CPU rehearsal of the multi-rank path (native fake replicas, gloo)")
+    ap.add_argument("--echo-service-us", type=float, default=1400.0, help="echo backend: batch service time")
     ap.add_argument("--pipeline-depth", type=int, default=4)
     ap.add_argument("--compute-streams", type=int, default=2, help="batches executing concurrently per GPU")
     ap.add_argument("--layers", type=int, default=12)
     ap.add_argument("--json-out", default="")
     ap.add_argument("--trace-out", default="", help="write a Chrome trace of the replicas' batches")
     return ap.parse_args()
+
+
+class _EchoRunner:
+    """CPU stand-in for EngineRunner (native EchoServer fake replica)."""
+
+    def __init__(self, srv):
+        self.srv = srv
+
+    def start(self):
+        self.srv.start()
+
+    def stop(self):
+        self.srv.stop()
+
+    def error(self):
+        return ""
 
 
 def main():
@@ -58,11 +76,19 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    echo = args.backend == "echo"
+    if echo:
+        if world > 1:
+            dist.init_process_group("gloo")
+    elif world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     else:
         torch.cuda.set_device(0)
+
+    def sync():
+        if not echo:
+            torch.cuda.synchronize()
 
     from ray_dynamic_batching_amd.models.bert import BertConfig, BertForSequenceClassification
     from ray_dynamic_batching_amd.runtime import job as rjob
@@ -85,10 +111,13 @@ def main():
     job.configure_queue(rank, rank, 0, args.concurrency * 2, 0.0, True)
 
     cfg = BertConfig(seq_len=args.seq, layers=args.layers)
-    model = BertForSequenceClassification(cfg, device="cuda", backend=args.backend)
-    spec = SessionSpec(model=model, queue=rank, max_batch=args.max_batch, max_wait_s=args.max_wait_ms / 1e3)
-    runner = EngineRunner(name, rank, [spec], pipeline_depth=args.pipeline_depth,
-                          compute_streams=args.compute_streams).build()
+    if echo:
+        runner = _EchoRunner(rjob.EchoServer(job, rank, [rank], args.max_batch, args.echo_service_us, 0.0, 8))
+    else:
+        model = BertForSequenceClassification(cfg, device="cuda", backend=args.backend)
+        spec = SessionSpec(model=model, queue=rank, max_batch=args.max_batch, max_wait_s=args.max_wait_ms / 1e3)
+        runner = EngineRunner(name, rank, [spec], pipeline_depth=args.pipeline_depth,
+                              compute_streams=args.compute_streams).build()
     runner.start()
     barrier()
 
@@ -107,7 +136,7 @@ def main():
         rate = args.rate * n
         lg.run(args.warmup * per_step, conc, rate, 0.0, False, 600.0)
     barrier()
-    torch.cuda.synchronize()
+    sync()
     if rank == 0:
         job.reset_stats()
         rep0 = [job.replica_stats(r) for r in range(n)]
@@ -116,12 +145,12 @@ def main():
     if rank == 0:
         result = lg.run(args.steps * per_step, conc, rate, 0.0, True, 1200.0)
     barrier()
-    torch.cuda.synchronize()
+    sync()
     elapsed = time.perf_counter() - t0
     barrier()
     err = runner.error()
     if world > 1:
-        t = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
+        t = torch.tensor([elapsed], device="cpu" if echo else "cuda", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
     if rank == 0 and args.trace_out:
