@@ -51,7 +51,7 @@ def _aligned(t: torch.Tensor, n: int = 16) -> bool:
 # while a hipGraph is being captured (those calls use the cached choice, or the
 # on-device heuristic if the shape was never seen eagerly).
 # ---------------------------------------------------------------------------
-NUM_TILE_CFGS = 8
+NUM_TILE_CFGS = 13
 _TUNE: Dict[tuple, int] = {}
 
 

@@ -172,18 +172,26 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, char* lds, uint3
 }
 
 // ---- the kernel ---------------------------------------------------------------
+// 4 waves per block laid out WGM (along M) x 4/WGM (along N).  BN only has to
+// be a multiple of 16 x (4/WGM): the W tile is DMA'd in whole 32-row wave
+// pieces, rows past BN are zero-filled into LDS padding and never read --
+// this is what allows quantisation-exact tiles such as 128x144 (N = 2304 in
+// 16 column blocks, 512 tiles at M = 4096 = 2 per CU exactly).
 template <typename T, typename OutT, int BM, int BN, template <typename, int> class LoaderT, bool HAS_BIAS,
-          bool HAS_RES>
+          bool HAS_RES, int WGM = 2>
 __global__ void __launch_bounds__(256, 2)
 mfma_gemm_kernel(typename LoaderT<T, BM * 8 / 256>::Params ap, const T* __restrict__ W, int ldw,
                  OutT* __restrict__ C, int ldc, const T* __restrict__ bias,
                  const T* __restrict__ R, int ldr, int M, int N, int K, float alpha, int act) {
   constexpr int BK = 64;
-  constexpr int WM = BM / 2, WN = BN / 2;
+  constexpr int WGN = 4 / WGM;
+  constexpr int WM = BM / WGM, WN = BN / WGN;
   constexpr int TM = WM / 16, TN = WN / 16;
+  static_assert(WM % 16 == 0 && WN % 16 == 0 && BM % 32 == 0, "tile / wave layout mismatch");
   constexpr int A_CH = BM * 8 / 256;  // 16-B chunks per thread per A tile
-  constexpr int W_CH = BN * 8 / 256;
-  constexpr int kStage = (BM + BN) * BK * 2;  // bytes per LDS stage (A tile, then W tile)
+  constexpr int W_CH = (BN + 31) / 32;  // rounded up: rows >= BN are LDS padding
+  constexpr int BNP = W_CH * 32;
+  constexpr int kStage = (BM + BNP) * BK * 2;  // bytes per LDS stage (A tile, then W tile)
   typedef typename MfmaOp<T>::frag frag;
 
   __shared__ __attribute__((aligned(16))) char smem[2 * kStage];
@@ -191,7 +199,7 @@ mfma_gemm_kernel(typename LoaderT<T, BM * 8 / 256>::Params ap, const T* __restri
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wid = tid >> 6;
-  const int wm = wid >> 1, wn = wid & 1;
+  const int wm = wid / WGN, wn = wid % WGN;
 
   const int tiles_n = (N + BN - 1) / BN;
   const int tiles_m = (M + BM - 1) / BM;
@@ -211,7 +219,7 @@ mfma_gemm_kernel(typename LoaderT<T, BM * 8 / 256>::Params ap, const T* __restri
     const int row = dma_row(tid, W_CH, i);
     wch[i] = dma_chunk(tid, row);
     const int gn = n0 + row;
-    woff[i] = gn < N ? (uint32_t)((size_t)gn * ldw * sizeof(T)) : kOOB;
+    woff[i] = (row < BN && gn < N) ? (uint32_t)((size_t)gn * ldw * sizeof(T)) : kOOB;
   }
   // wave-uniform LDS bases of this wave's DMA pieces
   const int wid_u = __builtin_amdgcn_readfirstlane(wid);
@@ -251,6 +259,9 @@ mfma_gemm_kernel(typename LoaderT<T, BM * 8 / 256>::Params ap, const T* __restri
       for (int i = 0; i < TN; ++i)
 #pragma unroll
         for (int j = 0; j < TM; ++j) acc[i][j] = MfmaOp<T>::mma(wf[i], af[j], acc[i][j]);
+      // keep the two K-halves' fragments from being hoisted together (register
+      // pressure: the big tiles spilled without it)
+      if constexpr (TM * TN >= 16) __builtin_amdgcn_sched_barrier(0);
     }
   };
 
@@ -287,7 +298,9 @@ mfma_gemm_kernel(typename LoaderT<T, BM * 8 / 256>::Params ap, const T* __restri
       for (int q = 0; q < 4; ++q) bv[i][q] = 0.f;
     }
   }
-  float rv[TM][TN][4];
+  // residual kept PACKED (4 x 16-bit in 2 VGPRs) until it is added: halves the
+  // epilogue's register footprint (the unpacked tile made 128x128+ spill)
+  u32x2 rraw[TM][TN];
   if constexpr (HAS_RES) {
     const __amdgpu_buffer_rsrc_t rsrc = make_rsrc(R, (uint32_t)((size_t)(M - 1) * ldr * sizeof(T) + (size_t)n_out * sizeof(T)));
 #pragma unroll
@@ -298,28 +311,18 @@ mfma_gemm_kernel(typename LoaderT<T, BM * 8 / 256>::Params ap, const T* __restri
         const int n = n0 + wn * WN + i * 16 + fg * 4;
         if (!swiglu) {
           const uint32_t off = (m < M && n < N) ? (uint32_t)(((size_t)m * ldr + n) * sizeof(T)) : kOOB;
-          const u32x2 raw = bload8(rsrc, off);
-          const T* e = reinterpret_cast<const T*>(&raw);
-#pragma unroll
-          for (int q = 0; q < 4; ++q) rv[j][i][q] = (float)e[q];
+          rraw[j][i] = bload8(rsrc, off);
         } else {
           const uint32_t off = (m < M && n < N) ? (uint32_t)(((size_t)m * ldr + (n >> 1)) * sizeof(T)) : kOOB;
-          const uint32_t raw = bload4(rsrc, off);
-          const T* e = reinterpret_cast<const T*>(&raw);
-          rv[j][i][0] = (float)e[0];
-          rv[j][i][1] = (float)e[1];
+          rraw[j][i] = u32x2{bload4(rsrc, off), 0u};
         }
       }
     }
   }
-  // x = alpha * acc + bias (in place)
-#pragma unroll
-  for (int i = 0; i < TN; ++i)
-#pragma unroll
-    for (int j = 0; j < TM; ++j)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) acc[i][j][q] = alpha * acc[i][j][q] + bv[i][q];
-
+  auto rv = [&](int j, int i, int q) -> float {
+    const T* e = reinterpret_cast<const T*>(&rraw[j][i]);
+    return (float)e[q];
+  };
   if (swiglu) {
 #pragma unroll
     for (int j = 0; j < TM; ++j) {
@@ -327,9 +330,12 @@ mfma_gemm_kernel(typename LoaderT<T, BM * 8 / 256>::Params ap, const T* __restri
 #pragma unroll
       for (int i = 0; i < TN; ++i) {
         const int n = n0 + wn * WN + i * 16 + fg * 4;
-        float r0 = apply_act<ACT_SILU>(acc[i][j][0]) * acc[i][j][1];
-        float r1 = apply_act<ACT_SILU>(acc[i][j][2]) * acc[i][j][3];
-        if constexpr (HAS_RES) { r0 += rv[j][i][0]; r1 += rv[j][i][1]; }
+        float x[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) x[q] = alpha * acc[i][j][q] + bv[i][q];
+        float r0 = apply_act<ACT_SILU>(x[0]) * x[1];
+        float r1 = apply_act<ACT_SILU>(x[2]) * x[3];
+        if constexpr (HAS_RES) { r0 += rv(j, i, 0); r1 += rv(j, i, 1); }
         if (m < M && n < N) {
           OutT* cp = C + (size_t)m * ldc + (n >> 1);
           cp[0] = (OutT)r0;
@@ -339,59 +345,63 @@ mfma_gemm_kernel(typename LoaderT<T, BM * 8 / 256>::Params ap, const T* __restri
     }
     return;
   }
-  if constexpr (HAS_RES) {
-#pragma unroll
-    for (int i = 0; i < TN; ++i)
-#pragma unroll
-      for (int j = 0; j < TM; ++j)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) acc[i][j][q] += rv[j][i][q];
-  }
-#define RDB_ACT_LOOP(A)                                       \
-  _Pragma("unroll") for (int i = 0; i < TN; ++i)             \
-  _Pragma("unroll") for (int j = 0; j < TM; ++j)             \
-  _Pragma("unroll") for (int q = 0; q < 4; ++q) acc[i][j][q] = apply_act<A>(acc[i][j][q]);
-  switch (act) {
-    case ACT_GELU: RDB_ACT_LOOP(ACT_GELU) break;
-    case ACT_RELU: RDB_ACT_LOOP(ACT_RELU) break;
-    case ACT_TANH: RDB_ACT_LOOP(ACT_TANH) break;
-    case ACT_SILU: RDB_ACT_LOOP(ACT_SILU) break;
-    case ACT_GELU_TANH: RDB_ACT_LOOP(ACT_GELU_TANH) break;
-    case ACT_SIGMOID: RDB_ACT_LOOP(ACT_SIGMOID) break;
-    default: break;
-  }
-#undef RDB_ACT_LOOP
+  // y = act(alpha * acc + bias + residual), computed and stored fragment by
+  // fragment: only the accumulators stay live (a separate activation pass over
+  // the whole tile made the big tiles spill).  One switch selects the
+  // activation for the whole tile.
   const bool vec_ok = ((ldc & 3) == 0);
+  auto store_tile = [&](auto actf) {
 #pragma unroll
-  for (int j = 0; j < TM; ++j) {
-    const int m = m0 + wm * WM + j * 16 + fr;
+    for (int j = 0; j < TM; ++j) {
+      const int m = m0 + wm * WM + j * 16 + fr;
 #pragma unroll
-    for (int i = 0; i < TN; ++i) {
-      const int n = n0 + wn * WN + i * 16 + fg * 4;
-      if (m >= M || n >= N) continue;
-      OutT* cp = C + (size_t)m * ldc + n;
-      if (n + 3 < N && vec_ok) {
-        store4<OutT>(cp, acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
-      } else {
+      for (int i = 0; i < TN; ++i) {
+        const int n = n0 + wn * WN + i * 16 + fg * 4;
+        float y[4];
 #pragma unroll
-        for (int e = 0; e < 4; ++e)
-          if (n + e < N) cp[e] = (OutT)acc[i][j][e];
+        for (int q = 0; q < 4; ++q) {
+          float x = alpha * acc[i][j][q] + bv[i][q];
+          if constexpr (HAS_RES) x += rv(j, i, q);
+          y[q] = actf(x);
+        }
+        if (m >= M || n >= N) continue;
+        OutT* cp = C + (size_t)m * ldc + n;
+        if (n + 3 < N && vec_ok) {
+          store4<OutT>(cp, y[0], y[1], y[2], y[3]);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (n + e < N) cp[e] = (OutT)y[e];
+        }
       }
     }
+  };
+  switch (act) {
+    case ACT_GELU: store_tile([](float x) { return apply_act<ACT_GELU>(x); }); break;
+    case ACT_RELU: store_tile([](float x) { return apply_act<ACT_RELU>(x); }); break;
+    case ACT_TANH: store_tile([](float x) { return apply_act<ACT_TANH>(x); }); break;
+    case ACT_SILU: store_tile([](float x) { return apply_act<ACT_SILU>(x); }); break;
+    case ACT_GELU_TANH: store_tile([](float x) { return apply_act<ACT_GELU_TANH>(x); }); break;
+    case ACT_SIGMOID: store_tile([](float x) { return apply_act<ACT_SIGMOID>(x); }); break;
+    default: store_tile([](float x) { return x; }); break;
   }
 }
 
-// Tile table (index = the `cfg` argument).  4 waves per block in a 2x2 grid;
-// LDS = 2 stages x (BM + BN) x 64 x 2 B (64..96 KiB).  The host picks the entry
-// (autotuned per shape from Python, or the heuristic below): for the serving
-// shapes the dominant effect is wave quantisation -- #tiles vs 256 CUs x
-// blocks/CU -- so non-power-of-two tiles (128x192) matter.
-constexpr int kNumTiles = 8;
-constexpr int kTileBM[kNumTiles] = {128, 64, 128, 64, 128, 192, 256, 128};
-constexpr int kTileBN[kNumTiles] = {128, 128, 64, 64, 192, 128, 128, 256};
+// Tile table (index = the `cfg` argument): BM x BN with WGM waves along M.
+// LDS = 2 stages x (BM + BN rounded to 32) x 64 x 2 B.  The host picks the
+// entry (autotuned per shape from Python, or the heuristic below): for the
+// serving shapes the dominant effect is wave quantisation -- #tiles vs 256
+// CUs x blocks/CU -- hence the non-power-of-two tiles: 128x192 (N = 3072),
+// 128x144 (N = 2304), 64x96 / 128x48 (N = 768) each give exactly 512 tiles
+// at M = 4096 (BERT-base, batch 32).
+constexpr int kNumTiles = 13;
+constexpr int kTileBM[kNumTiles] = {128, 64, 128, 64, 128, 192, 256, 128, 128, 64, 128, 256, 128};
+constexpr int kTileBN[kNumTiles] = {128, 128, 64, 64, 192, 128, 128, 256, 144, 96, 96, 144, 48};
+constexpr int kTileWGM[kNumTiles] = {2, 2, 2, 2, 2, 2, 2, 2, 4, 2, 2, 4, 4};
 
 inline int tile_blocks_per_cu(int cfg) {
-  const int lds = 2 * (kTileBM[cfg] + kTileBN[cfg]) * 64 * 2;
+  const int bnp = (kTileBN[cfg] + 31) / 32 * 32;
+  const int lds = 2 * (kTileBM[cfg] + bnp) * 64 * 2;
   return std::min(2, 163840 / lds);
 }
 // Heuristic: minimise (rounds of blocks over 256 CUs) x (tile work / tile efficiency).
@@ -411,31 +421,36 @@ inline int pick_tile_cfg(int M, int N) {
 }
 
 template <typename T, typename OutT, template <typename, int> class LoaderT, bool HB, bool HR, int BM, int BN,
-          typename P>
+          int WGM = 2, typename P>
 void launch_one(const P& ap, const T* W, int ldw, OutT* C, int ldc, const T* bias, const T* R, int ldr, int M,
                 int N, int K, float alpha, int act, hipStream_t s) {
   const int nwg = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
-  hipLaunchKernelGGL((mfma_gemm_kernel<T, OutT, BM, BN, LoaderT, HB, HR>), dim3(nwg), dim3(256), 0, s, ap, W, ldw,
-                     C, ldc, bias, R, ldr, M, N, K, alpha, act);
+  hipLaunchKernelGGL((mfma_gemm_kernel<T, OutT, BM, BN, LoaderT, HB, HR, WGM>), dim3(nwg), dim3(256), 0, s, ap, W,
+                     ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act);
 }
 
 template <typename T, typename OutT, template <typename, int> class LoaderT, bool HB, bool HR, typename P>
 void launch_mfma_gemm_t(const P& ap, const T* W, int ldw, OutT* C, int ldc, const T* bias, const T* R,
                         int ldr, int M, int N, int K, float alpha, int act, hipStream_t s, int cfg) {
-#define RDB_TILE(IDX, BM_, BN_) \
-  case IDX: launch_one<T, OutT, LoaderT, HB, HR, BM_, BN_>(ap, W, ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act, s); break;
+#define RDB_TILE(IDX, BM_, BN_, WGM_) \
+  case IDX: launch_one<T, OutT, LoaderT, HB, HR, BM_, BN_, WGM_>(ap, W, ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act, s); break;
   if constexpr (std::is_same<OutT, float>::value) {
     // f32 output is only used by small heads: one tile shape
     launch_one<T, OutT, LoaderT, HB, HR, 64, 64>(ap, W, ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act, s);
   } else {
     switch (cfg) {
-      RDB_TILE(0, 128, 128)
-      RDB_TILE(1, 64, 128)
-      RDB_TILE(2, 128, 64)
-      RDB_TILE(4, 128, 192)
-      RDB_TILE(5, 192, 128)
-      RDB_TILE(6, 256, 128)
-      RDB_TILE(7, 128, 256)
+      RDB_TILE(0, 128, 128, 2)
+      RDB_TILE(1, 64, 128, 2)
+      RDB_TILE(2, 128, 64, 2)
+      RDB_TILE(4, 128, 192, 2)
+      RDB_TILE(5, 192, 128, 2)
+      RDB_TILE(6, 256, 128, 2)
+      RDB_TILE(7, 128, 256, 2)
+      RDB_TILE(8, 128, 144, 4)
+      RDB_TILE(9, 64, 96, 2)
+      RDB_TILE(10, 128, 96, 2)
+      RDB_TILE(11, 256, 144, 4)
+      RDB_TILE(12, 128, 48, 4)
       default: launch_one<T, OutT, LoaderT, HB, HR, 64, 64>(ap, W, ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act, s);
     }
   }

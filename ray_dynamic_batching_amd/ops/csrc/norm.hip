@@ -36,12 +36,21 @@ norm_kernel(const T* __restrict__ x, const T* __restrict__ res, T* __restrict__ 
   if (row >= rows) return;
   const T* xr = x + (size_t)row * D;
   float v[NV][4];
+  float gv[NV][4], bv[NV][4];
+  // gamma/beta are issued with the row loads so their latency overlaps the
+  // reductions instead of following them
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = i * 256 + lane * 4;
+    load4(xr + c, v[i]);
+    load4(gamma + c, gv[i]);
+    if (MODE == 0) load4(beta + c, bv[i]);
+  }
   float s = 0.f;
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
     {
       const int c = i * 256 + lane * 4;
-      load4(xr + c, v[i]);
       if (res != nullptr) {
         float r[4];
         load4(res + (size_t)row * D + c, r);
@@ -72,16 +81,13 @@ norm_kernel(const T* __restrict__ x, const T* __restrict__ res, T* __restrict__ 
   for (int i = 0; i < NV; ++i) {
     {
       const int c = i * 256 + lane * 4;
-      float g[4], o[4];
-      load4(gamma + c, g);
+      float o[4];
       if (MODE == 0) {
-        float b[4];
-        load4(beta + c, b);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) o[e] = (v[i][e] - mean) * rstd * g[e] + b[e];
+        for (int e = 0; e < 4; ++e) o[e] = (v[i][e] - mean) * rstd * gv[i][e] + bv[i][e];
       } else {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) o[e] = v[i][e] * rstd * g[e];
+        for (int e = 0; e < 4; ++e) o[e] = v[i][e] * rstd * gv[i][e];
       }
       st4(yr + c, o);
     }
