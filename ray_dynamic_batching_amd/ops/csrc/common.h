@@ -41,10 +41,24 @@ __device__ __forceinline__ float wave_max(float v) {
 // the output has N/2 columns and holds silu(gate_j) * up_j.
 enum Act : int { ACT_NONE = 0, ACT_GELU = 1, ACT_RELU = 2, ACT_TANH = 3, ACT_SILU = 4, ACT_GELU_TANH = 5, ACT_SWIGLU = 6, ACT_SIGMOID = 7 };
 
+// erf with |error| <= 1.5e-7 (Abramowitz & Stegun 7.1.26): one exp, one rcp,
+// five FMAs and no branches -- ocml's erff is a branchy piecewise polynomial
+// that dominated the GELU epilogue of the FFN-up GEMM.
+__device__ __forceinline__ float fast_erf(float x) {
+  const float a = fabsf(x);
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, a, 1.0f));
+  float p = fmaf(1.061405429f, t, -1.453152027f);
+  p = fmaf(p, t, 1.421413741f);
+  p = fmaf(p, t, -0.284496736f);
+  p = fmaf(p, t, 0.254829592f);
+  const float y = 1.0f - p * t * __expf(-a * a);
+  return copysignf(y, x);
+}
+
 template <int ACT>
 __device__ __forceinline__ float apply_act(float x) {
   if constexpr (ACT == ACT_GELU) {
-    return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f));
+    return 0.5f * x * (1.0f + fast_erf(x * 0.70710678118654752f));
   } else if constexpr (ACT == ACT_RELU) {
     return fmaxf(x, 0.0f);
   } else if constexpr (ACT == ACT_TANH) {

@@ -74,6 +74,7 @@ struct Session {
   // duty-cycle mode (Nexus): GPU time this session may use per cycle
   int64_t duty_share_ns = 0;
   int64_t used_ns = 0;                               // charged in the current cycle
+  uint64_t launched_cycle = UINT64_MAX;              // duty-cycle index of the last launch
   std::atomic<bool> active{true};                    // model loaded / unloaded by the planner
   Session() = default;
   Session(Session&& o) noexcept { *this = std::move(o); }
@@ -82,7 +83,8 @@ struct Session {
     in_row_bytes = o.in_row_bytes; out_row_bytes = o.out_row_bytes; priority = o.priority; slo_ns = o.slo_ns;
     drop_stale = o.drop_stale; est_ns = std::move(o.est_ns); graphs = std::move(o.graphs);
     out_dev = std::move(o.out_dev); in_dev = std::move(o.in_dev); ring = o.ring; peek_pos = o.peek_pos;
-    duty_share_ns = o.duty_share_ns; used_ns = o.used_ns; active.store(o.active.load());
+    duty_share_ns = o.duty_share_ns; used_ns = o.used_ns; launched_cycle = o.launched_cycle;
+    active.store(o.active.load());
     return *this;
   }
 };
@@ -321,32 +323,35 @@ class Engine {
     return best;
   }
   // Duty-cycle policy (fork GPUWorker.execute_schedule, scheduler.py:525-588, with
-  // the cycle-end sleep sign fixed): round-robin over the active sessions; a
-  // session may launch while its charged GPU time in this cycle is below its
-  // share; once every session with work is out of budget the launcher idles to
-  // the cycle boundary, where budgets reset.  Sessions without a share
-  // (duty_share 0) are unconstrained (work-conserving fill).
+  // the cycle-end sleep sign fixed): every `cycle` each planned session runs ONE
+  // batch of up to its planned size (Nexus: a session's batch per duty cycle),
+  // round-robin; its GPU time is charged against its share.  When every session
+  // with work has had its turn the launcher idles to the cycle boundary.
+  // Sessions without a share (duty_share 0) are unconstrained (work-conserving).
   int pick_duty_cycle() {
     const int64_t cyc = duty_cycle_ns_.load(std::memory_order_relaxed);
     const int64_t now = now_ns();
     if (cyc > 0 && now - cycle_start_ns_ >= cyc) {
-      cycle_start_ns_ = cyc > 0 && now - cycle_start_ns_ < 2 * cyc ? cycle_start_ns_ + cyc : now;
+      cycle_start_ns_ = now - cycle_start_ns_ < 2 * cyc ? cycle_start_ns_ + cyc : now;
+      ++cycle_idx_;
       for (auto& s : sessions_) s.used_ns = 0;
     }
     const size_t n = sessions_.size();
-    bool starved = false;
+    bool waiting = false;
     for (size_t k = 0; k < n; ++k) {
       const size_t i = (rr_next_ + k) % n;
       Session& s = sessions_[i];
       if (!s.active.load(std::memory_order_relaxed) || !s.ring.peek(s.peek_pos)) continue;
-      if (cyc > 0 && s.duty_share_ns > 0 && s.used_ns >= s.duty_share_ns) {
-        starved = true;
+      if (cyc > 0 && s.duty_share_ns > 0 &&
+          (s.launched_cycle == cycle_idx_ || s.used_ns >= s.duty_share_ns)) {
+        waiting = true;
         continue;
       }
       rr_next_ = (i + 1) % n;
+      s.launched_cycle = cycle_idx_;
       return (int)i;
     }
-    if (starved) {  // everyone with work is out of budget: idle until the cycle boundary
+    if (waiting) {  // everyone with work had its turn: idle until the cycle boundary
       const int64_t wait = cycle_start_ns_ + cyc - now_ns();
       if (wait > 0) std::this_thread::sleep_for(std::chrono::nanoseconds(std::min<int64_t>(wait, 2000000)));
     }
@@ -602,6 +607,7 @@ class Engine {
   long long fault_drop_every_ = 0, fault_delay_batch_us_ = 0, fault_kill_after_ = 0;
   long long fault_req_count_ = 0, fault_batch_count_ = 0;
   int64_t cycle_start_ns_ = 0;
+  uint64_t cycle_idx_ = 0;
   size_t rr_next_ = 0;
   std::vector<hipEvent_t> ev_copy_, ev_start_, ev_done_;
   std::vector<void*> host_ptrs_, host_out_;

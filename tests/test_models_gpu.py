@@ -124,8 +124,8 @@ def test_engine_concurrent_streams_match_single_stream():
 
 def test_engine_colocated_sessions_duty_cycle_shares():
     """Config 5 in miniature: two models on one GPU with per-model queues.  Under
-    the duty-cycle policy GPU time splits by the planned shares (15 vs 2 ms of
-    a 20 ms cycle), so the favoured queue drains while the other is throttled."""
+    the duty-cycle policy each session runs one batch of its planned size per
+    cycle (A: 16, B: 2), so A drains while B is throttled to its plan."""
     from ray_dynamic_batching_amd.models.bert import BertConfig, BertForSequenceClassification
     from ray_dynamic_batching_amd.runtime import job as rjob
     from ray_dynamic_batching_amd.runtime.engine import EngineRunner, SessionSpec
@@ -141,7 +141,9 @@ def test_engine_colocated_sessions_duty_cycle_shares():
     runner = EngineRunner(name, 0, [SessionSpec(model=ma, queue=0, max_batch=16, max_wait_s=0.001),
                                     SessionSpec(model=mb, queue=1, max_batch=16, max_wait_s=0.001)],
                           policy=EngineRunner.POLICY_DUTY_CYCLE).build()
-    runner.set_duty_cycle(20.0, [15.0, 2.0])
+    # Nexus plan: one batch per session per 5 ms cycle -- A batch 16, B batch 2
+    runner.set_duty_cycle(5.0, [4.0, 1.0])
+    runner.engine.set_max_batch(runner.sessions[1].sid, 2)
     try:
         c = rjob.Client(j)
         ids = ma.example_input(64, seed=3).cpu()
