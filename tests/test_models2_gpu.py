@@ -159,12 +159,13 @@ def test_slo_scheduler_engine_executor_colocates_two_models():
                                                              backend="hip", seed=seed)
     m0 = fac(0)("cuda")
     codec = TensorCodec.for_model(m0)
-    prof = {"a": synthetic_profile(0.3, 0.01, 50, 1, batches=(1, 2, 4, 8, 16)),
-            "b": synthetic_profile(0.3, 0.02, 50, 1, batches=(1, 2, 4, 8, 16))}
+    prof = {"a": synthetic_profile(0.3, 0.01, 50, 1, batches=(1, 2, 4, 8, 16, 32)),
+            "b": synthetic_profile(0.3, 0.02, 50, 1, batches=(1, 2, 4, 8, 16, 32))}
     s = SLOScheduler(prof, {"a": 50.0, "b": 80.0}, {"a": fac(0), "b": fac(1)}, {"a": codec, "b": codec},
-                     num_gpus=1, executor="engine", devices=[0], max_batch={"a": 16, "b": 16})
+                     num_gpus=1, executor="engine", devices=[0], max_batch={"a": 32, "b": 32})
     try:
-        s.check_and_update({"a": 400.0, "b": 200.0})
+        # planned rates above the ~600 + 300 req/s the loop below offers
+        s.check_and_update({"a": 900.0, "b": 450.0})
         node = s.slots[0]
         assert node is not None and set(node.models()) == {"a", "b"}
         ids = m0.example_input(8, seed=2).cpu()
