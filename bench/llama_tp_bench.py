@@ -30,6 +30,9 @@ def main(argv=None):
     ap.add_argument("--batches", default="1,2,4,8")
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--serve", action="store_true", help="serve prompts through the shm rings (TPReplica)")
+    ap.add_argument("--requests", type=int, default=400)
+    ap.add_argument("--concurrency", type=int, default=16)
     ap.add_argument("--json-out", default="")
     a = ap.parse_args(argv)
 
@@ -49,6 +52,8 @@ def main(argv=None):
     t0 = time.time()
     m = LlamaTP(cfg, rank, world, "tp" if world > 1 else None, device=f"cuda:{local}", init="shard")
     init_s = time.time() - t0
+    if a.serve:
+        return _serve(a, m, world, rank)
     results = []
     for b in [int(x) for x in a.batches.split(",")]:
         ids = m.example_input(b, seed=b)
@@ -103,6 +108,64 @@ def main(argv=None):
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def _serve(a, m, world, rank):
+    """Config 4 serving: prompts -> shm queue -> rank-0 batching (<= 8) -> RCCL
+    broadcast -> graph replay on every TP rank -> next-token completions."""
+    import threading
+
+    import torch
+    import torch.distributed as dist
+
+    from ray_dynamic_batching_amd.runtime import job as rjob
+    from ray_dynamic_batching_amd.runtime.tp_replica import TPReplica
+
+    name = f"llama_tp_{os.environ.get('MASTER_PORT', os.getpid())}"
+    job = None
+    if rank == 0:
+        job = rjob.Job(name, create=True, n_replicas=1, n_queues=1, n_clients=2, req_capacity=1024,
+                       req_slot_bytes=a.seq * 4, cmp_capacity=2048, cmp_slot_bytes=64)
+        job.configure_queue(0, 0, 0, 1024, 0.0, True)
+    buckets = [1, 2, 4, 8]
+    rep = TPReplica(m, name if rank == 0 else None, 0, 0, buckets, "tp" if world > 1 else None).capture()
+    if world > 1:
+        dist.barrier()
+    if rank != 0:
+        while rep.step() >= 0:
+            pass
+        dist.barrier()
+        dist.destroy_process_group()
+        return
+    ids = m.example_input(64, seed=3).cpu()
+    payloads = [ids[i].numpy().tobytes() for i in range(64)]
+    res = {}
+
+    def drive():
+        c = rjob.Client(job, 1)
+        lg = rjob.LoadGen(c, 0, payloads)
+        lg.run(min(64, a.requests), a.concurrency, 0.0, 0.0, False, 600.0)   # warmup
+        res.update(lg.run(a.requests, a.concurrency, 0.0, 0.0, True, 600.0))
+
+    t = threading.Thread(target=drive)
+    t.start()
+    while t.is_alive():
+        rep.step(0.01)
+    rep.stop_all()
+    lat = res["latency"]
+    rep_out = dict(metric="Llama-3-8B bf16 TP prefill serving (<= 8 prompts / batch)", tp=world, seq_len=a.seq,
+                   layers=a.layers, prompts_per_s=round(res["ok"] / res["elapsed_s"], 1),
+                   p50_ms=round(lat["p50_ms"], 3), p99_ms=round(lat["p99_ms"], 3), ok=res["ok"],
+                   mean_batch=round(job.replica_stats(0)["batch_items"] / max(1, job.replica_stats(0)["batches"]), 2),
+                   data="synthetic token ids, random-init weights")
+    print(json.dumps(rep_out), flush=True)
+    if a.json_out:
+        with open(a.json_out, "w") as f:
+            json.dump(rep_out, f, indent=1)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    job.close()
 
 
 if __name__ == "__main__":

@@ -191,3 +191,32 @@ def test_slo_scheduler_engine_executor_colocates_two_models():
         assert st["a"]["completed"] > 0 and st["b"]["completed"] > 0
     finally:
         s.shutdown()
+
+
+def test_tp_replica_serves_llama_tp1_through_rings():
+    import threading
+
+    from ray_dynamic_batching_amd.models.llama import LlamaConfig, LlamaTP
+    from ray_dynamic_batching_amd.runtime import job as rjob
+    from ray_dynamic_batching_amd.runtime.tp_replica import TPReplica
+
+    m = LlamaTP(LlamaConfig.tiny(seq_len=64), device="cuda", backend="hip", init="full")
+    name = rjob.unique_job_name("tp")
+    j = rjob.Job(name, create=True, n_replicas=1, n_queues=1, n_clients=2, req_slot_bytes=64 * 4, cmp_slot_bytes=64)
+    j.configure_queue(0, 0, 0, 256, 0.0, True)
+    try:
+        rep = TPReplica(m, name, 0, 0, [1, 2, 4, 8]).capture()
+        ids = m.example_input(20, seed=9).cpu()
+        c = rjob.Client(j, 1)
+        rids = {c.submit(0, ids[i].numpy().tobytes()): i for i in range(20)}
+        got = {}
+        while len(got) < 20:
+            rep.step(0.01)
+            for rid, st, q, ts, td, tr, kind, payload in c.poll(64, 0.0):
+                assert st == 0
+                got[rids[rid]] = np.frombuffer(payload, dtype=np.int32)
+        ref = m(ids.cuda()).cpu().numpy()
+        assert all(got[i][0] == ref[i][0] for i in range(20))
+        assert rep.batches >= 3
+    finally:
+        j.close()
