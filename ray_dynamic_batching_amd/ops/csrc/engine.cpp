@@ -283,6 +283,7 @@ class Engine {
     d["dropped"] = dropped_.load();
     d["padded"] = padded_.load();
     d["gpu_busy_ms"] = gpu_busy_ms_.load();
+    d["backfill_batches"] = backfills_.load();
     d["error"] = error();
     return d;
   }
@@ -351,9 +352,32 @@ class Engine {
       s.launched_cycle = cycle_idx_;
       return (int)i;
     }
-    if (waiting) {  // everyone with work had its turn: idle until the cycle boundary
-      const int64_t wait = cycle_start_ns_ + cyc - now_ns();
-      if (wait > 0) std::this_thread::sleep_for(std::chrono::nanoseconds(std::min<int64_t>(wait, 2000000)));
+    if (waiting) {
+      // Work-conserving backfill: every session with work already had its turn.
+      // Rather than idle, run another batch of the session with the oldest head
+      // request IF it finishes before the next cycle starts (estimated), so
+      // the planned turns of the next cycle are never delayed.
+      const int64_t left = cycle_start_ns_ + cyc - now_ns();
+      int best = -1;
+      int64_t oldest = INT64_MAX;
+      for (size_t i = 0; i < n; ++i) {
+        Session& s = sessions_[i];
+        if (!s.active.load(std::memory_order_relaxed)) continue;
+        SlotHeader* h = s.ring.peek(s.peek_pos);
+        if (!h) continue;
+        const uint64_t depth = s.ring.h->head.load(std::memory_order_relaxed) - s.peek_pos;
+        const int bi = bucket_for(s, (int)std::min<uint64_t>(depth, (uint64_t)s.max_batch));
+        if ((double)left < s.est_ns[bi]) continue;
+        if (h->t_submit_ns < oldest) {
+          oldest = h->t_submit_ns;
+          best = (int)i;
+        }
+      }
+      if (best >= 0) {
+        ++backfills_;
+        return best;
+      }
+      if (left > 0) std::this_thread::sleep_for(std::chrono::nanoseconds(std::min<int64_t>(left, 2000000)));
     }
     return -1;
   }
@@ -608,6 +632,7 @@ class Engine {
   long long fault_req_count_ = 0, fault_batch_count_ = 0;
   int64_t cycle_start_ns_ = 0;
   uint64_t cycle_idx_ = 0;
+  std::atomic<uint64_t> backfills_{0};
   size_t rr_next_ = 0;
   std::vector<hipEvent_t> ev_copy_, ev_start_, ev_done_;
   std::vector<void*> host_ptrs_, host_out_;
