@@ -354,12 +354,13 @@ class Engine {
     }
     if (waiting) {
       // Work-conserving backfill: every session with work already had its turn.
-      // Rather than idle, run another batch of the session with the oldest head
-      // request IF it finishes before the next cycle starts (estimated), so
-      // the planned turns of the next cycle are never delayed.
+      // Rather than idle, run another batch IF it finishes before the next
+      // cycle starts (estimated), so the planned turns are never delayed; the
+      // spare time goes to the session least served relative to its share
+      // (used / share), so overload is split in the planned proportions.
       const int64_t left = cycle_start_ns_ + cyc - now_ns();
       int best = -1;
-      int64_t oldest = INT64_MAX;
+      double best_key = 1e300;
       for (size_t i = 0; i < n; ++i) {
         Session& s = sessions_[i];
         if (!s.active.load(std::memory_order_relaxed)) continue;
@@ -368,8 +369,10 @@ class Engine {
         const uint64_t depth = s.ring.h->head.load(std::memory_order_relaxed) - s.peek_pos;
         const int bi = bucket_for(s, (int)std::min<uint64_t>(depth, (uint64_t)s.max_batch));
         if ((double)left < s.est_ns[bi]) continue;
-        if (h->t_submit_ns < oldest) {
-          oldest = h->t_submit_ns;
+        const double key = (double)s.used_ns / (double)std::max<int64_t>(1, s.duty_share_ns) +
+                           1e-12 * (double)(h->t_submit_ns & 0xFFFFFFF);  // tie-break: older head first
+        if (key < best_key) {
+          best_key = key;
           best = (int)i;
         }
       }
