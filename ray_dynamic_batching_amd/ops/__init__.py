@@ -170,7 +170,7 @@ def _norm(x, gamma, beta, eps, residual, residual_out, mode):
     _check(x.is_cuda and x.is_contiguous() and x.dtype in (torch.bfloat16, torch.float16), "norm: bad x")
     D = x.shape[-1]
     rows = x.numel() // D
-    _check(D % 256 == 0 and D <= 8192, "norm: D must be a multiple of 256, <= 8192")
+    _check(D % 4 == 0 and D <= 8192, "norm: D must be a multiple of 4, <= 8192")
     _check(gamma.numel() == D and gamma.dtype == x.dtype, "norm: bad gamma")
     if beta is not None:
         _check(beta.numel() == D and beta.dtype == x.dtype, "norm: bad beta")

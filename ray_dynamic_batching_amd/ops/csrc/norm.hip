@@ -39,19 +39,26 @@ norm_kernel(const T* __restrict__ x, const T* __restrict__ res, T* __restrict__ 
   float gv[NV][4], bv[NV][4];
   // gamma/beta are issued with the row loads so their latency overlaps the
   // reductions instead of following them
+  // rows need not be a multiple of 256: lanes past D (last vector only) hold
+  // zeros, are excluded from the variance and are not stored
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
     const int c = i * 256 + lane * 4;
-    load4(xr + c, v[i]);
-    load4(gamma + c, gv[i]);
-    if (MODE == 0) load4(beta + c, bv[i]);
+    if (c < D) {
+      load4(xr + c, v[i]);
+      load4(gamma + c, gv[i]);
+      if (MODE == 0) load4(beta + c, bv[i]);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[i][e] = gv[i][e] = bv[i][e] = 0.f;
+    }
   }
   float s = 0.f;
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
     {
       const int c = i * 256 + lane * 4;
-      if (res != nullptr) {
+      if (res != nullptr && c < D) {
         float r[4];
         load4(res + (size_t)row * D + c, r);
 #pragma unroll
@@ -68,9 +75,11 @@ norm_kernel(const T* __restrict__ x, const T* __restrict__ res, T* __restrict__ 
     mean = s / D;
     float q = 0.f;
 #pragma unroll
-    for (int i = 0; i < NV; ++i)
-  #pragma unroll
-        for (int e = 0; e < 4; ++e) { const float d = v[i][e] - mean; q += d * d; }
+    for (int i = 0; i < NV; ++i) {
+      if (i * 256 + lane * 4 >= D) continue;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { const float d = v[i][e] - mean; q += d * d; }
+    }
     q = wave_sum(q);
     rstd = rsqrtf(q / D + eps);
   } else {
@@ -89,7 +98,7 @@ norm_kernel(const T* __restrict__ x, const T* __restrict__ res, T* __restrict__ 
 #pragma unroll
         for (int e = 0; e < 4; ++e) o[e] = v[i][e] * rstd * gv[i][e];
       }
-      st4(yr + c, o);
+      if (c < D) st4(yr + c, o);
     }
   }
 }
@@ -157,10 +166,19 @@ static void check_d(int D) {
     throw std::invalid_argument("norm: row length must be 256*NV with NV in {1..6,8,10,12,14,16,20,24,28,32}");
 }
 
+static int norm_nv(int D) {  // smallest instantiated NV covering the row
+  const int need = (D + 255) / 256;
+  int best = 1 << 30;
+#define RDB_PICK(N) if (N >= need && N < best) best = N;
+  RDB_NV_LIST(RDB_PICK)
+#undef RDB_PICK
+  return best;
+}
+
 template <typename T, int MODE>
 static void launch_norm(dim3 grid, hipStream_t s, uintptr_t x, uintptr_t res, uintptr_t res_out,
                         uintptr_t gamma, uintptr_t beta, uintptr_t y, int rows, int D, float eps) {
-  const int nv = D / 256;
+  const int nv = norm_nv(D);
 #define RDB_CASE(N)                                                                             \
   if (nv == N) {                                                                                \
     hipLaunchKernelGGL((norm_kernel<T, MODE, N>), grid, dim3(256), 0, s, (const T*)x,          \
@@ -190,7 +208,7 @@ static void launch_embed(dim3 grid, hipStream_t s, uintptr_t ids, uintptr_t type
 
 void norm_fwd(int dtype, int mode, uintptr_t x, uintptr_t res, uintptr_t res_out, uintptr_t gamma,
               uintptr_t beta, uintptr_t y, int rows, int D, float eps, uintptr_t stream) {
-  check_d(D);
+  if (D % 4 != 0 || D <= 0 || D > 8192) throw std::invalid_argument("norm: D must be a multiple of 4, <= 8192");
   if (rows <= 0) return;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   dim3 grid((rows + 3) / 4);

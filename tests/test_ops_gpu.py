@@ -255,3 +255,19 @@ def test_se_scale_and_sigmoid_gemm():
     y = ops.linear(a, w, bias, act="sigmoid")
     r = ops.linear_ref(a, w, bias, act="sigmoid")
     assert torch.allclose(y.float(), r.float(), atol=5e-3)
+
+
+@pytest.mark.parametrize("D", [100, 1664, 4100])
+def test_norms_non_multiple_of_256(D):
+    from ray_dynamic_batching_amd import ops
+
+    torch.manual_seed(D)
+    x = torch.randn(37, D, device="cuda", dtype=torch.bfloat16)
+    r = torch.randn(37, D, device="cuda", dtype=torch.bfloat16)
+    g = torch.rand(D, device="cuda", dtype=torch.bfloat16) + 0.5
+    b = torch.randn(D, device="cuda", dtype=torch.bfloat16)
+    y = ops.layer_norm(x, g, b, 1e-5, residual=r)
+    ref = ops.layer_norm_ref(x, g, b, 1e-5, residual=r)
+    assert torch.allclose(y.float(), ref.float(), atol=3e-2, rtol=3e-2)
+    y2 = ops.rms_norm(x, g, 1e-5)
+    assert torch.allclose(y2.float(), ops.rms_norm_ref(x, g, 1e-5).float(), atol=3e-2, rtol=3e-2)
