@@ -62,6 +62,7 @@ class BertForSequenceClassification:
         if backend == "hip" and self.device.type != "cuda":
             raise ValueError("the hip backend needs a GPU device")
         self.backend = backend
+        self.cls_only_last_layer = True
         g = torch.Generator(device="cpu").manual_seed(seed)
         D, I = cfg.hidden, cfg.intermediate
 
@@ -126,15 +127,22 @@ class BertForSequenceClassification:
         D, H = c.hidden, c.heads
         lens = (ids != c.pad_token_id).sum(dim=1, dtype=torch.int32).clamp_(min=1)
         h = ops.embed_ln(ids, self.word, self.pos, self.typ, self.emb_g, self.emb_b, c.eps)
-        for L in self.layers:
+        n = len(self.layers)
+        for i, L in enumerate(self.layers):
             qkv = ops.linear(h, L["w_qkv"], L["b_qkv"])
             ctx = ops.attention(qkv, B, S, H, H, D // H, lens=lens)
+            if i == n - 1 and self.cls_only_last_layer:
+                # Only the [CLS] row of the last layer reaches the pooler: its
+                # keys/values need every token, but the o-proj, LN and FFN after
+                # attention are row-wise, so they run on the B CLS rows (strided
+                # views, no copy) instead of B*S -- the same logits, ~1/12 fewer FLOPs.
+                ctx, h = ctx.view(B, S, D)[:, 0, :], h.view(B, S, D)[:, 0, :]
             a = ops.linear(ctx, L["w_o"], L["b_o"], residual=h)
             h1 = ops.layer_norm(a, L["ln1_g"], L["ln1_b"], c.eps)
             inter = ops.linear(h1, L["w_i"], L["b_i"], act="gelu")
             o = ops.linear(inter, L["w_out"], L["b_out"], residual=h1)
             h = ops.layer_norm(o, L["ln2_g"], L["ln2_b"], c.eps)
-        cls = h.view(B, S, D)[:, 0, :]
+        cls = h if self.cls_only_last_layer else h.view(B, S, D)[:, 0, :]
         pooled = ops.linear(cls, self.w_pool, self.b_pool, act="tanh")
         return ops.linear(pooled, self.w_cls, self.b_cls, out_dtype=torch.float32)
 

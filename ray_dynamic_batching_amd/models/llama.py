@@ -15,7 +15,9 @@ Per rank (TP = t, MI355X-first layout):
     last-token logits, takes a local (max, argmax) and only 2 x B numbers are
     all-gathered to pick the global next token.
 Two all-reduces of T x hidden bf16 per layer -- sized for the 7-link xGMI mesh
-(see parallel.collective.xgmi_allreduce_time_model).
+(see parallel.collective.xgmi_allreduce_time_model).  With the custom xGMI
+all-reduce enabled on the group (parallel.xgmi, push-based one/two-shot over
+peer memory) each all-reduce also applies the following RMSNorm.
 """
 from __future__ import annotations
 
@@ -66,6 +68,7 @@ class LlamaTP:
             raise ValueError("heads, kv_heads, intermediate and vocab must be divisible by tp_size")
         self.rank, self.tp = tp_rank, tp_size
         self.group = group_name
+        self.use_xgmi = True          # custom xGMI all-reduce when the group has one (collective.enable_xgmi)
         self.device = torch.device(device)
         self.dtype = dtype
         self.backend = backend
@@ -163,12 +166,22 @@ class LlamaTP:
             return self._layers_hip(ids)
         return self._layers_torch(ids)
 
+    def _xgmi(self):
+        if self.tp == 1 or not self.use_xgmi:
+            return None
+        from ..parallel import collective as col
+
+        return col.get_xgmi(self.group or "default")
+
     def _layers_hip(self, ids):
         c = self.cfg
         B, S = ids.shape
         Dh = c.head_dim
         x = self.embed[ids.long().clamp_(0, c.vocab_size - 1)].reshape(B * S, c.hidden)
         first = self.rank == 0
+        xg = self._xgmi()
+        if xg is not None and B * S * c.hidden <= xg.max_elems:
+            return self._layers_hip_xgmi(x, B, S, xg)
         for L in self.layers:
             h = ops.rms_norm(x, L["attn_norm"], c.eps)
             qkv = ops.linear(h, L["w_qkv"])
@@ -178,6 +191,31 @@ class LlamaTP:
             h = ops.rms_norm(x, L["mlp_norm"], c.eps)
             g = ops.linear(h, L["w_gu"], act="swiglu")
             x = self._allreduce(ops.linear(g, L["w_down"], residual=x if first else None))
+        return x
+
+    def _layers_hip_xgmi(self, x, B, S, xg):
+        """TP layers with the custom xGMI all-reduce: each all-reduce also
+        applies the NEXT RMSNorm (fused in the all-gather phase), so a layer is
+        qkv GEMM -> RoPE -> attention -> o GEMM(+res) -> AR+norm -> gate/up
+        GEMM(SwiGLU) -> down GEMM(+res) -> AR+norm; x lives in the
+        communicator's gather buffer between the two all-reduces."""
+        c = self.cfg
+        Dh = c.head_dim
+        first = self.rank == 0
+        h = ops.rms_norm(x, self.layers[0]["attn_norm"], c.eps)
+        n = len(self.layers)
+        for i, L in enumerate(self.layers):
+            qkv = ops.linear(h, L["w_qkv"])
+            ops.rope_(qkv, self.cos, self.sin, B, S, self.Hl, self.Hkvl, Dh)
+            a = ops.attention(qkv, B, S, self.Hl, self.Hkvl, Dh, causal=True)
+            o = ops.linear(a, L["w_o"], residual=x if first else None)
+            x, h = xg.all_reduce_rmsnorm(o, L["mlp_norm"], c.eps)
+            g = ops.linear(h, L["w_gu"], act="swiglu")
+            d = ops.linear(g, L["w_down"], residual=x if first else None)
+            if i + 1 < n:
+                x, h = xg.all_reduce_rmsnorm(d, self.layers[i + 1]["attn_norm"], c.eps)
+            else:
+                x = xg.all_reduce(d)
         return x
 
     def _layers_torch(self, ids):

@@ -118,9 +118,13 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
         _check(bias.is_contiguous() and bias.numel() == N and bias.dtype == x.dtype, "linear: bad bias")
     ldr = 0
     if residual is not None:
-        _check(residual.dtype == x.dtype and residual.shape[-1] == n_out and residual.is_contiguous()
-               and residual.numel() == M * n_out, "linear: bad residual")
-        ldr = n_out
+        if residual.dim() == 2 and residual.stride(1) == 1 and residual.shape[0] == M:
+            ldr = residual.stride(0)          # 2-D row-strided view (e.g. the CLS rows)
+        else:
+            _check(residual.is_contiguous() and residual.numel() == M * n_out, "linear: bad residual")
+            ldr = n_out
+        _check(residual.dtype == x.dtype and residual.shape[-1] == n_out and ldr % 4 == 0
+               and _aligned(residual, 8), "linear: bad residual")
     args = (DTYPE_CODE[x.dtype], DTYPE_CODE[od], x2.data_ptr(), lda, w.data_ptr(), K, out.data_ptr(),
             n_out, _ptr(bias), _ptr(residual), ldr, M, N, K, float(alpha), ACT_CODE[act])
     fn = _ops().gemm_tn

@@ -4,6 +4,7 @@
 // the launches are capturable into hipGraphs (torch.cuda.graph).
 #include <hip/hip_runtime.h>
 #include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
 #include <stdexcept>
 #include <string>
 
@@ -38,6 +39,18 @@ void shuffle_remap(uintptr_t A, int ldA, uintptr_t B, int ldB, int Ch, long pixe
                    uintptr_t O2, int ld2, int split, uintptr_t stream);
 void se_scale(uintptr_t x, uintptr_t s, uintptr_t y, int N, long HW, int C, uintptr_t stream);
 void register_engine(py::module_& m);
+size_t xgmi_signal_bytes();
+void xgmi_allreduce(int dtype, const std::vector<uintptr_t>& recv, const std::vector<uintptr_t>& gather,
+                    const std::vector<uintptr_t>& sig, int rank, uintptr_t in, uintptr_t out_norm,
+                    uintptr_t gamma, float eps, int T, int D, long long slot_elems, int two_shot,
+                    int grid, unsigned long long timeout_ticks, uintptr_t stream);
+uintptr_t xgmi_alloc_uncached(size_t bytes);
+void xgmi_free(uintptr_t p);
+std::string xgmi_ipc_handle(uintptr_t p);
+uintptr_t xgmi_ipc_open(const std::string& handle);
+void xgmi_ipc_close(uintptr_t p);
+uint32_t xgmi_read_error(uintptr_t sig);
+unsigned long long xgmi_ticks_per_second();
 }  // namespace rdb
 
 static void hip_check(hipError_t e, const char* what) {
@@ -77,5 +90,16 @@ PYBIND11_MODULE(_rdb_ops, m) {
     if (hipGetDeviceCount(&n) != hipSuccess) return 0;
     return n;
   });
+
+  // Custom all-reduce over xGMI peer memory (xgmi.hip) for TP groups.
+  m.def("xgmi_signal_bytes", &rdb::xgmi_signal_bytes);
+  m.def("xgmi_allreduce", &rdb::xgmi_allreduce, py::call_guard<py::gil_scoped_release>());
+  m.def("xgmi_alloc_uncached", &rdb::xgmi_alloc_uncached);
+  m.def("xgmi_free", &rdb::xgmi_free);
+  m.def("xgmi_ipc_handle", [](uintptr_t p) { return py::bytes(rdb::xgmi_ipc_handle(p)); });
+  m.def("xgmi_ipc_open", [](py::bytes h) { return rdb::xgmi_ipc_open(std::string(h)); });
+  m.def("xgmi_ipc_close", &rdb::xgmi_ipc_close);
+  m.def("xgmi_read_error", &rdb::xgmi_read_error);
+  m.def("xgmi_ticks_per_second", &rdb::xgmi_ticks_per_second);
   rdb::register_engine(m);
 }

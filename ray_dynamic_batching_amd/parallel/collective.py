@@ -38,6 +38,7 @@ class _Group:
         self.rank = rank
         self.backend = backend
         self.pg = pg
+        self.xgmi = None   # optional parallel.xgmi.XgmiCommunicator (enable_xgmi)
 
 
 _groups: Dict[str, _Group] = {}
@@ -98,6 +99,9 @@ def is_group_initialized(group_name: str = "default") -> bool:
 def destroy_collective_group(group_name: str = "default") -> None:
     with _lock:
         g = _groups.pop(group_name, None)
+    if g is not None and g.xgmi is not None:
+        g.xgmi.close()
+        g.xgmi = None
     if g is not None and g.pg is not dist.group.WORLD:
         dist.destroy_process_group(g.pg)
     if not _groups and dist.is_initialized() and g is not None and g.pg is dist.group.WORLD:
@@ -123,8 +127,48 @@ def get_group_handle(group_name: str = "default"):
     return _g(group_name).pg
 
 
+def enable_xgmi(group_name: str = "default", **kw):
+    """Attach the custom xGMI all-reduce (``parallel.xgmi``) to a GPU group: from
+    then on ``allreduce`` of bf16/f16 tensors up to ``max_elems`` goes through
+    it instead of RCCL.  Every rank of the group must call it.  Returns the
+    communicator (or None -- RCCL stays in use -- when IPC is unavailable)."""
+    g = _g(group_name)
+    if getattr(g, "xgmi", None) is not None:
+        return g.xgmi
+    from .xgmi import XgmiCommunicator
+
+    try:
+        g.xgmi = XgmiCommunicator.create(group_name, **kw)
+    except RuntimeError as e:  # no IPC / uncached memory on this platform: RCCL fallback
+        import warnings
+
+        warnings.warn(f"xgmi all-reduce unavailable, using RCCL: {e}")
+        g.xgmi = None
+    return g.xgmi
+
+
+def get_xgmi(group_name: str = "default"):
+    g = _groups.get(group_name)
+    return getattr(g, "xgmi", None) if g is not None else None
+
+
+def _xgmi_rows(n: int) -> int:
+    for d in (4096, 8192, 2048, 1024, 512, 256, 128, 64, 32, 16, 8):
+        if n % d == 0:
+            return d
+    return 0
+
+
 def allreduce(tensor: torch.Tensor, group_name: str = "default", op: ReduceOp = ReduceOp.SUM) -> torch.Tensor:
-    dist.all_reduce(tensor, op=_TORCH_OP[op], group=_g(group_name).pg)
+    g = _g(group_name)
+    xg = getattr(g, "xgmi", None)
+    if (xg is not None and op == ReduceOp.SUM and tensor.is_cuda and tensor.dtype == xg.dtype
+            and tensor.is_contiguous() and 0 < tensor.numel() <= xg.max_elems and _xgmi_rows(tensor.numel())):
+        d = _xgmi_rows(tensor.numel())
+        out = xg.all_reduce(tensor.view(-1, d))
+        tensor.view(-1, d).copy_(out)
+        return tensor
+    dist.all_reduce(tensor, op=_TORCH_OP[op], group=g.pg)
     return tensor
 
 

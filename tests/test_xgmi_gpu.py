@@ -1,0 +1,225 @@
+"""Custom xGMI all-reduce (ops/csrc/xgmi.hip, parallel/xgmi.py) on one MI355X.
+
+A one-GPU box has no xGMI peers, so the protocol is exercised two ways:
+  * several ranks inside ONE process, one HIP stream each (no IPC);
+  * two PROCESSES on the same GPU exchanging HIP IPC handles over gloo -- the
+    exact code path of a real TP group (IPC-mapped peer buffers), minus the link.
+Numerics: the all-reduced x must equal a plain fp32 sum in rank order rounded
+to bf16 (bit-exact: the kernel sums in the same fixed order on every rank);
+the fused RMSNorm is checked against a PyTorch fp32 RMSNorm of that x.
+"""
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+
+def _inputs(world, T, D, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    xs = [torch.randn(T, D, generator=g).to(torch.bfloat16) for _ in range(world)]
+    gamma = (1.0 + 0.1 * torch.randn(D, generator=g)).to(torch.bfloat16)
+    return xs, gamma
+
+
+def _reference(xs, gamma, eps):
+    acc = torch.zeros_like(xs[0], dtype=torch.float32)
+    for x in xs:
+        acc = acc + x.float()
+    s = acc.to(torch.bfloat16)
+    sf = s.float()
+    h = (sf * torch.rsqrt(sf.pow(2).mean(-1, keepdim=True) + eps) * gamma.float()).to(torch.bfloat16)
+    return s, h
+
+
+_STREAMS = []
+
+
+def _streams(n):
+    """Ranks in one process need truly concurrent streams: the box has 4 HW
+    queues per process (GPU_MAX_HW_QUEUES), so create 2 once and reuse them."""
+    while len(_STREAMS) < n:
+        _STREAMS.append(torch.cuda.Stream())
+    return _STREAMS[:n]
+
+
+@pytest.mark.parametrize("world", [2])
+@pytest.mark.parametrize("T,D,two_shot", [(4, 4096, False), (33, 1024, False), (256, 4096, True),
+                                          (37, 2048, True), (130, 768, True), (16, 8192, True)])
+def test_xgmi_local_group_matches_fp32_sum(world, T, D, two_shot):
+    from ray_dynamic_batching_amd.parallel.xgmi import XgmiCommunicator
+
+    eps = 1e-5
+    comms = XgmiCommunicator.local_group(world, max_elems=T * D, timeout_s=5.0)
+    streams = _streams(world)
+    try:
+        for it in range(4):  # several calls: epochs and receive-slot parity advance
+            xs, gamma = _inputs(world, T, D, seed=it)
+            ref_s, ref_h = _reference(xs, gamma, eps)
+            dx = [x.cuda() for x in xs]
+            dg = gamma.cuda()
+            torch.cuda.synchronize()
+            outs = []
+            for r in range(world):
+                with torch.cuda.stream(streams[r]):
+                    if it % 2 == 0:
+                        outs.append(comms[r].all_reduce_rmsnorm(dx[r], dg, eps, two_shot=two_shot))
+                    else:
+                        outs.append((comms[r].all_reduce(dx[r], two_shot=two_shot), None))
+            torch.cuda.synchronize()
+            for r in range(world):
+                assert comms[r].error() == 0, f"rank {r}: barrier timeout"
+                s, h = outs[r]
+                assert torch.equal(s.cpu(), ref_s), f"rank {r} it {it}: sum mismatch"
+                if h is not None:
+                    torch.testing.assert_close(h.cpu().float(), ref_h.float(), atol=2e-2, rtol=2e-2)
+    finally:
+        for c in comms:
+            c.close()
+
+
+def test_xgmi_local_group_graph_replay():
+    """The kernel keeps its epochs in device memory, so a captured call
+    replays correctly (what the TP replica's per-bucket hipGraphs rely on)."""
+    from ray_dynamic_batching_amd.parallel.xgmi import XgmiCommunicator
+
+    world, T, D, eps = 2, 64, 4096, 1e-5
+    comms = XgmiCommunicator.local_group(world, max_elems=T * D, timeout_s=5.0)
+    streams = _streams(world)
+    xs, gamma = _inputs(world, T, D)
+    dx = [x.cuda() for x in xs]
+    dg = gamma.cuda()
+    outs, graphs = [None] * world, []
+    try:
+        for r in range(world):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.stream(streams[r]):
+                with torch.cuda.graph(g, stream=streams[r]):
+                    outs[r] = comms[r].all_reduce_rmsnorm(dx[r], dg, eps)
+            graphs.append(g)
+        torch.cuda.synchronize()
+        for it in range(5):
+            xs, _ = _inputs(world, T, D, seed=100 + it)
+            for r in range(world):
+                dx[r].copy_(xs[r].cuda())
+            torch.cuda.synchronize()
+            for r in range(world):
+                with torch.cuda.stream(streams[r]):
+                    graphs[r].replay()
+            torch.cuda.synchronize()
+            ref_s, ref_h = _reference(xs, gamma, eps)
+            for r in range(world):
+                assert comms[r].error() == 0
+                assert torch.equal(outs[r][0].cpu(), ref_s)
+                torch.testing.assert_close(outs[r][1].cpu().float(), ref_h.float(), atol=2e-2, rtol=2e-2)
+    finally:
+        del graphs
+        for c in comms:
+            c.close()
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _ipc_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch
+
+    from ray_dynamic_batching_amd.parallel import collective as col
+
+    torch.cuda.set_device(0)
+    col.init_collective_group(world, rank, backend="gloo", group_name="tp")
+    try:
+        xg = col.enable_xgmi("tp", max_elems=1 << 20, timeout_s=10.0)
+        res = []
+        for T, D in [(8, 4096), (512, 2048)]:      # one-shot, two-shot
+            xs, gamma = _inputs(world, T, D, seed=T)
+            s, h = xg.all_reduce_rmsnorm(xs[rank].cuda(), gamma.cuda(), 1e-5)
+            torch.cuda.synchronize()
+            ref_s, ref_h = _reference(xs, gamma, 1e-5)
+            res.append((xg.error(), torch.equal(s.cpu(), ref_s),
+                        float((h.cpu().float() - ref_h.float()).abs().max())))
+        # the generic collective.allreduce entry point routes bf16 through xgmi
+        t = torch.full((4096,), float(rank + 1), dtype=torch.bfloat16, device="cuda")
+        col.allreduce(t, "tp")
+        torch.cuda.synchronize()
+        res.append((xg.error(), bool((t.cpu() == sum(range(1, world + 1))).all()), 0.0))
+        q.put((rank, res))
+    finally:
+        col.barrier("tp")
+        col.destroy_collective_group("tp")
+
+
+def test_xgmi_two_processes_ipc_one_gpu():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=_ipc_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    try:
+        got = dict(q.get(timeout=100) for _ in range(2))
+    finally:
+        for p in ps:
+            p.join(30)
+            if p.is_alive():
+                p.kill()
+    for r in range(2):
+        for err, exact, herr in got[r]:
+            assert err == 0 and exact and herr < 3e-2, got
+
+
+def _llama_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch
+
+    from ray_dynamic_batching_amd.models.llama import LlamaConfig, LlamaTP
+    from ray_dynamic_batching_amd.parallel import collective as col
+
+    torch.cuda.set_device(0)
+    if world > 1:
+        col.init_collective_group(world, rank, backend="gloo", group_name="tp")
+        col.enable_xgmi("tp", max_elems=1 << 20, timeout_s=10.0)
+    try:
+        cfg = LlamaConfig.tiny()
+        m = LlamaTP(cfg, rank, world, group_name="tp", device="cuda", backend="hip", init="full")
+        ids = m.example_input(2, seed=3)
+        x = m.hidden_states(ids).float().cpu()
+        q.put((rank, x[:, :64].tolist()))   # plain lists: tensors over an mp queue need the sender alive
+    finally:
+        if world > 1:
+            col.barrier("tp")
+            col.destroy_collective_group("tp")
+
+
+def test_llama_tp2_xgmi_matches_tp1():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_llama_worker, args=(0, 1, _port(), q))
+    p.start()
+    _, ref = q.get(timeout=100)
+    ref = torch.tensor(ref)
+    p.join(30)
+    port = _port()
+    ps = [ctx.Process(target=_llama_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    try:
+        got = {r: torch.tensor(v) for r, v in (q.get(timeout=100) for _ in range(2))}
+    finally:
+        for p in ps:
+            p.join(30)
+            if p.is_alive():
+                p.kill()
+    assert torch.equal(got[0], got[1])           # every TP rank holds the same x
+    err = (got[0] - ref).abs().max().item()
+    scale = ref.abs().max().item()
+    assert err <= 0.05 * scale + 0.05, (err, scale)
