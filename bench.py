@@ -47,6 +47,9 @@ def parse():
     ap.add_argument("--pipeline-depth", type=int, default=4)
     ap.add_argument("--compute-streams", type=int, default=2, help="batches executing concurrently per GPU")
     ap.add_argument("--layers", type=int, default=12)
+    ap.add_argument("--tune-streams", type=int, default=0,
+                    help="GEMM tile autotuning objective: throughput with this many concurrent streams "
+                         "(0 = --compute-streams)")
     ap.add_argument("--json-out", default="")
     ap.add_argument("--trace-out", default="", help="write a Chrome trace of the replicas' batches")
     return ap.parse_args()
@@ -111,6 +114,7 @@ def main():
     job.configure_queue(rank, rank, 0, args.concurrency * 2, 0.0, True)
 
     cfg = BertConfig(seq_len=args.seq, layers=args.layers)
+    os.environ.setdefault("RDB_TUNE_STREAMS", str(args.tune_streams or args.compute_streams))
     if echo:
         runner = _EchoRunner(rjob.EchoServer(job, rank, [rank], args.max_batch, args.echo_service_us, 0.0, 8))
     else:

@@ -34,6 +34,8 @@ def main(argv=None):
     ap.add_argument("--requests", type=int, default=400)
     ap.add_argument("--concurrency", type=int, default=16)
     ap.add_argument("--json-out", default="")
+    ap.add_argument("--allreduce", default="xgmi", choices=["xgmi", "rccl"],
+                    help="TP all-reduce: custom push-based xGMI kernel (fused RMSNorm) or RCCL")
     a = ap.parse_args(argv)
 
     import torch
@@ -48,6 +50,9 @@ def main(argv=None):
     torch.cuda.set_device(local)
     if world > 1:
         col.init_collective_group(world, rank, "nccl", "tp")
+        if a.allreduce == "xgmi":
+            # 8 prompts x seq tokens x hidden bf16 per all-reduce
+            col.enable_xgmi("tp", max_elems=8 * a.seq * 4096)
     cfg = LlamaConfig.llama3_8b(seq_len=a.seq, layers=a.layers)
     t0 = time.time()
     m = LlamaTP(cfg, rank, world, "tp" if world > 1 else None, device=f"cuda:{local}", init="shard")
@@ -98,7 +103,7 @@ def main(argv=None):
                             tokens_per_s=round(tokens / p50 * 1e3, 1), tflops_whole_node=round(flops / p50 / 1e9, 1),
                             next_token=int(out[0, 0].item())))
     if rank == 0:
-        rep = dict(metric="Llama-3-8B bf16 TP prefill latency", tp=world, seq_len=a.seq, layers=a.layers,
+        rep = dict(metric="Llama-3-8B bf16 TP prefill latency", tp=world, allreduce=a.allreduce if world > 1 else "none", seq_len=a.seq, layers=a.layers,
                    graph=not a.no_graph, init_s=round(init_s, 1), results=results,
                    data="synthetic token ids, random-init weights")
         print(json.dumps(rep), flush=True)
@@ -153,7 +158,7 @@ def _serve(a, m, world, rank):
         rep.step(0.01)
     rep.stop_all()
     lat = res["latency"]
-    rep_out = dict(metric="Llama-3-8B bf16 TP prefill serving (<= 8 prompts / batch)", tp=world, seq_len=a.seq,
+    rep_out = dict(metric="Llama-3-8B bf16 TP prefill serving (<= 8 prompts / batch)", tp=world, allreduce=a.allreduce if world > 1 else "none", seq_len=a.seq,
                    layers=a.layers, prompts_per_s=round(res["ok"] / res["elapsed_s"], 1),
                    p50_ms=round(lat["p50_ms"], 3), p99_ms=round(lat["p99_ms"], 3), ok=res["ok"],
                    mean_batch=round(job.replica_stats(0)["batch_items"] / max(1, job.replica_stats(0)["batches"]), 2),

@@ -125,7 +125,7 @@ class BertForSequenceClassification:
         c = self.cfg
         B, S = ids.shape
         D, H = c.hidden, c.heads
-        lens = (ids != c.pad_token_id).sum(dim=1, dtype=torch.int32).clamp_(min=1)
+        lens = ops.seq_lens(ids, c.pad_token_id)
         h = ops.embed_ln(ids, self.word, self.pos, self.typ, self.emb_g, self.emb_b, c.eps)
         n = len(self.layers)
         for i, L in enumerate(self.layers):

@@ -52,6 +52,8 @@ def _aligned(t: torch.Tensor, n: int = 16) -> bool:
 # on-device heuristic if the shape was never seen eagerly).
 # ---------------------------------------------------------------------------
 NUM_TILE_CFGS = 13
+FORCE_TILED = 99      # tile_cfg value that bypasses the skinny-M GEMM (M <= 64)
+SKINNY_MAX_M = 64
 _TUNE: Dict[tuple, int] = {}
 
 
@@ -71,11 +73,25 @@ def _tuned_cfg(key: tuple, launch: Callable[[int], None], candidates=range(NUM_T
         return -1
     best_t, best_c = float("inf"), -1
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    # RDB_TUNE_STREAMS=n (n > 1): rank tiles by THROUGHPUT with n launches in
+    # flight on n streams -- what a replica running n concurrent batches sees --
+    # instead of the isolated latency, which favours small tiles that fill the
+    # CUs alone but cost more LDS/VMEM traffic per FLOP when streams overlap.
+    ns = max(1, int(os.environ.get("RDB_TUNE_STREAMS", "1")))
+    side = [torch.cuda.Stream() for _ in range(ns - 1)]
+    cur = torch.cuda.current_stream()
     for c in candidates:
         launch(c)
         s.record()
+        for sd in side:
+            sd.wait_stream(cur)
         for _ in range(4):
             launch(c)
+            for sd in side:
+                with torch.cuda.stream(sd):
+                    launch(c)
+        for sd in side:
+            cur.wait_stream(sd)
         e.record()
         e.synchronize()
         t = s.elapsed_time(e)
@@ -118,17 +134,19 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
         _check(bias.is_contiguous() and bias.numel() == N and bias.dtype == x.dtype, "linear: bad bias")
     ldr = 0
     if residual is not None:
-        if residual.dim() == 2 and residual.stride(1) == 1 and residual.shape[0] == M:
-            ldr = residual.stride(0)          # 2-D row-strided view (e.g. the CLS rows)
-        else:
-            _check(residual.is_contiguous() and residual.numel() == M * n_out, "linear: bad residual")
+        if residual.is_contiguous():
+            _check(residual.numel() == M * n_out, "linear: bad residual")
             ldr = n_out
-        _check(residual.dtype == x.dtype and residual.shape[-1] == n_out and ldr % 4 == 0
-               and _aligned(residual, 8), "linear: bad residual")
+        else:
+            _check(residual.dim() == 2 and residual.stride(1) == 1 and residual.shape[0] == M
+                   and residual.stride(0) % 4 == 0 and _aligned(residual, 8), "linear: bad strided residual")
+            ldr = residual.stride(0)          # 2-D row-strided view (e.g. the CLS rows)
+        _check(residual.dtype == x.dtype and residual.shape[-1] == n_out, "linear: bad residual")
     args = (DTYPE_CODE[x.dtype], DTYPE_CODE[od], x2.data_ptr(), lda, w.data_ptr(), K, out.data_ptr(),
             n_out, _ptr(bias), _ptr(residual), ldr, M, N, K, float(alpha), ACT_CODE[act])
     fn = _ops().gemm_tn
-    if tile_cfg < 0 and od != torch.float32:
+    skinny = M <= SKINNY_MAX_M and K % 32 == 0 and act != "swiglu"   # C++ routes these to the skinny-M kernel
+    if tile_cfg < 0 and od != torch.float32 and not skinny:
         key = ("gemm", x.dtype, M, N, K, lda, act, bias is not None, residual is not None)
         tile_cfg = _tuned_cfg(key, lambda c: fn(*args, _stream(), c))
     fn(*args, _stream(), int(tile_cfg))
@@ -228,6 +246,19 @@ def embed_ln_ref(ids, word, pos, typ, gamma, beta, eps=1e-12, types=None):
     idl = ids.long().clamp(0, word.shape[0] - 1)
     x = word.float()[idl] + pos.float()[:S][None] + typ.float()[(types.long() if types is not None else torch.zeros_like(idl))]
     return F.layer_norm(x, (word.shape[1],), gamma.float(), beta.float(), eps).to(word.dtype).reshape(B * S, -1)
+
+
+def seq_lens(ids: torch.Tensor, pad_id: int = 0) -> torch.Tensor:
+    """int32 [B]: number of non-pad ids per row of ``ids`` [B, S] int32 (min 1)."""
+    _check(ids.is_cuda and ids.dtype == torch.int32 and ids.dim() == 2 and ids.is_contiguous(), "seq_lens: ids")
+    B, S = ids.shape
+    lens = torch.empty(B, device=ids.device, dtype=torch.int32)
+    _ops().seq_lens(ids.data_ptr(), B, S, int(pad_id), lens.data_ptr(), _stream())
+    return lens
+
+
+def seq_lens_ref(ids, pad_id=0):
+    return (ids != pad_id).sum(dim=1, dtype=torch.int32).clamp_(min=1)
 
 
 # ---------------------------------------------------------------------------

@@ -39,6 +39,7 @@ void shuffle_remap(uintptr_t A, int ldA, uintptr_t B, int ldB, int Ch, long pixe
                    uintptr_t O2, int ld2, int split, uintptr_t stream);
 void se_scale(uintptr_t x, uintptr_t s, uintptr_t y, int N, long HW, int C, uintptr_t stream);
 void register_engine(py::module_& m);
+void seq_lens(uintptr_t ids, int B, int S, int pad, uintptr_t lens, uintptr_t stream);
 size_t xgmi_signal_bytes();
 void xgmi_allreduce(int dtype, const std::vector<uintptr_t>& recv, const std::vector<uintptr_t>& gather,
                     const std::vector<uintptr_t>& sig, int rank, uintptr_t in, uintptr_t out_norm,
@@ -73,6 +74,7 @@ PYBIND11_MODULE(_rdb_ops, m) {
   m.def("dwconv_nhwc", &rdb::dwconv_nhwc, py::call_guard<py::gil_scoped_release>());
   m.def("shuffle_remap", &rdb::shuffle_remap, py::call_guard<py::gil_scoped_release>());
   m.def("se_scale", &rdb::se_scale, py::call_guard<py::gil_scoped_release>());
+  m.def("seq_lens", &rdb::seq_lens, py::call_guard<py::gil_scoped_release>());
 
   // Pinning of shared-memory regions so the device can read request payloads
   // in place (zero-copy H2D gather) -- the "pinned shm tensor arena".

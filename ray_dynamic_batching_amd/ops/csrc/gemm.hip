@@ -16,6 +16,11 @@ void gemm_tn_bf16(const DenseParams& p, uintptr_t W, int ldw, uintptr_t C, int l
 void gemm_tn_f16(const DenseParams& p, uintptr_t W, int ldw, uintptr_t C, int ldc, uintptr_t bias, uintptr_t R,
                  int ldr, int M, int N, int K, float alpha, int act, hipStream_t s, int cfg, int out_dtype);
 
+bool skinny_gemm_ok(int M, int N, int K, int lda, int ldw, int act, uintptr_t A, uintptr_t W);
+void skinny_gemm(int in_dtype, int out_dtype, uintptr_t A, int lda, uintptr_t W, int ldw, uintptr_t C, int ldc,
+                 uintptr_t bias, uintptr_t R, int ldr, int M, int N, int K, float alpha, int act, hipStream_t s);
+constexpr int kForceTiled = 99;  // force_cfg value that bypasses the skinny-M kernel (tests)
+
 // dtype codes shared with the Python side: 0 = bf16, 1 = f16, 2 = f32
 void gemm_tn(int in_dtype, int out_dtype, uintptr_t A, int lda, uintptr_t W, int ldw, uintptr_t C,
              int ldc, uintptr_t bias, uintptr_t R, int ldr, int M, int N, int K, float alpha,
@@ -26,6 +31,12 @@ void gemm_tn(int in_dtype, int out_dtype, uintptr_t A, int lda, uintptr_t W, int
   if (act == ACT_SWIGLU && N % 4 != 0) throw std::invalid_argument("gemm_tn: SWIGLU needs N % 4 == 0");
   if (M <= 0 || N <= 0 || K <= 0) return;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (force_cfg != kForceTiled && skinny_gemm_ok(M, N, K, lda, ldw, act, A, W)) {
+    skinny_gemm(in_dtype, out_dtype, A, lda, W, ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act, s);
+    RDB_HIP_CHECK(hipGetLastError());
+    return;
+  }
+  if (force_cfg == kForceTiled) force_cfg = -1;
   DenseParams p{reinterpret_cast<const void*>(A), lda, M, K};
   if (in_dtype == 0) {
     gemm_tn_bf16(p, W, ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act, s, force_cfg, out_dtype);

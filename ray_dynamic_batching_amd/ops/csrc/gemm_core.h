@@ -73,8 +73,14 @@ __device__ __forceinline__ float act_rt(int act, float x) {
 
 // ---- buffer-resource helpers (T8): out-of-range loads return 0 with no branch ----
 constexpr uint32_t kOOB = 0x80000000u;  // voffset sentinel beyond every num_records
+// The descriptor inputs are readfirstlane'd so hipcc can PROVE the SRD wave-
+// uniform; otherwise it wraps every buffer op in a waterfall loop (guide T20).
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p, uint32_t bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+  const uint64_t a = reinterpret_cast<uint64_t>(p);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  void* base = reinterpret_cast<void*>(((uint64_t)hi << 32) | lo);
+  return __builtin_amdgcn_make_buffer_rsrc(base, (short)0, (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
 }
 __device__ __forceinline__ u32x4 bload16(__amdgpu_buffer_rsrc_t r, uint32_t off) {
   return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
@@ -192,9 +198,12 @@ mfma_gemm_kernel(typename LoaderT<T, BM * 8 / 256>::Params ap, const T* __restri
   constexpr int W_CH = (BN + 31) / 32;  // rounded up: rows >= BN are LDS padding
   constexpr int BNP = W_CH * 32;
   constexpr int kStage = (BM + BNP) * BK * 2;  // bytes per LDS stage (A tile, then W tile)
+  // Three LDS stages (two K-tiles in flight across each barrier) whenever they
+  // still fit two blocks per CU; the big tiles keep two stages.
+  constexpr int kStages = (3 * kStage <= 80 * 1024) ? 3 : 2;
   typedef typename MfmaOp<T>::frag frag;
 
-  __shared__ __attribute__((aligned(16))) char smem[2 * kStage];
+  __shared__ __attribute__((aligned(16))) char smem[kStages * kStage];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -265,15 +274,43 @@ mfma_gemm_kernel(typename LoaderT<T, BM * 8 / 256>::Params ap, const T* __restri
     }
   };
 
-  // Two LDS stages: the DMA of tile k+1 runs under the MFMAs of tile k; the
-  // __syncthreads() at the end of a step waits the issuing waves' DMA
-  // (vmcnt(0)) and orders every wave's reads before the buffer is refilled.
   const int nk = (K + BK - 1) / BK;
-  stage(0, 0);
-  __syncthreads();
-  for (int kt = 0; kt < nk; ++kt) {
-    if (kt + 1 < nk) stage((kt + 1) & 1, (kt + 1) * BK);
-    compute(kt & 1);
+  if constexpr (kStages == 2) {
+    // Two LDS stages: the DMA of tile k+1 runs under the MFMAs of tile k; the
+    // __syncthreads() at the end of a step waits the issuing waves' DMA
+    // (vmcnt(0)) and orders every wave's reads before the buffer is refilled.
+    stage(0, 0);
+    __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+      if (kt + 1 < nk) stage((kt + 1) & 1, (kt + 1) * BK);
+      compute(kt & 1);
+      __syncthreads();
+    }
+  } else {
+    // Three LDS stages (guide §5 "Pipelining across barriers"): tiles k+1 and
+    // k+2 stay in flight while tile k is consumed.  Each wave retires ITS OWN
+    // DMA of tile k with a counted vmcnt (leaving tile k+1's kLoads pending),
+    // then a RAW s_barrier (no __syncthreads: its fence would drain vmcnt to 0)
+    // makes every wave's pieces of tile k visible.  Buffer (k+2)%3 was last
+    // read by compute(k-1), which every wave finished before this barrier, so
+    // it is refilled right after it (WAR-safe).
+    constexpr int kLoads = A_CH + W_CH;                  // DMA instructions per wave per stage
+    constexpr int kWaitOne = (kLoads & 15) | ((kLoads >> 4) << 14) | 0x70 | 0xF00;  // vmcnt(kLoads)
+    constexpr int kWaitAll = 0x70 | 0xF00;                                             // vmcnt(0)
+    static_assert(kLoads < 64, "vmcnt field is 6 bits");
+    stage(0, 0);
+    if (nk > 1) stage(1, BK);
+    int buf = 0;
+    for (int kt = 0; kt < nk; ++kt) {
+      if (kt + 1 < nk) __builtin_amdgcn_s_waitcnt(kWaitOne);
+      else __builtin_amdgcn_s_waitcnt(kWaitAll);
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      if (kt + 2 < nk) stage(buf == 0 ? 2 : buf - 1, (kt + 2) * BK);
+      compute(buf);
+      buf = buf == 2 ? 0 : buf + 1;
+    }
     __syncthreads();
   }
 

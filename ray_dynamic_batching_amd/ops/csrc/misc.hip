@@ -157,4 +157,21 @@ void image_to_nhwc(uintptr_t src, int N, int HW, int Cp, uintptr_t dst, uintptr_
   RDB_HIP_CHECK(hipGetLastError());
 }
 
+// Per-sequence valid length = number of non-pad token ids (BERT key-padding
+// mask for the attention kernel): one wave per sequence, one launch.
+__global__ void __launch_bounds__(64) seq_lens_kernel(const int* __restrict__ ids, int S, int pad, int* __restrict__ lens) {
+  const int b = blockIdx.x;
+  int c = 0;
+  for (int t = threadIdx.x; t < S; t += 64) c += ids[(size_t)b * S + t] != pad;
+  const float tot = wave_sum((float)c);
+  if (threadIdx.x == 0) lens[b] = max(1, (int)tot);
+}
+
+void seq_lens(uintptr_t ids, int B, int S, int pad, uintptr_t lens, uintptr_t stream) {
+  if (B <= 0) return;
+  hipLaunchKernelGGL(seq_lens_kernel, dim3(B), dim3(64), 0, reinterpret_cast<hipStream_t>(stream),
+                     reinterpret_cast<const int*>(ids), S, pad, reinterpret_cast<int*>(lens));
+  RDB_HIP_CHECK(hipGetLastError());
+}
+
 }  // namespace rdb

@@ -271,3 +271,41 @@ def test_norms_non_multiple_of_256(D):
     assert torch.allclose(y.float(), ref.float(), atol=3e-2, rtol=3e-2)
     y2 = ops.rms_norm(x, g, 1e-5)
     assert torch.allclose(y2.float(), ops.rms_norm_ref(x, g, 1e-5).float(), atol=3e-2, rtol=3e-2)
+
+
+@pytest.mark.parametrize("M,N,K", [(1, 1000, 2048), (8, 2304, 768), (32, 768, 3072), (32, 2, 768),
+                                   (33, 3072, 768), (64, 130, 96), (17, 4008, 4096)])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_skinny_gemm_matches_fp32(M, N, K, dtype):
+    """M <= 64 runs the weight-streaming skinny kernel (gemm_skinny.hip)."""
+    ops = _ops()
+    torch.manual_seed(M * 7 + N)
+    x = torch.randn(M, K, device="cuda", dtype=dtype)
+    w = torch.randn(N, K, device="cuda", dtype=dtype) * (K ** -0.5)
+    b = torch.randn(N, device="cuda", dtype=dtype)
+    r = torch.randn(M, N, device="cuda", dtype=dtype)
+    _close(ops.linear(x, w), ops.linear_ref(x, w), 2e-2, 2e-2)
+    _close(ops.linear(x, w, b, act="gelu", residual=r), ops.linear_ref(x, w, b, act="gelu", residual=r), 3e-2, 2e-2)
+    y = ops.linear(x, w, b, act="tanh", out_dtype=torch.float32)
+    _close(y, ops.linear_ref(x, w, b, act="tanh", out_dtype=torch.float32), 1e-2, 1e-2)
+    # identical to the tiled kernel up to accumulation order
+    _close(ops.linear(x, w, b), ops.linear(x, w, b, tile_cfg=ops.FORCE_TILED), 2e-2, 2e-2)
+
+
+def test_skinny_gemm_strided_rows_and_residual():
+    """BERT's CLS-only last layer: A and the residual are row-strided views."""
+    ops = _ops()
+    h = torch.randn(8, 128, 768, device="cuda", dtype=torch.bfloat16)
+    w = torch.randn(768, 768, device="cuda", dtype=torch.bfloat16) * 0.03
+    cls = h[:, 0, :]
+    y = ops.linear(cls, w, residual=cls)
+    _close(y, ops.linear_ref(cls.contiguous(), w, residual=cls.contiguous()), 2e-2, 2e-2)
+
+
+def test_seq_lens():
+    ops = _ops()
+    ids = torch.randint(1, 100, (37, 128), device="cuda", dtype=torch.int32)
+    ids[3, 50:] = 0
+    ids[5, :] = 0
+    ids[7, 1:] = 0
+    assert torch.equal(ops.seq_lens(ids), ops.seq_lens_ref(ids))
