@@ -51,7 +51,8 @@ def _aligned(t: torch.Tensor, n: int = 16) -> bool:
 # while a hipGraph is being captured (those calls use the cached choice, or the
 # on-device heuristic if the shape was never seen eagerly).
 # ---------------------------------------------------------------------------
-NUM_TILE_CFGS = 13
+NUM_TILE_CFGS = 19   # gemm_core.h kTileBM/BN: 0..12 4-wave (GEMM and conv), 13..18 8-wave (GEMM only)
+NUM_CONV_TILE_CFGS = 13
 FORCE_TILED = 99      # tile_cfg value that bypasses the skinny-M GEMM (M <= 64)
 SKINNY_MAX_M = 64
 _TUNE: Dict[tuple, int] = {}
@@ -414,7 +415,7 @@ def conv2d_nhwc(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] =
     fn = _ops().conv2d_nhwc
     if tile_cfg < 0:
         key = ("conv", N, H, W, C, K, R, S, stride, pad, act, bias is not None, residual is not None)
-        tile_cfg = _tuned_cfg(key, lambda c: fn(*args, _stream(), c))
+        tile_cfg = _tuned_cfg(key, lambda c: fn(*args, _stream(), c), range(NUM_CONV_TILE_CFGS))
     fn(*args, _stream(), int(tile_cfg))
     return out
 

@@ -183,24 +183,31 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, char* lds, uint3
 // pieces, rows past BN are zero-filled into LDS padding and never read --
 // this is what allows quantisation-exact tiles such as 128x144 (N = 2304 in
 // 16 column blocks, 512 tiles at M = 4096 = 2 per CU exactly).
+//
+// NW = 8 waves (512 threads, one block per CU) runs the big tiles (256x128,
+// 256x192, ...): twice the MFMA work per staged byte of a 4-wave 128-row tile,
+// which is what the L2-bandwidth-bound BERT shapes need (FFN2 at 128x48 moves
+// ~14 TB/s through L2 for 0.5 PF).
 template <typename T, typename OutT, int BM, int BN, template <typename, int> class LoaderT, bool HAS_BIAS,
-          bool HAS_RES, int WGM = 2>
-__global__ void __launch_bounds__(256, 2)
-mfma_gemm_kernel(typename LoaderT<T, BM * 8 / 256>::Params ap, const T* __restrict__ W, int ldw,
+          bool HAS_RES, int WGM = 2, int NW = 4>
+__global__ void __launch_bounds__(64 * NW, NW == 4 ? 2 : 1)
+mfma_gemm_kernel(typename LoaderT<T, 1>::Params ap, const T* __restrict__ W, int ldw,
                  OutT* __restrict__ C, int ldc, const T* __restrict__ bias,
                  const T* __restrict__ R, int ldr, int M, int N, int K, float alpha, int act) {
   constexpr int BK = 64;
-  constexpr int WGN = 4 / WGM;
+  constexpr int WGN = NW / WGM;
+  constexpr int NT = 64 * NW;                 // threads
   constexpr int WM = BM / WGM, WN = BN / WGN;
   constexpr int TM = WM / 16, TN = WN / 16;
   static_assert(WM % 16 == 0 && WN % 16 == 0 && BM % 32 == 0, "tile / wave layout mismatch");
-  constexpr int A_CH = BM * 8 / 256;  // 16-B chunks per thread per A tile
-  constexpr int W_CH = (BN + 31) / 32;  // rounded up: rows >= BN are LDS padding
-  constexpr int BNP = W_CH * 32;
+  static_assert(WGM * WGN == NW && BM % (8 * NW) == 0, "wave layout / DMA split");
+  constexpr int A_CH = BM * 8 / NT;                  // 16-B chunks per thread per A tile
+  constexpr int W_CH = (BN + 8 * NW - 1) / (8 * NW);  // rounded up: rows >= BN are LDS padding
+  constexpr int BNP = W_CH * 8 * NW;
   constexpr int kStage = (BM + BNP) * BK * 2;  // bytes per LDS stage (A tile, then W tile)
   // Three LDS stages (two K-tiles in flight across each barrier) whenever they
   // still fit two blocks per CU; the big tiles keep two stages.
-  constexpr int kStages = (3 * kStage <= 80 * 1024) ? 3 : 2;
+  constexpr int kStages = (3 * kStage <= (NW == 4 ? 80 : 160) * 1024) ? 3 : 2;
   typedef typename MfmaOp<T>::frag frag;
 
   __shared__ __attribute__((aligned(16))) char smem[kStages * kStage];
@@ -431,21 +438,25 @@ mfma_gemm_kernel(typename LoaderT<T, BM * 8 / 256>::Params ap, const T* __restri
 // CUs x blocks/CU -- hence the non-power-of-two tiles: 128x192 (N = 3072),
 // 128x144 (N = 2304), 64x96 / 128x48 (N = 768) each give exactly 512 tiles
 // at M = 4096 (BERT-base, batch 32).
-constexpr int kNumTiles = 13;
-constexpr int kTileBM[kNumTiles] = {128, 64, 128, 64, 128, 192, 256, 128, 128, 64, 128, 256, 128};
-constexpr int kTileBN[kNumTiles] = {128, 128, 64, 64, 192, 128, 128, 256, 144, 96, 96, 144, 48};
-constexpr int kTileWGM[kNumTiles] = {2, 2, 2, 2, 2, 2, 2, 2, 4, 2, 2, 4, 4};
+constexpr int kNumTiles = 19;
+//                                 0    1    2    3    4    5    6    7    8    9   10   11   12 | 8-wave tiles: 13   14   15   16   17   18
+constexpr int kTileBM[kNumTiles] = {128, 64, 128, 64, 128, 192, 256, 128, 128, 64, 128, 256, 128, 256, 128, 256, 256, 128, 256};
+constexpr int kTileBN[kNumTiles] = {128, 128, 64, 64, 192, 128, 128, 256, 144, 96, 96, 144, 48, 128, 256, 192, 144, 96, 96};
+constexpr int kTileWGM[kNumTiles] = {2, 2, 2, 2, 2, 2, 2, 2, 4, 2, 2, 4, 4, 4, 2, 4, 8, 4, 8};
+constexpr int kTileNW[kNumTiles] = {4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 8, 8, 8, 8, 8, 8};
 
 inline int tile_blocks_per_cu(int cfg) {
-  const int bnp = (kTileBN[cfg] + 31) / 32 * 32;
+  const int q = 8 * kTileNW[cfg];
+  const int bnp = (kTileBN[cfg] + q - 1) / q * q;
   const int lds = 2 * (kTileBM[cfg] + bnp) * 64 * 2;
-  return std::min(2, 163840 / lds);
+  return std::min(8 / kTileNW[cfg], 163840 / lds);
 }
 // Heuristic: minimise (rounds of blocks over 256 CUs) x (tile work / tile efficiency).
-inline int pick_tile_cfg(int M, int N) {
+constexpr int kNumTiles4 = 13;  // tiles 0..12 are 4-wave (every loader); 13.. are 8-wave (dense only)
+inline int pick_tile_cfg(int M, int N, bool dense) {
   int best = 3;
   double best_t = 1e30;
-  for (int c = 0; c < kNumTiles; ++c) {
+  for (int c = 0; c < (dense ? kNumTiles : kNumTiles4); ++c) {
     const int bm = kTileBM[c], bn = kTileBN[c];
     const long tiles = (long)((M + bm - 1) / bm) * ((N + bn - 1) / bn);
     const long slots = 256L * tile_blocks_per_cu(c);
@@ -458,12 +469,12 @@ inline int pick_tile_cfg(int M, int N) {
 }
 
 template <typename T, typename OutT, template <typename, int> class LoaderT, bool HB, bool HR, int BM, int BN,
-          int WGM = 2, typename P>
+          int WGM = 2, int NW = 4, typename P>
 void launch_one(const P& ap, const T* W, int ldw, OutT* C, int ldc, const T* bias, const T* R, int ldr, int M,
                 int N, int K, float alpha, int act, hipStream_t s) {
   const int nwg = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
-  hipLaunchKernelGGL((mfma_gemm_kernel<T, OutT, BM, BN, LoaderT, HB, HR, WGM>), dim3(nwg), dim3(256), 0, s, ap, W,
-                     ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act);
+  hipLaunchKernelGGL((mfma_gemm_kernel<T, OutT, BM, BN, LoaderT, HB, HR, WGM, NW>), dim3(nwg), dim3(64 * NW), 0, s,
+                     ap, W, ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act);
 }
 
 template <typename T, typename OutT, template <typename, int> class LoaderT, bool HB, bool HR, typename P>
@@ -488,7 +499,19 @@ void launch_mfma_gemm_t(const P& ap, const T* W, int ldw, OutT* C, int ldc, cons
       RDB_TILE(10, 128, 96, 2)
       RDB_TILE(11, 256, 144, 4)
       RDB_TILE(12, 128, 48, 4)
-      default: launch_one<T, OutT, LoaderT, HB, HR, 64, 64>(ap, W, ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act, s);
+      default:
+        if constexpr (std::is_same<LoaderT<T, 1>, DenseLoader<T, 1>>::value) {
+          // 8-wave big tiles: dense operands only (keeps the conv build small)
+          switch (cfg) {
+            case 13: launch_one<T, OutT, LoaderT, HB, HR, 256, 128, 4, 8>(ap, W, ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act, s); return;
+            case 14: launch_one<T, OutT, LoaderT, HB, HR, 128, 256, 2, 8>(ap, W, ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act, s); return;
+            case 15: launch_one<T, OutT, LoaderT, HB, HR, 256, 192, 4, 8>(ap, W, ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act, s); return;
+            case 16: launch_one<T, OutT, LoaderT, HB, HR, 256, 144, 8, 8>(ap, W, ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act, s); return;
+            case 17: launch_one<T, OutT, LoaderT, HB, HR, 128, 96, 4, 8>(ap, W, ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act, s); return;
+            case 18: launch_one<T, OutT, LoaderT, HB, HR, 256, 96, 8, 8>(ap, W, ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act, s); return;
+            default: break;
+          }
+        } launch_one<T, OutT, LoaderT, HB, HR, 64, 64>(ap, W, ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act, s);
     }
   }
 #undef RDB_TILE
@@ -497,7 +520,8 @@ void launch_mfma_gemm_t(const P& ap, const T* W, int ldw, OutT* C, int ldc, cons
 template <typename T, typename OutT, template <typename, int> class LoaderT, typename P>
 void launch_mfma_gemm(const P& ap, const T* W, int ldw, OutT* C, int ldc, const T* bias, const T* R,
                       int ldr, int M, int N, int K, float alpha, int act, hipStream_t s, int cfg) {
-  if (cfg < 0 || cfg >= kNumTiles) cfg = pick_tile_cfg(M, N);
+  constexpr bool dense = std::is_same<LoaderT<T, 1>, DenseLoader<T, 1>>::value;
+  if (cfg < 0 || cfg >= (dense ? kNumTiles : kNumTiles4)) cfg = pick_tile_cfg(M, N, dense);
   if (bias && R)
     launch_mfma_gemm_t<T, OutT, LoaderT, true, true>(ap, W, ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act, s, cfg);
   else if (bias)

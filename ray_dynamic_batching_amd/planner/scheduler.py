@@ -202,10 +202,13 @@ class SLOScheduler:
                  compat: bool = False, slo_divisor: float = 1.0, drop_stale: bool = True,
                  gpu_mem_gb: Optional[float] = None, queue_capacity: int = 2048, job_name: Optional[str] = None,
                  executor: str = "python", devices: Optional[List[int]] = None,
-                 max_batch: Optional[Dict[str, int]] = None):
+                 max_batch: Optional[Dict[str, int]] = None, plan_path: Optional[str] = None):
         """``executor``: "python" (DutyCycleExecutor threads; CPU / arbitrary torch
         models) or "engine" (native GPU engines, one per entry of ``devices``;
-        ``max_batch`` = largest batch captured per model)."""
+        ``max_batch`` = largest batch captured per model).  ``plan_path``: every
+        applied plan is checkpointed there, and a plan found there at start-up
+        is restored (resume after a restart)."""
+        self.plan_path = plan_path
         self.profiles = profiles
         self.slos = dict(slos_ms)
         self.model_factories = model_factories
@@ -248,6 +251,10 @@ class SLOScheduler:
         self._monitor: Optional[threading.Thread] = None
         self._stop = threading.Event()
         self.lock = threading.Lock()
+        if plan_path:
+            saved = self.load_plan(plan_path)
+            if saved and self.restore_plan(saved):
+                logger.info("restored the last plan from %s", plan_path)
 
     # --------------------------------------------------------------- ids
     def model_id(self, m: str) -> int:
@@ -357,6 +364,12 @@ class SLOScheduler:
         return False
 
     def replan(self, update: Dict[str, float]) -> Plan:
+        plan = self._replan_locked(update)
+        if self.plan_path:
+            self.save_plan(self.plan_path)       # checkpoint every applied plan
+        return plan
+
+    def _replan_locked(self, update: Dict[str, float]) -> Plan:
         with self.lock:
             sessions = []
             for m, s in self.sessions.items():
@@ -403,6 +416,88 @@ class SLOScheduler:
         # requests parked on queues that are no longer active stay there until a
         # plan re-activates them; move them forward by re-submitting is unnecessary
         # because every model keeps at least one active queue while its rate > 0.
+
+    # ---------------------------------------------------- checkpoint/resume
+    # the reference keeps its plan only in memory (scheduler.py:
+    # 894-897); here the last applied plan is a JSON document that the node
+    # agent's persistent KV (or a file) holds, and a restarted scheduler
+    # re-applies it before the first rate sample arrives.
+    def plan_state(self) -> Dict[str, Any]:
+        with self.lock:
+            def sess(s: Session) -> Dict[str, Any]:
+                return dict(model=s.model_name, slo_ms=s.latency_slo, rate=s.request_rate, batch=s.batch_size)
+
+            return dict(version=1, models=list(self.models), num_gpus=self.num_gpus,
+                        sessions={m: sess(s) for m, s in self.sessions.items()},
+                        slots=[None if n is None else dict(duty_cycle=n.duty_cycle, gpu_type=n.gpu_type,
+                                                           gpu_mem=n.gpu_mem,
+                                                           sessions=[dict(sess(s), occupancy=o) for s, o in n.sessions])
+                               for n in self.slots])
+
+    def save_plan(self, path: Optional[str] = None, agent_socket: Optional[str] = None,
+                  key: str = "planner/last_plan") -> str:
+        import json
+
+        blob = json.dumps(self.plan_state())
+        if path:
+            import os
+
+            tmp = path + ".tmp"
+            with open(tmp, "w") as f:
+                f.write(blob)
+            os.replace(tmp, path)
+        if agent_socket:
+            from ..runtime import agent as ragent
+
+            ragent.request(agent_socket, f"KV_PUT {key} {blob}")
+        return blob
+
+    def restore_plan(self, state: Any) -> bool:
+        """Re-apply a plan from ``plan_state()`` (dict or JSON text).  Returns False
+        when it does not fit this scheduler (different models or GPU count)."""
+        import json
+
+        if isinstance(state, (str, bytes)):
+            state = json.loads(state)
+        if not state or state.get("version") != 1 or state.get("num_gpus") != self.num_gpus:
+            return False
+        if any(m not in self.slos for m in state["sessions"]):
+            return False
+
+        def mk(d: Dict[str, Any]) -> Session:
+            return Session(d["model"], float(d["slo_ms"]), float(d["rate"]), int(d["batch"]))
+
+        slots: List[Optional[Node]] = []
+        for n in state["slots"]:
+            if n is None:
+                slots.append(None)
+                continue
+            slots.append(Node([(mk(s), float(s["occupancy"])) for s in n["sessions"]], float(n["duty_cycle"]),
+                              n.get("gpu_type", "MI355X"), float(n.get("gpu_mem", 288.0))))
+        with self.lock:
+            self.sessions = {m: mk(d) for m, d in state["sessions"].items()}
+            self.slots = slots
+            self._apply(slots)
+            self._flush_backlog()
+            self.changes.append(ScheduleChange(time.time(), {"restored": 1.0},
+                                               [n.as_tuples() if n else [] for n in slots], 0))
+        return True
+
+    @staticmethod
+    def load_plan(path: Optional[str] = None, agent_socket: Optional[str] = None,
+                  key: str = "planner/last_plan") -> Optional[str]:
+        if path:
+            try:
+                with open(path) as f:
+                    return f.read()
+            except FileNotFoundError:
+                return None
+        if agent_socket:
+            from ..runtime import agent as ragent
+
+            r = ragent.request(agent_socket, f"KV_GET {key}")
+            return r[3:] if r.startswith("OK ") else None
+        return None
 
     # ------------------------------------------------------------- metrics
     def get_stats(self) -> Dict[str, Dict[str, Any]]:

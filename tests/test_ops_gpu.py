@@ -31,7 +31,7 @@ def test_linear_plain(M, N, K, dtype):
     _close(y, ops.linear_ref(x, w), 2e-2, 2e-2)
 
 
-@pytest.mark.parametrize("cfg", list(range(8)))
+@pytest.mark.parametrize("cfg", list(range(19)))
 def test_linear_tile_configs_asymmetric(cfg):
     """A = I with an asymmetric W catches a transposed C-write (guide §3)."""
     ops = _ops()
@@ -200,7 +200,7 @@ def test_image_to_nhwc_and_gather():
     assert torch.equal(dst.cpu(), exp)
 
 
-@pytest.mark.parametrize("cfg", list(range(8)))
+@pytest.mark.parametrize("cfg", list(range(19)))
 def test_linear_all_tiles_random(cfg):
     ops = _ops()
     torch.manual_seed(11)
@@ -212,7 +212,7 @@ def test_linear_all_tiles_random(cfg):
            ops.linear_ref(x, w, b, act="gelu", residual=r), 3e-2, 2e-2)
 
 
-@pytest.mark.parametrize("cfg", list(range(8)))
+@pytest.mark.parametrize("cfg", list(range(13)))
 def test_conv_all_tiles(cfg):
     ops = _ops()
     torch.manual_seed(12)

@@ -62,6 +62,39 @@ def test_replan_on_rate_change_and_thresholds():
         s.shutdown()
 
 
+def test_plan_checkpoint_and_resume(tmp_path):
+    """every applied plan is checkpointed; a restarted scheduler
+    resumes it (same placement) before any rate sample arrives."""
+    path = str(tmp_path / "plan.json")
+    s = make_sched(plan_path=path)
+    try:
+        s.check_and_update({"a": 100.0, "b": 50.0})
+        before = [n.as_tuples() if n else [] for n in s.slots]
+        assert (tmp_path / "plan.json").exists()
+    finally:
+        s.shutdown()
+    s2 = make_sched(plan_path=path)
+    try:
+        assert [n.as_tuples() if n else [] for n in s2.slots] == before
+        assert s2.changes and s2.changes[-1].reason == {"restored": 1.0}
+        assert set(s2.sessions) == {"a", "b"}
+        # the restored plan serves: requests routed to the placed queues complete
+        x = np.random.rand(32).astype(np.float32)
+        rid = s2.submit("a", x)
+        got = {}
+        deadline = time.time() + 10
+        while rid not in got and time.time() < deadline:
+            for c in s2.poll(64, 0.1):
+                got[c[0]] = c[1]
+        assert got.get(rid) == 0
+        # a plan for a different node shape is refused
+        st = s2.plan_state()
+        st["num_gpus"] = 3
+        assert not s2.restore_plan(st)
+    finally:
+        s2.shutdown()
+
+
 def test_stale_requests_are_dropped_with_deadline():
     s = make_sched()
     try:
