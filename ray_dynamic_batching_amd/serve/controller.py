@@ -157,6 +157,7 @@ class ServeController:
         except (RuntimeError, OSError):  # pragma: no cover - control RPC is optional
             self.agent_socket = ""
         self.default_mode = os.environ.get("RDB_SERVE_MODE", "auto")
+        self.shutdown_requested = threading.Event()   # set by a remote `serve shutdown`
         self._stop = threading.Event()
         self._thread = threading.Thread(target=self._control_loop, name="rdb-serve-controller", daemon=True)
         self._thread.start()
@@ -394,6 +395,7 @@ class ServeController:
     # ------------------------------------------------------------ control loop
     def _control_loop(self) -> None:
         last_health: Dict[Tuple[str, str], float] = {}
+        ticks = 0
         while not self._stop.wait(CONTROL_LOOP_INTERVAL_S):
             try:
                 with self.lock:
@@ -401,8 +403,37 @@ class ServeController:
                         for st in states.values():
                             self._health_tick(st, last_health)
                             self._autoscale_tick(st)
+                ticks += 1
+                if ticks % 5 == 0:
+                    self._remote_requests()
             except Exception:  # pragma: no cover
                 logger.error("controller loop error:\n%s", traceback.format_exc())
+
+    # ------------------------------------------------------------ remote control
+    # `serve deploy` / `serve shutdown` from another process (reference: the CLI
+    # talks to the running controller, serve/scripts.py:320,779): the request is
+    # a key in the node agent's KV (written over the agent's control socket) and
+    # this loop picks it up within ~0.5 s.
+    SHUTDOWN_KEY = "serve/request/shutdown"
+    DEPLOY_KEY = "serve/request/deploy"
+
+    def _remote_requests(self) -> None:
+        dep = self.agent.kv_get(self.DEPLOY_KEY)
+        if dep:
+            self.agent.kv_delete(self.DEPLOY_KEY)
+            try:
+                from .schema import ServeDeploySchema, deploy_config
+
+                deploy_config(ServeDeploySchema.model_validate(json.loads(bytes(dep).decode())))
+                self.agent.kv_put("serve/request/deploy_result", b"OK")
+            except Exception as e:  # report back to the CLI instead of killing the loop
+                logger.error("remote deploy failed:\n%s", traceback.format_exc())
+                self.agent.kv_put("serve/request/deploy_result", f"ERROR {e}".encode())
+        if self.agent.kv_get(self.SHUTDOWN_KEY):
+            self.agent.kv_delete(self.SHUTDOWN_KEY)
+            logger.info("shutdown requested over the control socket")
+            self.shutdown_requested.set()
+            threading.Thread(target=self.shutdown, name="rdb-serve-shutdown", daemon=True).start()
 
     def _health_tick(self, st: DeploymentState, last: Dict) -> None:
         now = time.time()
@@ -546,6 +577,12 @@ class ServeController:
         try:
             self.agent.shutdown(5.0)
         except Exception:  # pragma: no cover
+            pass
+        try:  # no stale discovery record for `serve status` / `serve shutdown`
+            with open(discovery_file()) as f:
+                if json.load(f).get("pid") == os.getpid():
+                    os.remove(discovery_file())
+        except (OSError, ValueError):
             pass
         with _CTRL_LOCK:
             if _CONTROLLER is self:

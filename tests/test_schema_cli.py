@@ -57,3 +57,32 @@ def test_cli_status_queries_live_node_agent(tmp_path):
     finally:
         serve.shutdown()
         os.environ.pop("RDB_SERVE_DISCOVERY", None)
+
+
+def test_cli_start_remote_deploy_status_shutdown(tmp_path):
+    """`serve start` in one process; `serve deploy` hands the YAML to it over the
+    node agent's control socket; `serve shutdown` stops it (reference:
+    serve/scripts.py start/deploy/shutdown against a running instance)."""
+    env = dict(os.environ, PYTHONPATH=ROOT, RDB_SERVE_DISCOVERY=str(tmp_path / "disc.json"))
+    cli = [sys.executable, "-m", "ray_dynamic_batching_amd.serve.cli"]
+    inst = subprocess.Popen(cli + ["start", "--duration", "120"], stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
+                            text=True, env=env, cwd=ROOT)
+    try:
+        import time
+
+        t_end = time.time() + 60
+        while not (tmp_path / "disc.json").exists() and time.time() < t_end:
+            time.sleep(0.1)
+        assert (tmp_path / "disc.json").exists(), "instance never published its discovery record"
+        out = subprocess.run(cli + ["deploy", os.path.join(ROOT, "configs", "mlp_local.yaml")], capture_output=True,
+                             text=True, env=env, cwd=ROOT, timeout=120)
+        assert out.returncode == 0 and "running instance" in out.stdout, out.stdout + out.stderr
+        out = subprocess.run(cli + ["status"], capture_output=True, text=True, env=env, cwd=ROOT, timeout=60)
+        assert out.returncode == 0 and '"mlp"' in out.stdout, out.stdout + out.stderr
+        out = subprocess.run(cli + ["shutdown", "-y"], capture_output=True, text=True, env=env, cwd=ROOT, timeout=60)
+        assert out.returncode == 0 and "shut down" in out.stdout, out.stdout + out.stderr
+        assert inst.wait(timeout=60) == 0
+    finally:
+        if inst.poll() is None:
+            inst.kill()
+            inst.wait(10)
