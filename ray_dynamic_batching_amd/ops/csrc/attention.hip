@@ -24,7 +24,9 @@ namespace rdb {
 
 template <int D>
 struct AttnCfg {
-  static constexpr int KB = 128;                 // keys per LDS block
+  // keys per LDS block: 64 at D = 128 keeps S^T (and the K/V staging) within
+  // the register budget next to the 128-wide O accumulator (KB = 128 spilled)
+  static constexpr int KB = D == 128 ? 64 : 128;
   static constexpr int ROWB = D * 2;             // bytes per K row
   static constexpr int CPR = ROWB / 16;          // 16-B chunks per K row (8 or 16)
   static constexpr int VT_LD = KB + 8;           // V^T row length (elements)
@@ -72,27 +74,59 @@ attn_fwd_kernel(const T* __restrict__ qkv, int ld_qkv, int q_off, int k_off, int
   const int hk = h / (H / Hkv);
   const int q0 = blockIdx.x * 128 + wid * 32;  // this wave's first query row
   const size_t tok0 = (size_t)b * S;
-  int kv_len = lens ? lens[b] : S;
-  kv_len = kv_len > S ? S : kv_len;
+
+  // K/V staging: EVERY load of a block is issued before the first LDS write
+  // (one memory round trip per block); rows past S clamp to a valid row, their
+  // scores are masked below.  Block 0 is always needed, so its loads go out
+  // before anything else -- in particular before the key length arrives.
+  // D = 128 stages in two halves so the staging registers stay at 32 VGPRs
+  // (holding all 16 K/V vectors spilled at D = 128).
+  constexpr int NST = KB * C::CPR / 256;          // 16-B K (and V) vectors per thread per block
+  constexpr int NCH = NST > 4 ? 4 : NST;          // ... held in registers at a time
+  constexpr int NPART = NST / NCH;
+  u32x4 kreg[NCH];
+  frag8 vreg[NCH];
+  auto load_kv = [&](int key0, int part) {
+#pragma unroll
+    for (int j = 0; j < NCH; ++j) {
+      const int qd = tid + 256 * (part * NCH + j);
+      const int krow = min(key0 + qd / C::CPR, S - 1), kc = qd % C::CPR;
+      kreg[j] = *reinterpret_cast<const u32x4*>(qkv + (tok0 + krow) * ld_qkv + k_off + hk * D + kc * 8);
+      const int vrow = min(key0 + (qd & (KB - 1)), S - 1), vc = qd / KB;
+      vreg[j] = *reinterpret_cast<const frag8*>(qkv + (tok0 + vrow) * ld_qkv + v_off + hk * D + vc * 8);
+    }
+  };
+  auto store_kv = [&](int part) {
+#pragma unroll
+    for (int j = 0; j < NCH; ++j) {   // K row-major, swizzled
+      const int qd = tid + 256 * (part * NCH + j), row = qd / C::CPR, c = qd % C::CPR;
+      *reinterpret_cast<u32x4*>(Ks + kswz<C::CPR>(row, c)) = kreg[j];
+    }
+#pragma unroll
+    for (int j = 0; j < NCH; ++j) {   // V transposed: lanes of a wave take consecutive keys
+      const int qd = tid + 256 * (part * NCH + j), row = qd & (KB - 1), c = qd / KB;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) Vt[(c * 8 + e) * C::VT_LD + row] = vreg[j][e];
+    }
+  };
+  load_kv(0, 0);
 
   // Q fragments (B operand): lane holds Q[q][ks*32 + 8*fg + j].
   frag8 qf[2][NKS];
 #pragma unroll
   for (int qt = 0; qt < 2; ++qt) {
-    const int q = q0 + qt * 16 + fr;
+    const int q = min(q0 + qt * 16 + fr, S - 1);  // rows past S are computed, never stored
 #pragma unroll
-    for (int ks = 0; ks < NKS; ++ks) {
-      if (q < S)
-        qf[qt][ks] = *reinterpret_cast<const frag8*>(qkv + (tok0 + q) * ld_qkv + q_off + h * D +
-                                                        ks * 32 + fg * 8);
-      else
-        qf[qt][ks] = frag8{};
-    }
+    for (int ks = 0; ks < NKS; ++ks)
+      qf[qt][ks] = *reinterpret_cast<const frag8*>(qkv + (tok0 + q) * ld_qkv + q_off + h * D + ks * 32 + fg * 8);
   }
+  int kv_len = lens ? lens[b] : S;
+  kv_len = kv_len > S ? S : kv_len;
 
   f32x4 o[NDT][2];
 #pragma unroll
   for (int i = 0; i < NDT; ++i) o[i][0] = o[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // running max in the SCALED (log2) domain; raw scores are scaled inside exp2's FMA
   float m_run[2] = {-INFINITY, -INFINITY}, l_run[2] = {0.f, 0.f};
 
   // Causal: keys beyond the block's last query are never needed.
@@ -105,25 +139,12 @@ attn_fwd_kernel(const T* __restrict__ qkv, int ld_qkv, int q_off, int k_off, int
 
   for (int kb = 0; kb < nblk; ++kb) {
     const int key0 = kb * KB;
+    if (kb > 0) load_kv(key0, 0);
     __syncthreads();  // previous block's LDS reads are done
-    // ---- stage K (row-major, swizzled) ----
 #pragma unroll
-    for (int i = 0; i < KB * C::CPR / 256; ++i) {
-      const int qd = tid + 256 * i, row = qd / C::CPR, c = qd % C::CPR;
-      const int key = key0 + row;
-      u32x4 v = {0, 0, 0, 0};
-      if (key < S) v = *reinterpret_cast<const u32x4*>(qkv + (tok0 + key) * ld_qkv + k_off + hk * D + c * 8);
-      *reinterpret_cast<u32x4*>(Ks + kswz<C::CPR>(row, c)) = v;
-    }
-    // ---- stage V transposed: lanes of a wave take consecutive keys ----
-#pragma unroll
-    for (int i = 0; i < KB * C::CPR / 256; ++i) {
-      const int qd = tid + 256 * i, row = qd & (KB - 1), c = qd / KB;
-      const int key = key0 + row;
-      frag8 v = frag8{};
-      if (key < S) v = *reinterpret_cast<const frag8*>(qkv + (tok0 + key) * ld_qkv + v_off + hk * D + c * 8);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) Vt[(c * 8 + j) * C::VT_LD + row] = v[j];
+    for (int part = 0; part < NPART; ++part) {
+      if (part > 0) load_kv(key0, part);
+      store_kv(part);
     }
     __syncthreads();
 
@@ -140,37 +161,46 @@ attn_fwd_kernel(const T* __restrict__ qkv, int ld_qkv, int q_off, int k_off, int
       }
     }
 
-    // ---- mask, online softmax (lane-local query q = q0 + qt*16 + fr) ----
+    // ---- mask (only blocks that need it: wave-uniform test), online softmax
+    // (lane-local query q = q0 + qt*16 + fr) ----
+    const bool need_mask = key0 + KB > kv_len || (causal && key0 + KB - 1 > q0);
 #pragma unroll
     for (int qt = 0; qt < 2; ++qt) {
       const int q = q0 + qt * 16 + fr;
       float mx = -INFINITY;
+      if (need_mask) {
 #pragma unroll
-      for (int kt = 0; kt < NKT; ++kt)
+        for (int kt = 0; kt < NKT; ++kt)
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int key = key0 + kt * 16 + fg * 4 + e;
-          float x = s[kt][qt][e] * scale_log2e;
-          const bool masked = (key >= kv_len) || (causal && key > q);
-          x = masked ? -INFINITY : x;
-          s[kt][qt][e] = x;
-          mx = fmaxf(mx, x);
-        }
+          for (int e = 0; e < 4; ++e) {
+            const int key = key0 + kt * 16 + fg * 4 + e;
+            const bool masked = (key >= kv_len) || (causal && key > q);
+            s[kt][qt][e] = masked ? -INFINITY : s[kt][qt][e];
+            mx = fmaxf(mx, s[kt][qt][e]);
+          }
+      } else {
+#pragma unroll
+        for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) mx = fmaxf(mx, s[kt][qt][e]);
+      }
       mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      const float m_new = fmaxf(m_run[qt], mx);
+      const float m_new = fmaxf(m_run[qt], mx * scale_log2e);   // scale > 0: max commutes
       const float m_use = (m_new == -INFINITY) ? 0.f : m_new;
-      const float alpha = exp2f(m_run[qt] - m_use);
-      m_run[qt] = m_new;
-      l_run[qt] *= alpha;
+      if (kb > 0) {  // the first block has nothing to rescale
+        const float alpha = exp2f(m_run[qt] - m_use);
+        l_run[qt] *= alpha;
 #pragma unroll
-      for (int dt = 0; dt < NDT; ++dt) o[dt][qt] *= alpha;
+        for (int dt = 0; dt < NDT; ++dt) o[dt][qt] *= alpha;
+      }
+      m_run[qt] = m_new;
       float ls = 0.f;
 #pragma unroll
       for (int kt = 0; kt < NKT; ++kt)
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          const float p = exp2f(s[kt][qt][e] - m_use);
+          const float p = exp2f(fmaf(s[kt][qt][e], scale_log2e, -m_use));
           s[kt][qt][e] = p;
           ls += p;
         }
