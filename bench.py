@@ -123,6 +123,9 @@ def main():
         runner = EngineRunner(name, rank, [spec], pipeline_depth=args.pipeline_depth,
                               compute_streams=args.compute_streams).build()
     runner.start()
+    if not echo and getattr(runner, "tuning_changes", None):
+        print(json.dumps({"rank": rank, "in_context_tile_changes": {str(k[2:5]): v for k, v in runner.tuning_changes.items()}}),
+              file=sys.stderr, flush=True)
     barrier()
 
     result = {}

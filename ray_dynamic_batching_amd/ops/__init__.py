@@ -66,13 +66,66 @@ def tuning_table() -> Dict[tuple, int]:
     return dict(_TUNE)
 
 
+_TUNE_TOP: Dict[tuple, list] = {}
+
+
+def tune_in_context(time_forward: Callable[[], float], keys: Optional[list] = None, min_gain: float = 0.01) -> dict:
+    """Pick among each GEMM shape's near-tied tiles by timing the WHOLE forward.
+
+    The per-shape tuner times a GEMM alone; inside a forward its inputs were just
+    written by the previous kernel (dirty L2 lines, MALL residency) and its
+    neighbours compete for the chip, and tiles within a few percent of each other
+    alone can differ by 20 % there.  ``time_forward()`` must re-capture/replay the
+    forward with the current ``_TUNE`` table and return its time; shapes are
+    visited one at a time (coordinate descent), a change is kept only if it beats
+    the current best by ``min_gain``.  Returns {key: (old, new)} for changed keys."""
+    changed = {}
+    best = time_forward()
+    for key in list(keys if keys is not None else _TUNE_TOP):
+        cands = _TUNE_TOP.get(key, [])
+        if len(cands) < 2 or key not in _TUNE:
+            continue
+        start = cur = _TUNE[key]
+        for c in cands:
+            if c == cur:
+                continue
+            _TUNE[key] = c
+            t = time_forward()
+            if t < best * (1 - min_gain):
+                best, cur = t, c
+        _TUNE[key] = cur
+        if cur != start:
+            changed[key] = (start, cur)
+    return changed
+
+
+_KEY_LOG: Optional[list] = None
+
+
+class record_tuning_keys:
+    """``with record_tuning_keys() as keys: model(x)`` -> the tuned GEMM/conv keys that forward used."""
+
+    def __enter__(self):
+        global _KEY_LOG
+        _KEY_LOG = []
+        return _KEY_LOG
+
+    def __exit__(self, *exc):
+        global _KEY_LOG
+        _KEY_LOG = None
+        return False
+
+
 def _tuned_cfg(key: tuple, launch: Callable[[int], None], candidates=range(NUM_TILE_CFGS)) -> int:
+    if _KEY_LOG is not None and key not in _KEY_LOG:
+        _KEY_LOG.append(key)
     cfg = _TUNE.get(key)
     if cfg is not None:
         return cfg
     if not autotune_enabled() or torch.cuda.is_current_stream_capturing():
         return -1
     best_t, best_c = float("inf"), -1
+    times: Dict[int, float] = {}
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     # RDB_TUNE_STREAMS=n (n > 1): rank tiles by THROUGHPUT with n launches in
     # flight on n streams -- what a replica running n concurrent batches sees --
@@ -96,8 +149,11 @@ def _tuned_cfg(key: tuple, launch: Callable[[int], None], candidates=range(NUM_T
         e.record()
         e.synchronize()
         t = s.elapsed_time(e)
+        times[c] = t
         if t < best_t:
             best_t, best_c = t, c
+    # the runners-up within 15 %: candidates for in-context selection (tune_in_context)
+    _TUNE_TOP[key] = [c for c in sorted(times, key=times.get) if times[c] <= best_t * 1.15][:3]
     _TUNE[key] = best_c
     return best_c
 

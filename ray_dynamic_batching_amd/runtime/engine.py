@@ -69,6 +69,12 @@ class EngineRunner:
         self.pools = []
         self.capture_s = 0.0
         self.warmup_iters = warmup_iters
+        # whole-forward selection among near-tied GEMM tiles for the largest bucket
+        # (ops.tune_in_context); RDB_TUNE_IN_CONTEXT=0 turns it off
+        import os
+
+        self.tune_in_context = os.environ.get("RDB_TUNE_IN_CONTEXT", "1") == "1"
+        self.tuning_changes = {}
 
     def _bytes(self, shape, dtype) -> int:
         n = 1
@@ -97,7 +103,8 @@ class EngineRunner:
                     x.copy_(m.example_input(s.max_batch, seed=slot, device=dev))
                 s.inputs.append(x)
                 self.engine.set_input(s.sid, slot, x.data_ptr())
-            # warm up every bucket eagerly on a side stream (lazy init, caches)
+            # warm up every bucket eagerly on a side stream (lazy init, caches,
+            # per-shape kernel autotuning)
             side = torch.cuda.Stream(device=dev)
             side.wait_stream(torch.cuda.current_stream())
             with torch.cuda.stream(side):
@@ -106,6 +113,8 @@ class EngineRunner:
                         m.forward(s.inputs[0][:b])
             torch.cuda.current_stream().wait_stream(side)
             torch.cuda.synchronize()
+            if self.tune_in_context:
+                self.tuning_changes.update(self._tune_in_context(m, s.inputs[0][:buckets[-1]], dev))
             s.graphs = [[None] * self.depth for _ in buckets]
             s.outputs = [[None] * self.depth for _ in buckets]
             for bi, b in enumerate(buckets):
@@ -131,6 +140,42 @@ class EngineRunner:
         torch.cuda.synchronize()
         self.capture_s = time.perf_counter() - t0
         return self
+
+    @staticmethod
+    def _tune_in_context(m, x, dev) -> dict:
+        from .. import ops
+
+        with ops.record_tuning_keys() as keys:
+            with torch.no_grad():
+                m.forward(x)
+        torch.cuda.synchronize()
+        if not keys:
+            return {}
+        pool = torch.cuda.graph_pool_handle()
+
+        def time_forward() -> float:
+            g = torch.cuda.CUDAGraph()
+            side = torch.cuda.Stream(device=dev)
+            side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side):
+                with torch.cuda.graph(g, pool=pool, stream=side):
+                    m.forward(x)
+            torch.cuda.synchronize()
+            for _ in range(3):
+                g.replay()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            best = float("inf")
+            for _ in range(3):
+                e0.record()
+                for _ in range(10):
+                    g.replay()
+                e1.record()
+                torch.cuda.synchronize()
+                best = min(best, e0.elapsed_time(e1) / 10)
+            del g
+            return best
+
+        return ops.tune_in_context(time_forward, keys=list(keys), min_gain=0.02)
 
     def start(self):
         self.engine.start()
