@@ -11,7 +11,7 @@
     handle.remote(x).result()
 """
 from .api import Application, Deployment, delete, deployment, get_app_handle, get_deployment_handle, http_port, \
-    run, shutdown, start, status
+    metrics_text, run, shutdown, start, status
 from .batching import batch
 from .config import AutoscalingConfig, DeploymentConfig, EngineConfig
 from .context import get_replica_context
@@ -26,5 +26,5 @@ __all__ = [
     "get_app_handle", "get_deployment_handle", "get_replica_context", "multiplexed", "get_multiplexed_model_id",
     "DeploymentHandle", "DeploymentResponse", "DeploymentResponseGenerator", "AutoscalingConfig",
     "DeploymentConfig", "EngineConfig", "BackPressureError", "RayServeException", "RequestCancelledError",
-    "RequestDroppedError", "model_deployment", "TensorCodec", "HTTPRequest", "http_port",
+    "RequestDroppedError", "model_deployment", "TensorCodec", "HTTPRequest", "http_port", "metrics_text",
 ]

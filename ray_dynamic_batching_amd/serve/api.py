@@ -200,6 +200,11 @@ def delete(name: str, _blocking: bool = True) -> None:
         ctrl.delete_application(name)
 
 
+def metrics_text() -> str:
+    """Prometheus text of the running instance (user metrics + serving counters)."""
+    return _controller().metrics_text()
+
+
 def status():
     ctrl = _controller(create=False)
     return ctrl.status() if ctrl is not None else {"applications": {}}

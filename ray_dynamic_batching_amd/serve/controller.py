@@ -299,6 +299,9 @@ class ServeController:
         env = dict(visible_devices_env(gpus))
         env["RDB_ROUTING_TABLE"] = self._routes_path
         env["RDB_JOB"] = job.info()["name"]
+        if self.agent_socket:   # user metrics (utils.user_metrics) are published through the agent KV
+            env["RDB_AGENT_SOCKET"] = self.agent_socket
+            env["RDB_METRICS_KEY"] = f"{st.app_name}/{st.name}/{rep.slot}"
         env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
         pkg_root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
         env["PYTHONPATH"] = pkg_root + os.pathsep + os.environ.get("PYTHONPATH", "")
@@ -509,6 +512,36 @@ class ServeController:
             app_name = matches[0]
         self.router_for(app_name, deployment)
         return DeploymentHandle(deployment, app_name)
+
+    def metrics_text(self) -> str:
+        """Prometheus exposition of the whole instance: user metrics of this
+        process and of every replica process (snapshots in the agent KV) plus
+        the native per-replica serving counters of every process-mode app."""
+        from ..utils import metrics as shm_metrics
+        from ..utils import user_metrics as um
+
+        snaps = [({"process": "controller"}, um.registry_snapshot())]
+        for k in self.agent.kv_keys(um.KV_PREFIX):
+            blob = self.agent.kv_get(k)
+            parts = k[len(um.KV_PREFIX):].split("/")
+            if not blob or len(parts) != 3:
+                continue
+            try:
+                snaps.append((dict(application=parts[0], deployment=parts[1], replica=parts[2]),
+                              json.loads(bytes(blob).decode())))
+            except ValueError:
+                continue
+        text = um.render_prometheus(snaps)
+        with self.lock:
+            for app_name, states in self.apps.items():
+                job = self.jobs.get(app_name)
+                if job is None:
+                    continue
+                deps = {st.model_id: st.name for st in states.values()}
+                qmap = {r.slot: r.slot for st in states.values() for r in st.proc_replicas}
+                if qmap:
+                    text += shm_metrics.prometheus_text(job, deps, qmap)
+        return text
 
     def status(self) -> Dict[str, Any]:
         out = {"applications": {}}

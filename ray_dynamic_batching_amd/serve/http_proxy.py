@@ -134,7 +134,12 @@ class HTTPProxy:
         async def routes(request):
             return JSONResponse({p or "/": a for a, p in self.controller.route_prefixes.items() if p is not None})
 
-        return Starlette(routes=[Route("/-/healthz", health), Route("/-/routes", routes),
+        async def metrics(request):
+            from starlette.responses import PlainTextResponse
+
+            return PlainTextResponse(self.controller.metrics_text(), media_type="text/plain; version=0.0.4")
+
+        return Starlette(routes=[Route("/-/healthz", health), Route("/-/routes", routes), Route("/-/metrics", metrics),
                                  Route("/{path:path}", handle, methods=["GET", "POST", "PUT", "DELETE"])])
 
     def start(self, timeout_s: float = 30.0) -> "HTTPProxy":

@@ -55,6 +55,10 @@ def main(argv=None) -> int:
     def _term(*_):
         stop.set()
     signal.signal(signal.SIGTERM, _term)
+    if os.environ.get("RDB_AGENT_SOCKET") and os.environ.get("RDB_METRICS_KEY"):
+        from ..utils import user_metrics
+
+        user_metrics.start_publisher(os.environ["RDB_AGENT_SOCKET"], os.environ["RDB_METRICS_KEY"])
 
     def heartbeat():
         while not stop.is_set():
