@@ -97,9 +97,14 @@ def main():
     from ray_dynamic_batching_amd.runtime import job as rjob
     from ray_dynamic_batching_amd.runtime.engine import EngineRunner, SessionSpec
 
+    # Host-side rendezvous runs over a gloo group: an RCCL barrier would leave a
+    # spinning all-reduce kernel on ranks 1..N-1 (occupying CUs their replica
+    # engine serves on) for the whole timed region, while rank 0 drives load.
+    host_pg = dist.new_group(backend="gloo") if (world > 1 and not echo) else None
+
     def barrier():
         if world > 1:
-            dist.barrier()
+            dist.barrier(group=host_pg)
 
     port = os.environ.get("MASTER_PORT", str(os.getpid()))
     name = f"bench_{port}"
@@ -157,8 +162,8 @@ def main():
     barrier()
     err = runner.error()
     if world > 1:
-        t = torch.tensor([elapsed], device="cpu" if echo else "cuda", dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=host_pg)
         elapsed = t.item()
     if rank == 0 and args.trace_out:
         from ray_dynamic_batching_amd.utils.tracing import collect, export_chrome_trace, summarize
