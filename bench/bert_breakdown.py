@@ -20,15 +20,23 @@ def main():
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--layers", type=int, default=12)
+    ap.add_argument("--tune-file", default="", help="load the GEMM tile table from this JSON if it exists, "
+                                                    "else write the tuned table to it")
     a = ap.parse_args()
     import torch
+
+    from ray_dynamic_batching_amd import ops
 
     from ray_dynamic_batching_amd.models.bert import BertConfig, BertForSequenceClassification
 
     m = BertForSequenceClassification(BertConfig(layers=a.layers), device="cuda:0", backend="hip")
     ids = m.example_input(a.batch, seed=0)
+    if a.tune_file and os.path.exists(a.tune_file):
+        ops.load_tuning(a.tune_file)
     for _ in range(3):
         m(ids)
+    if a.tune_file and not os.path.exists(a.tune_file):
+        ops.save_tuning(a.tune_file)
     torch.cuda.synchronize()
     g = torch.cuda.CUDAGraph()
     s = torch.cuda.Stream()

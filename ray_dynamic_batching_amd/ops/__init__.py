@@ -66,6 +66,35 @@ def tuning_table() -> Dict[tuple, int]:
     return dict(_TUNE)
 
 
+def _key_json(key: tuple) -> list:
+    return [str(v) if isinstance(v, torch.dtype) else v for v in key]
+
+
+def _key_from_json(key: list) -> tuple:
+    return tuple(getattr(torch, v.split(".", 1)[1]) if isinstance(v, str) and v.startswith("torch.") else v
+                 for v in key)
+
+
+def save_tuning(path: str) -> None:
+    """Write the per-shape tile table (JSON) so another process replays the same
+    kernel choices (profiling passes, A/B runs) instead of re-tuning."""
+    import json
+
+    with open(path, "w") as f:
+        json.dump([[_key_json(k), c] for k, c in _TUNE.items()], f)
+
+
+def load_tuning(path: str) -> int:
+    """Load a table written by save_tuning(); returns the number of entries."""
+    import json
+
+    with open(path) as f:
+        rows = json.load(f)
+    for k, c in rows:
+        _TUNE[_key_from_json(k)] = int(c)
+    return len(rows)
+
+
 _TUNE_TOP: Dict[tuple, list] = {}
 
 
