@@ -17,6 +17,8 @@ runs: ``model(inputs)`` at scheduler.py:450).
 """
 from __future__ import annotations
 
+import os
+
 import math
 from dataclasses import dataclass
 
@@ -63,6 +65,14 @@ class BertForSequenceClassification:
             raise ValueError("the hip backend needs a GPU device")
         self.backend = backend
         self.cls_only_last_layer = True
+        # deferred LayerNorm (ops.linear_ln): the GEMMs around each LayerNorm
+        # carry it, no LayerNorm kernel runs inside the layer stack
+        # (RDB_BERT_FOLD_LN=1/0 forces it; by default a replica engine enables it
+        # only with one compute stream -- see EngineRunner.build)
+        env = os.environ.get("RDB_BERT_FOLD_LN", "")
+        self.fold_ln = env != "0"
+        self.fold_ln_auto = env == ""
+        self._folded = None
         g = torch.Generator(device="cpu").manual_seed(seed)
         D, I = cfg.hidden, cfg.intermediate
 
@@ -121,7 +131,27 @@ class BertForSequenceClassification:
             return self._forward_hip(ids)
         return self._forward_torch(ids)
 
+    def refresh_folded_weights(self):
+        """Recompute the LayerNorm-folded weights (call after changing weights)."""
+        self._folded = None
+
+    def _folded_weights(self):
+        if self._folded is None:
+            f = []
+            for i, L in enumerate(self.layers):
+                d = {}
+                if i > 0:   # layer i's QKV consumes LN2 of layer i-1
+                    P = self.layers[i - 1]
+                    d["w_qkv"], d["cs_qkv"], d["b_qkv"] = ops.fold_ln_weights(L["w_qkv"], L["b_qkv"], P["ln2_g"],
+                                                                              P["ln2_b"])
+                d["w_i"], d["cs_i"], d["b_i"] = ops.fold_ln_weights(L["w_i"], L["b_i"], L["ln1_g"], L["ln1_b"])
+                f.append(d)
+            self._folded = f
+        return self._folded
+
     def _forward_hip(self, ids: torch.Tensor) -> torch.Tensor:
+        if self.fold_ln and self.dtype == torch.bfloat16 and self.cfg.hidden % 4 == 0:
+            return self._forward_hip_folded(ids)
         c = self.cfg
         B, S = ids.shape
         D, H = c.hidden, c.heads
@@ -144,6 +174,52 @@ class BertForSequenceClassification:
             h = ops.layer_norm(o, L["ln2_g"], L["ln2_b"], c.eps)
         cls = h if self.cls_only_last_layer else h.view(B, S, D)[:, 0, :]
         pooled = ops.linear(cls, self.w_pool, self.b_pool, act="tanh")
+        return ops.linear(pooled, self.w_cls, self.b_cls, out_dtype=torch.float32)
+
+    def _forward_hip_folded(self, ids: torch.Tensor) -> torch.Tensor:
+        """Post-LN BERT with every in-stack LayerNorm deferred into the GEMMs
+        (ops.linear_ln): o-proj / FFN-down accumulate row statistics of what they
+        store, FFN-up / next QKV consume the raw rows with gamma folded into their
+        weights, and the residual adds normalise their operand on load."""
+        c = self.cfg
+        B, S = ids.shape
+        D, H, eps = c.hidden, c.heads, c.eps
+        Fw = self._folded_weights()
+        lens = ops.seq_lens(ids, c.pad_token_id)
+        M = B * S
+        n = len(self.layers)
+        stats = torch.empty(n, 2, M, 2, device=ids.device, dtype=torch.float32)   # zeroed by embed_ln
+        x = ops.embed_ln(ids, self.word, self.pos, self.typ, self.emb_g, self.emb_b, eps, zero_stats=stats)
+        xs = xg = xb = None        # x is raw (pre-LN2 of the previous layer) iff xs is not None
+        h = None
+        for i, L in enumerate(self.layers):
+            if xs is None:
+                qkv = ops.linear(x, L["w_qkv"], L["b_qkv"])
+            else:
+                qkv = ops.linear_ln(x, Fw[i]["w_qkv"], lna=(xs, Fw[i]["cs_qkv"], Fw[i]["b_qkv"], D, eps))
+            ctx = ops.attention(qkv, B, S, H, H, D // H, lens=lens)
+            if i == n - 1 and self.cls_only_last_layer:
+                # CLS rows only (see _forward_hip): materialise their normalised
+                # residual and finish on the plain kernels (B rows)
+                xc = x.view(B, S, D)[:, 0, :]
+                hc = xc if xs is None else ops.layer_norm(xc, xg, xb, eps)
+                a = ops.linear(ctx.view(B, S, D)[:, 0, :], L["w_o"], L["b_o"], residual=hc)
+                h1 = ops.layer_norm(a, L["ln1_g"], L["ln1_b"], eps)
+                inter = ops.linear(h1, L["w_i"], L["b_i"], act="gelu")
+                o = ops.linear(inter, L["w_out"], L["b_out"], residual=h1)
+                h = ops.layer_norm(o, L["ln2_g"], L["ln2_b"], eps)
+                break
+            s_a, s_o = stats[i, 0], stats[i, 1]
+            a = ops.linear_ln(ctx, L["w_o"], L["b_o"], residual=x,
+                              lnr=None if xs is None else (xs, xg, xb, D, eps), out_stats=s_a)
+            inter = ops.linear_ln(a, Fw[i]["w_i"], act="gelu", lna=(s_a, Fw[i]["cs_i"], Fw[i]["b_i"], D, eps))
+            o = ops.linear_ln(inter, L["w_out"], L["b_out"], residual=a, lnr=(s_a, L["ln1_g"], L["ln1_b"], D, eps),
+                              out_stats=s_o)
+            x, xs, xg, xb = o, s_o, L["ln2_g"], L["ln2_b"]
+        if h is None:
+            h = ops.layer_norm(x, xg, xb, eps) if xs is not None else x
+            h = h.view(B, S, D)[:, 0, :]
+        pooled = ops.linear(h, self.w_pool, self.b_pool, act="tanh")
         return ops.linear(pooled, self.w_cls, self.b_cls, out_dtype=torch.float32)
 
     def _forward_torch(self, ids: torch.Tensor) -> torch.Tensor:

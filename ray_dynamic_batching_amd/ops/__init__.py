@@ -239,6 +239,110 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
     return out
 
 
+LN_LNA, LN_LNR, LN_STATS = 1, 2, 4
+
+
+def _stats_ld(st: torch.Tensor, M: int, what: str) -> int:
+    _check(st.dtype == torch.float32 and st.dim() == 2 and st.shape[0] == M and st.shape[1] >= 2
+           and st.stride(1) == 1 and st.stride(0) % 2 == 0 and _aligned(st, 8), f"linear_ln: bad {what} stats")
+    return st.stride(0)
+
+
+def linear_ln(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, act: str = "none",
+              residual: Optional[torch.Tensor] = None, lna: Optional[tuple] = None, lnr: Optional[tuple] = None,
+              out_stats: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None,
+              tile_cfg: int = -1) -> torch.Tensor:
+    """GEMM with the deferred-LayerNorm epilogues (bf16; ``gemm_ln.hip``).
+
+    * ``lna=(stats, colsum, bias_f32, D, eps)``: x holds RAW rows whose LayerNorm
+      is folded into w (w = W * gamma, colsum = w.float().sum(1), bias_f32 =
+      b + W @ beta); ``stats`` [M, 2] f32 = per-row (sum, sum of squares).
+      y = act(LN(x) @ W.T + b); ``bias`` must be None.
+    * ``lnr=(stats, gamma, beta, D, eps)``: ``residual`` holds raw rows and is
+      added as LayerNorm(residual) (normalised on load).
+    * ``out_stats`` [M, 2] f32: += per-row (sum, sum of squares) of the stored y
+      (must be zeroed by the caller before the first producer writes it).
+    """
+    _check(x.is_cuda and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16, "linear_ln: bf16 on the GPU")
+    _check(w.dim() == 2 and w.is_contiguous(), "linear_ln: w must be a contiguous [N, K] matrix")
+    N, K = w.shape
+    _check(x.dim() == 2 and x.stride(1) == 1 and x.shape[1] == K, "linear_ln: x must be a 2-D [M, K] (row-strided) view")
+    M, lda = x.shape[0], x.stride(0)
+    _check(K % 8 == 0 and lda % 8 == 0 and N % 4 == 0 and _aligned(x) and _aligned(w), "linear_ln: alignment")
+    _check(act != "swiglu", "linear_ln: no swiglu")
+    mode = (LN_LNA if lna is not None else 0) | (LN_LNR if lnr is not None else 0) | \
+        (LN_STATS if out_stats is not None else 0)
+    _check(mode in (LN_LNA, LN_STATS, LN_LNR | LN_STATS), "linear_ln: modes are lna, out_stats, or lnr + out_stats")
+    if out is None:
+        out = torch.empty(M, N, device=x.device, dtype=x.dtype)
+    _check(out.is_contiguous() and out.shape == (M, N), "linear_ln: bad out")
+    if bias is not None:
+        _check(bias.is_contiguous() and bias.numel() == N and bias.dtype == x.dtype, "linear_ln: bad bias")
+    ldr = 0
+    if residual is not None:
+        _check(residual.dim() == 2 and residual.shape == (M, N) and residual.stride(1) == 1
+               and residual.stride(0) % 4 == 0 and residual.dtype == x.dtype and _aligned(residual, 8),
+               "linear_ln: bad residual")
+        ldr = residual.stride(0)
+    a_st = a_cs = a_b = r_st = r_g = r_b = o_st = None
+    a_ld = r_ld = o_ld = 0
+    a_inv = r_inv = 0.0
+    eps = 0.0
+    if lna is not None:
+        a_st, a_cs, a_b, d, eps = lna
+        a_ld = _stats_ld(a_st, M, "lna")
+        _check(a_cs.dtype == torch.float32 and a_cs.numel() == N and a_cs.is_contiguous()
+               and a_b.dtype == torch.float32 and a_b.numel() == N and a_b.is_contiguous(), "linear_ln: bad lna vectors")
+        a_inv = 1.0 / d
+    if lnr is not None:
+        _check(residual is not None, "linear_ln: lnr needs the residual")
+        r_st, r_g, r_b, d, eps_r = lnr
+        r_ld = _stats_ld(r_st, M, "lnr")
+        _check(r_g.numel() == N and r_b.numel() == N and r_g.dtype == x.dtype and r_b.dtype == x.dtype
+               and r_g.is_contiguous() and r_b.is_contiguous(), "linear_ln: bad lnr gamma/beta")
+        _check(lna is None or eps_r == eps, "linear_ln: one eps")
+        r_inv, eps = 1.0 / d, eps_r
+    if out_stats is not None:
+        o_ld = _stats_ld(out_stats, M, "out")
+    args = (x.data_ptr(), lda, w.data_ptr(), K, out.data_ptr(), N, _ptr(bias), _ptr(residual), ldr, M, N, K, 1.0,
+            ACT_CODE[act], mode, _ptr(a_st), a_ld, _ptr(a_cs), _ptr(a_b), _ptr(r_st), r_ld, _ptr(r_g), _ptr(r_b),
+            _ptr(out_stats), o_ld, float(a_inv), float(r_inv), float(eps))
+    fn = _ops().gemm_tn_ln
+    if tile_cfg < 0:
+        key = ("gemm_ln", x.dtype, M, N, K, lda, act, mode)
+        tuned = key in _TUNE
+        tile_cfg = _tuned_cfg(key, lambda c: fn(*args, _stream(), c))
+        if not tuned and out_stats is not None and not torch.cuda.is_current_stream_capturing():
+            out_stats.zero_()        # the tuning launches accumulated into it
+    fn(*args, _stream(), int(tile_cfg))
+    return out
+
+
+def fold_ln_weights(w: torch.Tensor, b: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor):
+    """(w', colsum, bias_f32) for ``linear_ln(lna=...)``: LN(x) @ w.T + b ==
+    rstd * (x @ w'.T - mean * colsum) + bias_f32 with w' = w * gamma."""
+    wf = w.float()
+    w2 = (wf * gamma.float()[None, :]).to(w.dtype).contiguous()
+    return w2, w2.float().sum(1).contiguous(), (b.float() + wf @ beta.float()).contiguous()
+
+
+def linear_ln_ref(x, w, bias=None, act="none", residual=None, ln_x=None, ln_res=None, eps=1e-12):
+    """fp32 reference of linear_ln in terms of the UNFOLDED LayerNorms:
+    act(LN_x(x) @ w.T + bias + LN_res(residual)); ln_* = (gamma, beta) or None."""
+    xf = x.float()
+    if ln_x is not None:
+        xf = F.layer_norm(xf, (xf.shape[-1],), ln_x[0].float(), ln_x[1].float(), eps)
+    y = xf @ w.float().t()
+    if bias is not None:
+        y = y + bias.float()
+    if residual is not None:
+        rf = residual.float()
+        if ln_res is not None:
+            rf = F.layer_norm(rf, (rf.shape[-1],), ln_res[0].float(), ln_res[1].float(), eps)
+        y = y + rf
+    return _act_ref(y, act)
+
+
 def _act_ref(y: torch.Tensor, act: str) -> torch.Tensor:
     if act == "gelu":
         return F.gelu(y)
@@ -275,9 +379,15 @@ def linear_ref(x, w, bias=None, act="none", residual=None, out_dtype=None, alpha
 # Norms
 # ---------------------------------------------------------------------------
 def _norm(x, gamma, beta, eps, residual, residual_out, mode):
-    _check(x.is_cuda and x.is_contiguous() and x.dtype in (torch.bfloat16, torch.float16), "norm: bad x")
+    _check(x.is_cuda and x.dtype in (torch.bfloat16, torch.float16), "norm: bad x")
     D = x.shape[-1]
-    rows = x.numel() // D
+    if x.is_contiguous():
+        rows, ldx = x.numel() // D, D
+    else:
+        # a 2-D row-strided view (e.g. the [CLS] rows): read in place
+        _check(x.dim() == 2 and x.stride(1) == 1 and x.stride(0) % 4 == 0 and _aligned(x, 8)
+               and residual is None, "norm: x must be contiguous or a 2-D row-strided view without residual")
+        rows, ldx = x.shape[0], x.stride(0)
     _check(D % 4 == 0 and D <= 8192, "norm: D must be a multiple of 4, <= 8192")
     _check(gamma.numel() == D and gamma.dtype == x.dtype, "norm: bad gamma")
     if beta is not None:
@@ -286,9 +396,9 @@ def _norm(x, gamma, beta, eps, residual, residual_out, mode):
         _check(residual.shape == x.shape and residual.is_contiguous() and residual.dtype == x.dtype, "norm: bad residual")
     if residual_out is not None:
         _check(residual_out.shape == x.shape and residual_out.is_contiguous(), "norm: bad residual_out")
-    y = torch.empty_like(x)
+    y = torch.empty(x.shape, device=x.device, dtype=x.dtype)
     _ops().norm_fwd(DTYPE_CODE[x.dtype], mode, x.data_ptr(), _ptr(residual), _ptr(residual_out),
-                    gamma.data_ptr(), _ptr(beta), y.data_ptr(), rows, D, float(eps), _stream())
+                    gamma.data_ptr(), _ptr(beta), y.data_ptr(), rows, D, ldx, float(eps), _stream())
     return y
 
 
@@ -311,8 +421,10 @@ def rms_norm_ref(x, gamma, eps=1e-5, residual=None):
     return (xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps) * gamma.float()).to(x.dtype)
 
 
-def embed_ln(ids, word, pos, typ, gamma, beta, eps=1e-12, types=None):
-    """BERT embeddings: LN(word[ids] + pos[t % S] + type[types or 0]); ids [B, S] int32."""
+def embed_ln(ids, word, pos, typ, gamma, beta, eps=1e-12, types=None, zero_stats=None):
+    """BERT embeddings: LN(word[ids] + pos[t % S] + type[types or 0]); ids [B, S] int32.
+    ``zero_stats`` [..., B*S, 2] f32 (contiguous): also zeroed (the deferred-LN
+    row statistics of the folded forward), saving a fill kernel."""
     _check(ids.dtype == torch.int32 and ids.is_contiguous() and ids.dim() == 2, "embed_ln: ids must be [B, S] int32")
     B, S = ids.shape
     D = word.shape[1]
@@ -320,10 +432,15 @@ def embed_ln(ids, word, pos, typ, gamma, beta, eps=1e-12, types=None):
     _check(D % 256 == 0, "embed_ln: hidden size must be a multiple of 256")
     if types is not None:
         _check(types.dtype == torch.int32 and types.shape == ids.shape and types.is_contiguous(), "embed_ln: bad types")
+    zn = 0
+    if zero_stats is not None:
+        _check(zero_stats.dtype == torch.float32 and zero_stats.is_contiguous() and zero_stats.shape[-1] == 2
+               and zero_stats.shape[-2] == B * S, "embed_ln: zero_stats must be [..., B*S, 2] f32")
+        zn = zero_stats.numel() // (2 * B * S)
     y = torch.empty(B * S, D, device=ids.device, dtype=word.dtype)
     _ops().embed_ln_fwd(DTYPE_CODE[word.dtype], ids.data_ptr(), _ptr(types), word.data_ptr(), pos.data_ptr(),
                         typ.data_ptr(), gamma.data_ptr(), beta.data_ptr(), y.data_ptr(), B * S, S, D,
-                        word.shape[0], float(eps), _stream())
+                        word.shape[0], float(eps), _ptr(zero_stats), zn, B * S, _stream())
     return y
 
 

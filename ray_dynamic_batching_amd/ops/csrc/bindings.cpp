@@ -14,11 +14,15 @@ namespace rdb {
 void gemm_tn(int in_dtype, int out_dtype, uintptr_t A, int lda, uintptr_t W, int ldw, uintptr_t C,
              int ldc, uintptr_t bias, uintptr_t R, int ldr, int M, int N, int K, float alpha,
              int act, uintptr_t stream, int force_cfg);
+void gemm_tn_ln(uintptr_t A, int lda, uintptr_t W, int ldw, uintptr_t C, int ldc, uintptr_t bias, uintptr_t R,
+                int ldr, int M, int N, int K, float alpha, int act, int mode, uintptr_t a_stats, int a_ld,
+                uintptr_t a_colsum, uintptr_t a_bias, uintptr_t r_stats, int r_ld, uintptr_t r_g, uintptr_t r_b,
+                uintptr_t o_stats, int o_ld, float a_inv_d, float r_inv_d, float eps, uintptr_t stream, int cfg);
 void norm_fwd(int dtype, int mode, uintptr_t x, uintptr_t res, uintptr_t res_out, uintptr_t gamma,
-              uintptr_t beta, uintptr_t y, int rows, int D, float eps, uintptr_t stream);
+              uintptr_t beta, uintptr_t y, int rows, int D, int ldx, float eps, uintptr_t stream);
 void embed_ln_fwd(int dtype, uintptr_t ids, uintptr_t types, uintptr_t word, uintptr_t pos,
                   uintptr_t typ, uintptr_t gamma, uintptr_t beta, uintptr_t y, int tokens, int S,
-                  int D, int vocab, float eps, uintptr_t stream);
+                  int D, int vocab, float eps, uintptr_t zero_stats, int zn, int zstride, uintptr_t stream);
 void attn_fwd(int dtype, uintptr_t qkv, int ld_qkv, int q_off, int k_off, int v_off, int B, int H, int Hkv,
               int S, int D, uintptr_t lens, int causal, uintptr_t out, int ld_out, float scale,
               uintptr_t stream);
@@ -61,6 +65,7 @@ static void hip_check(hipError_t e, const char* what) {
 PYBIND11_MODULE(_rdb_ops, m) {
   m.doc() = "ray_dynamic_batching_amd gfx950 kernels (MFMA GEMM/conv, norm, attention, ...)";
   m.def("gemm_tn", &rdb::gemm_tn, py::call_guard<py::gil_scoped_release>());
+  m.def("gemm_tn_ln", &rdb::gemm_tn_ln, py::call_guard<py::gil_scoped_release>());
   m.def("norm_fwd", &rdb::norm_fwd, py::call_guard<py::gil_scoped_release>());
   m.def("embed_ln_fwd", &rdb::embed_ln_fwd, py::call_guard<py::gil_scoped_release>());
   m.def("attn_fwd", &rdb::attn_fwd, py::call_guard<py::gil_scoped_release>());

@@ -177,6 +177,33 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, char* lds, uint3
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_ptr_t)lds, 16, off, 0, 0, 0);
 }
 
+// ---- deferred-LayerNorm epilogue operands --------------------------------------
+// A post-LN transformer's LayerNorm can be folded into the GEMMs around it
+// (models/bert.py ``fold_ln``): the producing GEMM accumulates per-row (sum,
+// sum of squares) of the values it stores (STATS), the consuming GEMM multiplies
+// the RAW rows by W' = W * gamma and corrects in its epilogue (LNA):
+//     LN(a) W^T + b = rstd[m] * (a W'^T - mean[m] * colsum(W')[n]) + (b + W beta)[n]
+// and a residual operand that is a normalised row is normalised on load (LNR):
+//     R'[m, n] = (R[m, n] - mean_R[m]) * rstd_R[m] * g[n] + be[n].
+// No LayerNorm kernel runs and the normalised rows are never materialised.
+constexpr int EPI_LNA = 1, EPI_LNR = 2, EPI_STATS = 4;
+struct LnEpi {
+  const float* a_stats;   // LNA: (sum, sumsq) of A's rows, row stride a_ld floats
+  const float* a_colsum;  // LNA: colsum(W') [N]
+  const float* a_bias;    // LNA: b + W beta [N] (f32)
+  const float* r_stats;   // LNR: (sum, sumsq) of R's rows, row stride r_ld floats
+  const void* r_g;        // LNR: gamma, beta [N] (element type T)
+  const void* r_b;
+  float* o_stats;         // STATS: += (sum, sumsq) of the stored rows, row stride o_ld floats
+  int a_ld, r_ld, o_ld;
+  float a_inv_d, r_inv_d, eps;
+};
+
+__device__ __forceinline__ void ln_row_stats(float2 v, float inv_d, float eps, float& mu, float& rstd) {
+  mu = v.x * inv_d;
+  rstd = rsqrtf(fmaxf(v.y * inv_d - mu * mu, 0.f) + eps);
+}
+
 // ---- the kernel ---------------------------------------------------------------
 // 4 waves per block laid out WGM (along M) x 4/WGM (along N).  BN only has to
 // be a multiple of 16 x (4/WGM): the W tile is DMA'd in whole 32-row wave
@@ -189,11 +216,14 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, char* lds, uint3
 // which is what the L2-bandwidth-bound BERT shapes need (FFN2 at 128x48 moves
 // ~14 TB/s through L2 for 0.5 PF).
 template <typename T, typename OutT, int BM, int BN, template <typename, int> class LoaderT, bool HAS_BIAS,
-          bool HAS_RES, int WGM = 2, int NW = 4>
+          bool HAS_RES, int WGM = 2, int NW = 4, int EPI = 0>
 __global__ void __launch_bounds__(64 * NW, NW == 4 ? 2 : 1)
 mfma_gemm_kernel(typename LoaderT<T, 1>::Params ap, const T* __restrict__ W, int ldw,
                  OutT* __restrict__ C, int ldc, const T* __restrict__ bias,
-                 const T* __restrict__ R, int ldr, int M, int N, int K, float alpha, int act) {
+                 const T* __restrict__ R, int ldr, int M, int N, int K, float alpha, int act, LnEpi ln) {
+  constexpr bool LNA = (EPI & EPI_LNA) != 0, LNR = (EPI & EPI_LNR) != 0, OST = (EPI & EPI_STATS) != 0;
+  static_assert(!LNA || !HAS_BIAS, "LNA takes its (folded) bias from ln.a_bias");
+  static_assert(!LNR || HAS_RES, "LNR normalises the residual operand");
   constexpr int BK = 64;
   constexpr int WGN = NW / WGM;
   constexpr int NT = 64 * NW;                 // threads
@@ -281,6 +311,19 @@ mfma_gemm_kernel(typename LoaderT<T, 1>::Params ap, const T* __restrict__ W, int
     }
   };
 
+  // deferred-LN row statistics are fetched before the main loop: their latency
+  // hides under it instead of opening the epilogue
+  float2 ast[LNA ? TM : 1], rst[LNR ? TM : 1];
+  if constexpr (LNA || LNR) {
+#pragma unroll
+    for (int j = 0; j < TM; ++j) {
+      const int m = m0 + wm * WM + j * 16 + fr;
+      const size_t ms = (size_t)(m < M ? m : M - 1);
+      if constexpr (LNA) ast[j] = *reinterpret_cast<const float2*>(ln.a_stats + ms * ln.a_ld);
+      if constexpr (LNR) rst[j] = *reinterpret_cast<const float2*>(ln.r_stats + ms * ln.r_ld);
+    }
+  }
+
   const int nk = (K + BK - 1) / BK;
   if constexpr (kStages == 2) {
     // Two LDS stages: the DMA of tile k+1 runs under the MFMAs of tile k; the
@@ -328,9 +371,25 @@ mfma_gemm_kernel(typename LoaderT<T, 1>::Params ap, const T* __restrict__ W, int
   const bool swiglu = act == ACT_SWIGLU;
   const int n_out = swiglu ? (N >> 1) : N;
   float bv[TN][4];
+  float cs[LNA ? TN : 1][4];
+  u32x2 rg[LNR ? TN : 1], rb[LNR ? TN : 1];
 #pragma unroll
   for (int i = 0; i < TN; ++i) {
     const int n = n0 + wn * WN + i * 16 + fg * 4;
+    if constexpr (LNA) {
+      // N % 4 == 0 in the LN modes (host-checked): n < N covers n..n+3
+      const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+      const f32x4 b4 = n < N ? *reinterpret_cast<const f32x4*>(ln.a_bias + n) : z;
+      const f32x4 c4 = n < N ? *reinterpret_cast<const f32x4*>(ln.a_colsum + n) : z;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) { bv[i][q] = b4[q]; cs[i][q] = c4[q]; }
+      continue;
+    }
+    if constexpr (LNR) {
+      const u32x2 z = {0u, 0u};
+      rg[i] = n < N ? *reinterpret_cast<const u32x2*>(static_cast<const T*>(ln.r_g) + n) : z;
+      rb[i] = n < N ? *reinterpret_cast<const u32x2*>(static_cast<const T*>(ln.r_b) + n) : z;
+    }
     if constexpr (HAS_BIAS) {
       const __amdgpu_buffer_rsrc_t bsrc = make_rsrc(bias, (uint32_t)(N * sizeof(T)));
       const u32x2 raw = bload8(bsrc, (uint32_t)(n * sizeof(T)));
@@ -398,15 +457,34 @@ mfma_gemm_kernel(typename LoaderT<T, 1>::Params ap, const T* __restrict__ W, int
 #pragma unroll
     for (int j = 0; j < TM; ++j) {
       const int m = m0 + wm * WM + j * 16 + fr;
+      float amu = 0.f, ar = 1.f, rmu = 0.f, rr = 1.f, ssum = 0.f, ssq = 0.f;
+      if constexpr (LNA) ln_row_stats(ast[j], ln.a_inv_d, ln.eps, amu, ar);
+      if constexpr (LNR) ln_row_stats(rst[j], ln.r_inv_d, ln.eps, rmu, rr);
 #pragma unroll
       for (int i = 0; i < TN; ++i) {
         const int n = n0 + wn * WN + i * 16 + fg * 4;
         float y[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          float x = alpha * acc[i][j][q] + bv[i][q];
-          if constexpr (HAS_RES) x += rv(j, i, q);
+          float x;
+          if constexpr (LNA) x = alpha * ar * (acc[i][j][q] - amu * cs[i][q]) + bv[i][q];
+          else x = alpha * acc[i][j][q] + bv[i][q];
+          if constexpr (HAS_RES) {
+            float r = rv(j, i, q);
+            if constexpr (LNR) {
+              const T* g = reinterpret_cast<const T*>(&rg[i]);
+              const T* be = reinterpret_cast<const T*>(&rb[i]);
+              r = (r - rmu) * rr * (float)g[q] + (float)be[q];
+            }
+            x += r;
+          }
           y[q] = actf(x);
+          if constexpr (OST) {
+            // statistics of the values as STORED (rounded to OutT), as a
+            // LayerNorm kernel reading this output would see them
+            const float yr = (float)(OutT)y[q];
+            if (n + q < N) { ssum += yr; ssq += yr * yr; }
+          }
         }
         if (m >= M || n >= N) continue;
         OutT* cp = C + (size_t)m * ldc + n;
@@ -416,6 +494,17 @@ mfma_gemm_kernel(typename LoaderT<T, 1>::Params ap, const T* __restrict__ W, int
 #pragma unroll
           for (int e = 0; e < 4; ++e)
             if (n + e < N) cp[e] = (OutT)y[e];
+        }
+      }
+      if constexpr (OST) {
+        // the 4 lanes holding row m (lane, lane^16, ^32, ^48) combine, one adds
+        ssum += __shfl_xor(ssum, 16, 64);
+        ssq += __shfl_xor(ssq, 16, 64);
+        ssum += __shfl_xor(ssum, 32, 64);
+        ssq += __shfl_xor(ssq, 32, 64);
+        if (fg == 0 && m < M) {
+          unsafeAtomicAdd(ln.o_stats + (size_t)m * ln.o_ld, ssum);
+          unsafeAtomicAdd(ln.o_stats + (size_t)m * ln.o_ld + 1, ssq);
         }
       }
     }
@@ -469,50 +558,57 @@ inline int pick_tile_cfg(int M, int N, bool dense) {
 }
 
 template <typename T, typename OutT, template <typename, int> class LoaderT, bool HB, bool HR, int BM, int BN,
-          int WGM = 2, int NW = 4, typename P>
+          int WGM = 2, int NW = 4, int EPI = 0, typename P>
 void launch_one(const P& ap, const T* W, int ldw, OutT* C, int ldc, const T* bias, const T* R, int ldr, int M,
-                int N, int K, float alpha, int act, hipStream_t s) {
+                int N, int K, float alpha, int act, hipStream_t s, const LnEpi& ln = LnEpi{}) {
   const int nwg = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
-  hipLaunchKernelGGL((mfma_gemm_kernel<T, OutT, BM, BN, LoaderT, HB, HR, WGM, NW>), dim3(nwg), dim3(64 * NW), 0, s,
-                     ap, W, ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act);
+  hipLaunchKernelGGL((mfma_gemm_kernel<T, OutT, BM, BN, LoaderT, HB, HR, WGM, NW, EPI>), dim3(nwg), dim3(64 * NW), 0,
+                     s, ap, W, ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act, ln);
 }
 
-template <typename T, typename OutT, template <typename, int> class LoaderT, bool HB, bool HR, typename P>
+template <typename T, typename OutT, template <typename, int> class LoaderT, bool HB, bool HR, int EPI = 0,
+          typename P>
 void launch_mfma_gemm_t(const P& ap, const T* W, int ldw, OutT* C, int ldc, const T* bias, const T* R,
-                        int ldr, int M, int N, int K, float alpha, int act, hipStream_t s, int cfg) {
-#define RDB_TILE(IDX, BM_, BN_, WGM_) \
-  case IDX: launch_one<T, OutT, LoaderT, HB, HR, BM_, BN_, WGM_>(ap, W, ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act, s); break;
+                        int ldr, int M, int N, int K, float alpha, int act, hipStream_t s, int cfg,
+                        const LnEpi& ln = LnEpi{}) {
+#define RDB_TILE(IDX, BM_, BN_, WGM_, NW_)                                                                    \
+  case IDX:                                                                                                  \
+    launch_one<T, OutT, LoaderT, HB, HR, BM_, BN_, WGM_, NW_, EPI>(ap, W, ldw, C, ldc, bias, R, ldr, M, N, K, \
+                                                                  alpha, act, s, ln);                        \
+    return;
   if constexpr (std::is_same<OutT, float>::value) {
     // f32 output is only used by small heads: one tile shape
     launch_one<T, OutT, LoaderT, HB, HR, 64, 64>(ap, W, ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act, s);
   } else {
     switch (cfg) {
-      RDB_TILE(0, 128, 128, 2)
-      RDB_TILE(1, 64, 128, 2)
-      RDB_TILE(2, 128, 64, 2)
-      RDB_TILE(4, 128, 192, 2)
-      RDB_TILE(5, 192, 128, 2)
-      RDB_TILE(6, 256, 128, 2)
-      RDB_TILE(7, 128, 256, 2)
-      RDB_TILE(8, 128, 144, 4)
-      RDB_TILE(9, 64, 96, 2)
-      RDB_TILE(10, 128, 96, 2)
-      RDB_TILE(11, 256, 144, 4)
-      RDB_TILE(12, 128, 48, 4)
-      default:
-        if constexpr (std::is_same<LoaderT<T, 1>, DenseLoader<T, 1>>::value) {
-          // 8-wave big tiles: dense operands only (keeps the conv build small)
-          switch (cfg) {
-            case 13: launch_one<T, OutT, LoaderT, HB, HR, 256, 128, 4, 8>(ap, W, ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act, s); return;
-            case 14: launch_one<T, OutT, LoaderT, HB, HR, 128, 256, 2, 8>(ap, W, ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act, s); return;
-            case 15: launch_one<T, OutT, LoaderT, HB, HR, 256, 192, 4, 8>(ap, W, ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act, s); return;
-            case 16: launch_one<T, OutT, LoaderT, HB, HR, 256, 144, 8, 8>(ap, W, ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act, s); return;
-            case 17: launch_one<T, OutT, LoaderT, HB, HR, 128, 96, 4, 8>(ap, W, ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act, s); return;
-            case 18: launch_one<T, OutT, LoaderT, HB, HR, 256, 96, 8, 8>(ap, W, ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act, s); return;
-            default: break;
-          }
-        } launch_one<T, OutT, LoaderT, HB, HR, 64, 64>(ap, W, ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act, s);
+      RDB_TILE(0, 128, 128, 2, 4)
+      RDB_TILE(1, 64, 128, 2, 4)
+      RDB_TILE(2, 128, 64, 2, 4)
+      RDB_TILE(4, 128, 192, 2, 4)
+      RDB_TILE(5, 192, 128, 2, 4)
+      RDB_TILE(6, 256, 128, 2, 4)
+      RDB_TILE(7, 128, 256, 2, 4)
+      RDB_TILE(8, 128, 144, 4, 4)
+      RDB_TILE(9, 64, 96, 2, 4)
+      RDB_TILE(10, 128, 96, 2, 4)
+      RDB_TILE(11, 256, 144, 4, 4)
+      RDB_TILE(12, 128, 48, 4, 4)
+      default: break;
     }
+    if constexpr (std::is_same<LoaderT<T, 1>, DenseLoader<T, 1>>::value) {
+      // 8-wave big tiles: dense operands only (keeps the conv build small)
+      switch (cfg) {
+        RDB_TILE(13, 256, 128, 4, 8)
+        RDB_TILE(14, 128, 256, 2, 8)
+        RDB_TILE(15, 256, 192, 4, 8)
+        RDB_TILE(16, 256, 144, 8, 8)
+        RDB_TILE(17, 128, 96, 4, 8)
+        RDB_TILE(18, 256, 96, 8, 8)
+        default: break;
+      }
+    }
+    launch_one<T, OutT, LoaderT, HB, HR, 64, 64, 2, 4, EPI>(ap, W, ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act, s,
+                                                           ln);
   }
 #undef RDB_TILE
 }

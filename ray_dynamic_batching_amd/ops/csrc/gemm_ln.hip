@@ -1,0 +1,68 @@
+// Dense bf16 MFMA GEMM with the deferred-LayerNorm epilogues (gemm_core.h
+// LnEpi): the GEMMs of a post-LN transformer layer run with no LayerNorm
+// kernel between them.
+//
+//   mode LNA          y = act(rstd_A[m] (A W'^T - mean_A[m] colsum[n]) + bias'[n])   (W' = W * gamma)
+//   mode STATS        y = A W^T + bias + R,                 stats[m] += (sum y, sum y^2)
+//   mode LNR | STATS  y = A W^T + bias + LN(R) (normalised on load), stats[m] += ...
+//
+// Used by models/bert.py (fold_ln): QKV and FFN-up take LNA, o-proj and
+// FFN-down take (LNR |) STATS.  Reference behaviour being preserved: the
+// BertLayer LayerNorms of the served models.
+#include "gemm_core.h"
+#include <stdexcept>
+
+namespace rdb {
+
+void gemm_tn_ln(uintptr_t A, int lda, uintptr_t W, int ldw, uintptr_t C, int ldc, uintptr_t bias, uintptr_t R,
+                int ldr, int M, int N, int K, float alpha, int act, int mode, uintptr_t a_stats, int a_ld,
+                uintptr_t a_colsum, uintptr_t a_bias, uintptr_t r_stats, int r_ld, uintptr_t r_g, uintptr_t r_b,
+                uintptr_t o_stats, int o_ld, float a_inv_d, float r_inv_d, float eps, uintptr_t stream, int cfg) {
+  if (K % 8 != 0 || lda % 8 != 0 || ldw % 8 != 0) throw std::invalid_argument("gemm_tn_ln: K/lda/ldw % 8");
+  if ((A | W) & 15) throw std::invalid_argument("gemm_tn_ln: A/W must be 16-byte aligned");
+  if (N % 4 != 0 || ldc % 4 != 0) throw std::invalid_argument("gemm_tn_ln: N and ldc must be multiples of 4");
+  if (act == ACT_SWIGLU) throw std::invalid_argument("gemm_tn_ln: no SWIGLU");
+  if (M <= 0 || N <= 0 || K <= 0) return;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  LnEpi ln{};
+  ln.a_stats = reinterpret_cast<const float*>(a_stats);
+  ln.a_colsum = reinterpret_cast<const float*>(a_colsum);
+  ln.a_bias = reinterpret_cast<const float*>(a_bias);
+  ln.r_stats = reinterpret_cast<const float*>(r_stats);
+  ln.r_g = reinterpret_cast<const void*>(r_g);
+  ln.r_b = reinterpret_cast<const void*>(r_b);
+  ln.o_stats = reinterpret_cast<float*>(o_stats);
+  ln.a_ld = a_ld; ln.r_ld = r_ld; ln.o_ld = o_ld;
+  ln.a_inv_d = a_inv_d; ln.r_inv_d = r_inv_d; ln.eps = eps;
+  DenseParams p{reinterpret_cast<const void*>(A), lda, M, K};
+  auto w = reinterpret_cast<const bf16*>(W);
+  auto b = reinterpret_cast<const bf16*>(bias);
+  auto r = reinterpret_cast<const bf16*>(R);
+  auto c = reinterpret_cast<bf16*>(C);
+  if (cfg < 0 || cfg >= kNumTiles) cfg = pick_tile_cfg(M, N, true);
+  auto need = [](bool ok, const char* what) {
+    if (!ok) throw std::invalid_argument(what);
+  };
+  switch (mode) {
+    case EPI_LNA:
+      need(a_stats && a_colsum && a_bias && !bias && !R, "gemm_tn_ln: LNA needs a_stats/a_colsum/a_bias, no bias/R");
+      launch_mfma_gemm_t<bf16, bf16, DenseLoader, false, false, EPI_LNA>(p, w, ldw, c, ldc, b, r, ldr, M, N, K,
+                                                                         alpha, act, s, cfg, ln);
+      break;
+    case EPI_STATS:
+      need(o_stats && bias && R, "gemm_tn_ln: STATS needs o_stats, bias and R");
+      launch_mfma_gemm_t<bf16, bf16, DenseLoader, true, true, EPI_STATS>(p, w, ldw, c, ldc, b, r, ldr, M, N, K,
+                                                                         alpha, act, s, cfg, ln);
+      break;
+    case EPI_LNR | EPI_STATS:
+      need(o_stats && bias && R && r_stats && r_g && r_b, "gemm_tn_ln: LNR|STATS needs o_stats, bias, R, r_*");
+      launch_mfma_gemm_t<bf16, bf16, DenseLoader, true, true, EPI_LNR | EPI_STATS>(p, w, ldw, c, ldc, b, r, ldr, M,
+                                                                                   N, K, alpha, act, s, cfg, ln);
+      break;
+    default:
+      throw std::invalid_argument("gemm_tn_ln: mode must be LNA (1), STATS (4) or LNR|STATS (6)");
+  }
+  RDB_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace rdb

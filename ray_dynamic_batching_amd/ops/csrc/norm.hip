@@ -30,11 +30,11 @@ template <typename T, int MODE, int NV>
 __global__ void __launch_bounds__(256)
 norm_kernel(const T* __restrict__ x, const T* __restrict__ res, T* __restrict__ res_out,
             const T* __restrict__ gamma, const T* __restrict__ beta, T* __restrict__ y,
-            int rows, int D, float eps) {
+            int rows, int D, int ldx, float eps) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
-  const T* xr = x + (size_t)row * D;
+  const T* xr = x + (size_t)row * ldx;  // x may be a row-strided view (e.g. the [CLS] rows)
   float v[NV][4];
   float gv[NV][4], bv[NV][4];
   // gamma/beta are issued with the row loads so their latency overlaps the
@@ -109,10 +109,14 @@ __global__ void __launch_bounds__(256)
 embed_ln_kernel(const int* __restrict__ ids, const int* __restrict__ types,
                 const T* __restrict__ word, const T* __restrict__ pos, const T* __restrict__ typ,
                 const T* __restrict__ gamma, const T* __restrict__ beta, T* __restrict__ y,
-                int tokens, int S, int D, int vocab, float eps) {
+                int tokens, int S, int D, int vocab, float eps, float2* __restrict__ zst, int zn,
+                int zstride) {
   const int lane = threadIdx.x & 63;
   const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (t >= tokens) return;
+  // zero this token's deferred-LayerNorm row statistics of every layer (the
+  // folded forward's accumulators; models/bert.py fold_ln): saves a fill kernel
+  for (int k = lane; k < zn; k += 64) zst[(size_t)k * zstride + t] = float2{0.f, 0.f};
   int id = ids[t];
   id = id < 0 ? 0 : (id >= vocab ? vocab - 1 : id);
   const int tt = types ? types[t] : 0;
@@ -177,13 +181,13 @@ static int norm_nv(int D) {  // smallest instantiated NV covering the row
 
 template <typename T, int MODE>
 static void launch_norm(dim3 grid, hipStream_t s, uintptr_t x, uintptr_t res, uintptr_t res_out,
-                        uintptr_t gamma, uintptr_t beta, uintptr_t y, int rows, int D, float eps) {
+                        uintptr_t gamma, uintptr_t beta, uintptr_t y, int rows, int D, int ldx, float eps) {
   const int nv = norm_nv(D);
 #define RDB_CASE(N)                                                                             \
   if (nv == N) {                                                                                \
     hipLaunchKernelGGL((norm_kernel<T, MODE, N>), grid, dim3(256), 0, s, (const T*)x,          \
                        (const T*)res, (T*)res_out, (const T*)gamma, (const T*)beta, (T*)y, rows, \
-                       D, eps);                                                                 \
+                       D, ldx, eps);                                                            \
     return;                                                                                     \
   }
   RDB_NV_LIST(RDB_CASE)
@@ -193,13 +197,14 @@ static void launch_norm(dim3 grid, hipStream_t s, uintptr_t x, uintptr_t res, ui
 template <typename T>
 static void launch_embed(dim3 grid, hipStream_t s, uintptr_t ids, uintptr_t types, uintptr_t word,
                          uintptr_t pos, uintptr_t typ, uintptr_t gamma, uintptr_t beta, uintptr_t y,
-                         int tokens, int S, int D, int vocab, float eps) {
+                         int tokens, int S, int D, int vocab, float eps, uintptr_t zst, int zn, int zstride) {
   const int nv = D / 256;
 #define RDB_CASE(N)                                                                              \
   if (nv == N) {                                                                                 \
     hipLaunchKernelGGL((embed_ln_kernel<T, N>), grid, dim3(256), 0, s, (const int*)ids,         \
                        (const int*)types, (const T*)word, (const T*)pos, (const T*)typ,          \
-                       (const T*)gamma, (const T*)beta, (T*)y, tokens, S, D, vocab, eps);        \
+                       (const T*)gamma, (const T*)beta, (T*)y, tokens, S, D, vocab, eps,         \
+                       (float2*)zst, zn, zstride);                                              \
     return;                                                                                      \
   }
   RDB_NV_LIST(RDB_CASE)
@@ -207,17 +212,18 @@ static void launch_embed(dim3 grid, hipStream_t s, uintptr_t ids, uintptr_t type
 }
 
 void norm_fwd(int dtype, int mode, uintptr_t x, uintptr_t res, uintptr_t res_out, uintptr_t gamma,
-              uintptr_t beta, uintptr_t y, int rows, int D, float eps, uintptr_t stream) {
+              uintptr_t beta, uintptr_t y, int rows, int D, int ldx, float eps, uintptr_t stream) {
   if (D % 4 != 0 || D <= 0 || D > 8192) throw std::invalid_argument("norm: D must be a multiple of 4, <= 8192");
+  if (ldx < D || ldx % 4 != 0 || (ldx != D && res != 0)) throw std::invalid_argument("norm: bad x row stride");
   if (rows <= 0) return;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   dim3 grid((rows + 3) / 4);
   if (dtype == 0) {
-    if (mode == 0) launch_norm<bf16, 0>(grid, s, x, res, res_out, gamma, beta, y, rows, D, eps);
-    else launch_norm<bf16, 1>(grid, s, x, res, res_out, gamma, beta, y, rows, D, eps);
+    if (mode == 0) launch_norm<bf16, 0>(grid, s, x, res, res_out, gamma, beta, y, rows, D, ldx, eps);
+    else launch_norm<bf16, 1>(grid, s, x, res, res_out, gamma, beta, y, rows, D, ldx, eps);
   } else if (dtype == 1) {
-    if (mode == 0) launch_norm<f16, 0>(grid, s, x, res, res_out, gamma, beta, y, rows, D, eps);
-    else launch_norm<f16, 1>(grid, s, x, res, res_out, gamma, beta, y, rows, D, eps);
+    if (mode == 0) launch_norm<f16, 0>(grid, s, x, res, res_out, gamma, beta, y, rows, D, ldx, eps);
+    else launch_norm<f16, 1>(grid, s, x, res, res_out, gamma, beta, y, rows, D, ldx, eps);
   } else {
     throw std::invalid_argument("norm: dtype must be bf16 or f16");
   }
@@ -226,15 +232,17 @@ void norm_fwd(int dtype, int mode, uintptr_t x, uintptr_t res, uintptr_t res_out
 
 void embed_ln_fwd(int dtype, uintptr_t ids, uintptr_t types, uintptr_t word, uintptr_t pos,
                   uintptr_t typ, uintptr_t gamma, uintptr_t beta, uintptr_t y, int tokens, int S,
-                  int D, int vocab, float eps, uintptr_t stream) {
+                  int D, int vocab, float eps, uintptr_t zero_stats, int zn, int zstride, uintptr_t stream) {
   check_d(D);
+  if (zero_stats && (zn < 0 || zstride < tokens)) throw std::invalid_argument("embed_ln: bad zero_stats layout");
+  if (!zero_stats) zn = 0;
   if (tokens <= 0) return;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   dim3 grid((tokens + 3) / 4);
   if (dtype == 0)
-    launch_embed<bf16>(grid, s, ids, types, word, pos, typ, gamma, beta, y, tokens, S, D, vocab, eps);
+    launch_embed<bf16>(grid, s, ids, types, word, pos, typ, gamma, beta, y, tokens, S, D, vocab, eps, zero_stats, zn, zstride);
   else if (dtype == 1)
-    launch_embed<f16>(grid, s, ids, types, word, pos, typ, gamma, beta, y, tokens, S, D, vocab, eps);
+    launch_embed<f16>(grid, s, ids, types, word, pos, typ, gamma, beta, y, tokens, S, D, vocab, eps, zero_stats, zn, zstride);
   else
     throw std::invalid_argument("embed_ln: dtype must be bf16 or f16");
   RDB_HIP_CHECK(hipGetLastError());

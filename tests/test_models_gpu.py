@@ -22,6 +22,32 @@ def test_bert_hip_matches_torch():
     assert torch.allclose(y, ref, atol=5e-2, rtol=5e-2), (y - ref).abs().max()
 
 
+@pytest.mark.parametrize("cls_only", [True, False])
+def test_bert_folded_layernorm_matches_unfolded(cls_only):
+    """The deferred-LayerNorm forward (ops.linear_ln) == the LayerNorm-kernel
+    forward and the eager torch model, with non-trivial LN gamma/beta."""
+    from ray_dynamic_batching_amd.models.bert import BertConfig, BertForSequenceClassification
+
+    m = BertForSequenceClassification(BertConfig(layers=4), device="cuda", backend="hip", seed=2)
+    g = torch.Generator(device="cpu").manual_seed(5)
+    for L in m.layers:
+        for k in ("ln1_g", "ln2_g"):
+            L[k].copy_(1 + 0.2 * torch.randn(L[k].shape, generator=g))
+        for k in ("ln1_b", "ln2_b"):
+            L[k].copy_(0.1 * torch.randn(L[k].shape, generator=g))
+    m.cls_only_last_layer = cls_only
+    ids = m.example_input(16, seed=4)
+    ids[5, 60:] = 0
+    m.fold_ln = True
+    y = m(ids)
+    m.fold_ln = False
+    y_unfolded = m(ids)
+    m.backend = "torch"
+    ref = m(ids)
+    assert torch.allclose(y, y_unfolded, atol=3e-2, rtol=3e-2), (y - y_unfolded).abs().max()
+    assert torch.allclose(y, ref, atol=5e-2, rtol=5e-2), (y - ref).abs().max()
+
+
 def test_engine_serves_bert_tiny_correctly():
     from ray_dynamic_batching_amd.models.bert import BertConfig, BertForSequenceClassification
     from ray_dynamic_batching_amd.runtime import job as rjob

@@ -309,3 +309,68 @@ def test_seq_lens():
     ids[5, :] = 0
     ids[7, 1:] = 0
     assert torch.equal(ops.seq_lens(ids), ops.seq_lens_ref(ids))
+
+
+def _ln_stats(x):
+    xf = x.float()
+    return torch.stack([xf.sum(1), (xf * xf).sum(1)], 1).contiguous()
+
+
+@pytest.mark.parametrize("M,N,K", [(4096, 3072, 768), (4096, 2304, 768), (300, 768, 768)])
+@pytest.mark.parametrize("act", ["none", "gelu"])
+def test_linear_ln_lna_matches_layernorm_then_gemm(M, N, K, act):
+    """LNA: raw rows + folded gamma/beta == LayerNorm(x) @ W.T + b (fp32 reference)."""
+    ops = _ops()
+    torch.manual_seed(0)
+    x = (torch.randn(M, K, device="cuda") * 1.5 + 0.3).to(torch.bfloat16)
+    w = (torch.randn(N, K, device="cuda") * K ** -0.5).to(torch.bfloat16)
+    b = (torch.randn(N, device="cuda") * 0.1).to(torch.bfloat16)
+    g = (1 + 0.2 * torch.randn(K, device="cuda")).to(torch.bfloat16)
+    be = (0.1 * torch.randn(K, device="cuda")).to(torch.bfloat16)
+    w2, cs, b2 = ops.fold_ln_weights(w, b, g, be)
+    y = ops.linear_ln(x, w2, act=act, lna=(_ln_stats(x), cs, b2, K, 1e-12))
+    _close(y, ops.linear_ln_ref(x, w, b, act=act, ln_x=(g, be)), 3e-2, 3e-2)
+
+
+@pytest.mark.parametrize("cfg", list(range(19)))
+def test_linear_ln_stats_and_lnr_all_tiles(cfg):
+    """LNR|STATS on every tile: the residual is normalised on load and the row
+    statistics of the stored output match a torch reduction of it."""
+    ops = _ops()
+    torch.manual_seed(cfg)
+    M, N, K = 520, 768, 384
+    x = torch.randn(M, K, device="cuda").to(torch.bfloat16)
+    w = (torch.randn(N, K, device="cuda") * K ** -0.5).to(torch.bfloat16)
+    b = (torch.randn(N, device="cuda") * 0.1).to(torch.bfloat16)
+    r = (torch.randn(M, N, device="cuda") * 2 - 0.5).to(torch.bfloat16)
+    g = (1 + 0.2 * torch.randn(N, device="cuda")).to(torch.bfloat16)
+    be = (0.1 * torch.randn(N, device="cuda")).to(torch.bfloat16)
+    st = torch.zeros(M, 2, device="cuda")
+    y = ops.linear_ln(x, w, b, residual=r, lnr=(_ln_stats(r), g, be, N, 1e-12), out_stats=st, tile_cfg=cfg)
+    _close(y, ops.linear_ln_ref(x, w, b, residual=r, ln_res=(g, be)), 3e-2, 3e-2)
+    ref = _ln_stats(y)
+    assert torch.allclose(st, ref, rtol=1e-4, atol=1e-2), (st - ref).abs().max()
+    # plain-residual STATS mode (first layer of the stack)
+    st2 = torch.zeros(M, 2, device="cuda")
+    y2 = ops.linear_ln(x, w, b, residual=r, out_stats=st2, tile_cfg=cfg)
+    _close(y2, ops.linear_ref(x, w, b, residual=r), 3e-2, 3e-2)
+    assert torch.allclose(st2, _ln_stats(y2), rtol=1e-4, atol=1e-2)
+
+
+def test_layer_norm_row_strided_view_and_embed_zeroes_stats():
+    ops = _ops()
+    torch.manual_seed(1)
+    B, S, D = 6, 16, 768
+    h = torch.randn(B * S, D, device="cuda", dtype=torch.bfloat16)
+    g = (1 + 0.1 * torch.randn(D, device="cuda")).to(torch.bfloat16)
+    b = (0.1 * torch.randn(D, device="cuda")).to(torch.bfloat16)
+    cls = h.view(B, S, D)[:, 0, :]
+    _close(ops.layer_norm(cls, g, b), ops.layer_norm_ref(cls.contiguous(), g, b), 2e-2, 2e-2)
+    ids = torch.randint(1, 1000, (B, S), device="cuda", dtype=torch.int32)
+    word = torch.randn(1000, D, device="cuda", dtype=torch.bfloat16)
+    pos = torch.randn(S, D, device="cuda", dtype=torch.bfloat16)
+    typ = torch.randn(2, D, device="cuda", dtype=torch.bfloat16)
+    st = torch.full((3, 2, B * S, 2), 7.0, device="cuda")
+    y = ops.embed_ln(ids, word, pos, typ, g, b, zero_stats=st)
+    _close(y, ops.embed_ln_ref(ids, word, pos, typ, g, b), 2e-2, 2e-2)
+    assert st.abs().max().item() == 0.0
