@@ -477,6 +477,19 @@ class LoadGen {
     return d;
   }
 
+  // Fold another generator's recorded latencies into this one (several
+  // generator threads, each with its own Client / completion ring, drive one
+  // node-wide measurement: bench.py at 4+ GPUs).  Call after both runs ended.
+  void merge_from(const LoadGen& o) {
+    hist_.count.fetch_add(o.hist_.count.load());
+    hist_.sum_ns.fetch_add(o.hist_.sum_ns.load());
+    uint64_t m = hist_.max_ns.load();
+    const uint64_t om = o.hist_.max_ns.load();
+    if (om > m) hist_.max_ns.store(om);
+    for (int i = 0; i < kHistBuckets; ++i) hist_.buckets[i].fetch_add(o.hist_.buckets[i].load());
+  }
+  py::dict latency() const { return hist_dict(hist_); }
+
  private:
   Client& c_;
   uint32_t model_;
@@ -800,7 +813,9 @@ PYBIND11_MODULE(_rdb_runtime, m) {
       .def(py::init<Client&, uint32_t, std::vector<std::string>>(), py::keep_alive<1, 2>())
       .def("run", &LoadGen::run, py::arg("total"), py::arg("concurrency") = 64,
            py::arg("rate") = 0.0, py::arg("deadline_ms") = 0.0, py::arg("record") = true,
-           py::arg("timeout_s") = 600.0);
+           py::arg("timeout_s") = 600.0)
+      .def("merge_from", &LoadGen::merge_from)
+      .def("latency", &LoadGen::latency);
 
   py::class_<Consumer>(m, "Consumer")
       .def(py::init<JobHandle&, std::vector<uint32_t>>(), py::keep_alive<1, 2>())
