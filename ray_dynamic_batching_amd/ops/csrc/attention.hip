@@ -103,10 +103,26 @@ attn_fwd_kernel(const T* __restrict__ qkv, int ld_qkv, int q_off, int k_off, int
       *reinterpret_cast<u32x4*>(Ks + kswz<C::CPR>(row, c)) = kreg[j];
     }
 #pragma unroll
-    for (int j = 0; j < NCH; ++j) {   // V transposed: lanes of a wave take consecutive keys
+    for (int j = 0; j < NCH; ++j) {
+      // V transposed: lanes of a wave take consecutive keys, so lanes 2p / 2p+1
+      // hold keys (k, k+1).  They swap half their 8 d-values, then each writes
+      // 4 key PAIRS as dwords (the even lane d 0..3, the odd lane d 4..7): 4
+      // ds_write_b32 instead of 8 ds_write_b16, and every 32-lane group hits
+      // 32 distinct banks (VT_LD = KB + 8 puts d-row +4 at bank offset 16).
       const int qd = tid + 256 * (part * NCH + j), row = qd & (KB - 1), c = qd / KB;
+      const u32x4 mine = __builtin_bit_cast(u32x4, vreg[j]);
+      const bool odd = row & 1;
+      const uint32_t s0 = odd ? mine[0] : mine[2], s1 = odd ? mine[1] : mine[3];
+      const uint32_t r0 = __shfl_xor(s0, 1, 64), r1 = __shfl_xor(s1, 1, 64);
+      const uint32_t m0 = odd ? mine[2] : mine[0], m1 = odd ? mine[3] : mine[1];  // my d-values to write
+      const uint32_t mv[4] = {m0 & 0xffffu, m0 >> 16, m1 & 0xffffu, m1 >> 16};
+      const uint32_t pv[4] = {r0 & 0xffffu, r0 >> 16, r1 & 0xffffu, r1 >> 16};
+      const int d0 = c * 8 + (odd ? 4 : 0), k0 = row & ~1;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) Vt[(c * 8 + e) * C::VT_LD + row] = vreg[j][e];
+      for (int e = 0; e < 4; ++e) {
+        const uint32_t w = odd ? (pv[e] | (mv[e] << 16)) : (mv[e] | (pv[e] << 16));
+        *reinterpret_cast<uint32_t*>(Vt + (d0 + e) * C::VT_LD + k0) = w;
+      }
     }
   };
   load_kv(0, 0);
