@@ -83,9 +83,11 @@ def test_xgmi_local_group_matches_fp32_sum(world, T, D, two_shot):
 
 @pytest.mark.xfail(strict=False, reason=(
     "open issue: run after the test_ops_gpu kernel tests in the same process (not alone, not after "
-    "any subset of them), rank 0's fused-norm output of the FIRST graph replay reads all zeros while "
-    "its all-reduced sum is bit-exact; a preallocated output behaves the same. Eager calls, the "
-    "two-process IPC path and the TP Llama equivalence test are unaffected. Diagnosis in progress."))
+    "any subset of them), rank 0's fused-norm output of the FIRST graph replay is mostly never written "
+    "(a 7.0 sentinel survives in every row except rows = 1, 2 mod 8, which hold wrong values) while its "
+    "all-reduced sum in the uncached gather buffer is bit-exact; an agent-scope release fence after the "
+    "norm stores did not change it. Eager calls, the two-process IPC path and the TP Llama equivalence "
+    "test are unaffected."))
 @pytest.mark.parametrize("prealloc", [False, True])
 def test_xgmi_local_group_graph_replay(prealloc):
     """The kernel keeps its epochs in device memory, so a captured call
@@ -99,7 +101,7 @@ def test_xgmi_local_group_graph_replay(prealloc):
     dx = [x.cuda() for x in xs]
     dg = gamma.cuda()
     outs, graphs = [None] * world, []
-    nouts = [torch.empty_like(d) if prealloc else None for d in dx]
+    nouts = [torch.full_like(d, 7.0) if prealloc else None for d in dx]   # sentinel: tells "never written"
     try:
         for r in range(world):
             g = torch.cuda.CUDAGraph()
@@ -126,7 +128,9 @@ def test_xgmi_local_group_graph_replay(prealloc):
                 if bad.any():
                     rows = bad.nonzero().flatten().tolist()
                     prev = _reference(_inputs(world, T, D, seed=99 + it)[0], gamma, eps)[1].float() if it else None
-                    diag = dict(it=it, rank=r, rows=rows, zero_rows=[i for i in rows if h[i].abs().max() == 0],
+                    diag = dict(it=it, rank=r, n_rows=len(rows), first=rows[:4], zero_rows=[i for i in rows if h[i].abs().max() == 0],
+                                sentinel_rows=[i for i in rows if bool((h[i] == 7.0).all())],
+                                nan_rows=[i for i in rows if bool(h[i].isnan().any())],
                                 stale_rows=[i for i in rows if prev is not None and torch.equal(h[i], prev[i])],
                                 calls=comms[r].calls)
                     raise AssertionError(f"fused norm mismatch: {diag}")
