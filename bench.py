@@ -242,6 +242,8 @@ def main():
         if args.json_out:
             with open(args.json_out, "w") as f:
                 json.dump(line, f, indent=1)
+    if rank == 0:
+        pool.shutdown()
     runner.stop()
     barrier()
     job.close()
