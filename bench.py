@@ -53,6 +53,9 @@ def parse():
     ap.add_argument("--ingress-threads", type=int, default=0,
                     help="load-generator threads on rank 0, each with its own client / completion ring "
                          "(0 = one per 2 GPUs, at most 4)")
+    ap.add_argument("--rehearse-one-gpu", action="store_true",
+                    help="rehearsal only: every rank's replica on cuda:0, gloo instead of RCCL (a 1-GPU box "
+                         "running the N-rank protocol with real engines); never a measurement")
     ap.add_argument("--json-out", default="")
     ap.add_argument("--trace-out", default="", help="write a Chrome trace of the replicas' batches")
     return ap.parse_args()
@@ -86,6 +89,9 @@ def main():
     if echo:
         if world > 1:
             dist.init_process_group("gloo")
+    elif world > 1 and args.rehearse_one_gpu:
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo")
     elif world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -103,7 +109,7 @@ def main():
     # Host-side rendezvous runs over a gloo group: an RCCL barrier would leave a
     # spinning all-reduce kernel on ranks 1..N-1 (occupying CUs their replica
     # engine serves on) for the whole timed region, while rank 0 drives load.
-    host_pg = dist.new_group(backend="gloo") if (world > 1 and not echo) else None
+    host_pg = dist.new_group(backend="gloo") if (world > 1 and not echo and not args.rehearse_one_gpu) else None
 
     def barrier():
         if world > 1:
@@ -236,6 +242,9 @@ def main():
             "per_replica_requests": [r["batch_items"] for r in rep],
             "ingress_threads": G,
         }
+        if args.rehearse_one_gpu:
+            line["metric"] = "REHEARSAL (all ranks on one GPU, gloo): " + METRIC
+            line["vs_baseline"] = None
         if err:
             line["engine_error"] = err
         print(json.dumps(line), flush=True)
