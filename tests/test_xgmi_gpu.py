@@ -86,7 +86,8 @@ def test_xgmi_local_group_matches_fp32_sum(world, T, D, two_shot):
     "any subset of them), rank 0's fused-norm output of the FIRST graph replay is mostly never written "
     "(a 7.0 sentinel survives in every row except rows = 1, 2 mod 8, which hold wrong values) while its "
     "all-reduced sum in the uncached gather buffer is bit-exact; an agent-scope release fence after the "
-    "norm stores did not change it. Eager calls, the two-process IPC path and the TP Llama equivalence "
+    "norm stores did not change it (nor a system-scope one); device printf confirms the replayed kernel "
+    "runs with the right output pointer. Eager calls, the two-process IPC path and the TP Llama equivalence "
     "test are unaffected."))
 @pytest.mark.parametrize("prealloc", [False, True])
 def test_xgmi_local_group_graph_replay(prealloc):
