@@ -15,6 +15,7 @@ from __future__ import annotations
 import argparse
 import concurrent.futures as cf
 import os
+import re
 import shutil
 import subprocess
 import sys
@@ -55,6 +56,26 @@ def _deps(srcs: list[Path], extra_dirs: list[Path]) -> list[Path]:
     return deps
 
 
+_INC = re.compile(r'^\s*#\s*include\s+"([^"]+)"', re.M)
+
+
+def _local_includes(src: Path, seen: set | None = None) -> list[Path]:
+    """Transitive quoted includes of ``src`` that resolve inside the source
+    trees: an object is rebuilt only when a header it actually includes changed."""
+    seen = set() if seen is None else seen
+    out = []
+    for name in _INC.findall(src.read_text(errors="ignore")):
+        for base in (src.parent, OPS_SRC, RT_SRC):
+            p = (base / name).resolve()
+            if p.exists():
+                if p not in seen:
+                    seen.add(p)
+                    out.append(p)
+                    out += _local_includes(p, seen)
+                break
+    return out
+
+
 def _stale(target: Path, deps: list[Path]) -> bool:
     if not target.exists():
         return True
@@ -86,11 +107,11 @@ def build_ops(force: bool = False, jobs: int | None = None, verbose: bool = Fals
               f"-I{OPS_SRC}", f"-I{RT_SRC}"] + _pybind_includes()
     objs = []
     cmds = []
-    hdr_mtime = max((h.stat().st_mtime for d in (OPS_SRC, RT_SRC) for h in d.glob("*.h")), default=0.0)
     for s in srcs:
         o = BUILD / (s.name + ".o")
         objs.append(o)
-        if not force and o.exists() and o.stat().st_mtime >= max(s.stat().st_mtime, hdr_mtime):
+        newest = max(p.stat().st_mtime for p in [s] + _local_includes(s))
+        if not force and o.exists() and o.stat().st_mtime >= newest:
             continue  # object up to date
         lang = ["-x", "hip"] if s.suffix == ".hip" else []
         cmds.append([cc] + common + lang + ["-c", str(s), "-o", str(o)])

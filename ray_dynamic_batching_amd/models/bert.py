@@ -135,8 +135,19 @@ class BertForSequenceClassification:
         """Recompute the LayerNorm-folded weights (call after changing weights)."""
         self._folded = None
 
+    def _fold_key(self):
+        """Identity + in-place version of every tensor the folded weights derive
+        from: a weight swapped or modified after a warm-up forward re-folds."""
+        return tuple((t.data_ptr(), t._version) for L in self.layers
+                     for t in (L["w_qkv"], L["b_qkv"], L["w_i"], L["b_i"], L["ln1_g"], L["ln1_b"],
+                               L["ln2_g"], L["ln2_b"]))
+
     def _folded_weights(self):
+        key = self._fold_key()
+        if self._folded is not None and getattr(self, "_folded_key", None) != key:
+            self._folded = None
         if self._folded is None:
+            self._folded_key = key
             f = []
             for i, L in enumerate(self.layers):
                 d = {}

@@ -48,7 +48,8 @@ size_t xgmi_signal_bytes();
 void xgmi_allreduce(int dtype, const std::vector<uintptr_t>& recv, const std::vector<uintptr_t>& gather,
                     const std::vector<uintptr_t>& sig, int rank, uintptr_t in, uintptr_t out_norm,
                     uintptr_t gamma, float eps, int T, int D, long long slot_elems, int two_shot,
-                    int grid, unsigned long long timeout_ticks, uintptr_t stream);
+                    int grid, unsigned long long timeout_ticks, uintptr_t stream, uintptr_t dbg,
+                    int norm_store);
 uintptr_t xgmi_alloc_uncached(size_t bytes);
 void xgmi_free(uintptr_t p);
 std::string xgmi_ipc_handle(uintptr_t p);
@@ -100,7 +101,11 @@ PYBIND11_MODULE(_rdb_ops, m) {
 
   // Custom all-reduce over xGMI peer memory (xgmi.hip) for TP groups.
   m.def("xgmi_signal_bytes", &rdb::xgmi_signal_bytes);
-  m.def("xgmi_allreduce", &rdb::xgmi_allreduce, py::call_guard<py::gil_scoped_release>());
+  m.def("xgmi_allreduce", &rdb::xgmi_allreduce, py::arg("dtype"), py::arg("recv"), py::arg("gather"),
+        py::arg("sig"), py::arg("rank"), py::arg("in_ptr"), py::arg("out_norm"), py::arg("gamma"), py::arg("eps"),
+        py::arg("T"), py::arg("D"), py::arg("slot_elems"), py::arg("two_shot"), py::arg("grid"),
+        py::arg("timeout_ticks"), py::arg("stream"), py::arg("dbg") = 0, py::arg("norm_store") = 0,
+        py::call_guard<py::gil_scoped_release>());
   m.def("xgmi_alloc_uncached", &rdb::xgmi_alloc_uncached);
   m.def("xgmi_free", &rdb::xgmi_free);
   m.def("xgmi_ipc_handle", [](uintptr_t p) { return py::bytes(rdb::xgmi_ipc_handle(p)); });

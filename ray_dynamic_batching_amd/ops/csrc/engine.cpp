@@ -284,6 +284,7 @@ class Engine {
     d["padded"] = padded_.load();
     d["gpu_busy_ms"] = gpu_busy_ms_.load();
     d["backfill_batches"] = backfills_.load();
+    d["completions_dropped"] = cmp_dropped_.load();
     d["error"] = error();
     return d;
   }
@@ -392,10 +393,17 @@ class Engine {
                         uint32_t len, int64_t t_done) {
     Ring c = job_.cmp_ring(req->client);
     uint64_t pos;
-    SlotHeader* s;
-    while ((s = c.reserve(&pos)) == nullptr) {
-      if (!running_ && job_.hdr()->shutdown.load()) return;
-      cpu_relax();
+    // Bounded: a client whose ring stays full (crashed / wedged proxy) is marked
+    // stalled and loses this completion instead of stalling every other client.
+    SlotHeader* s = reserve_completion(job_, req->client, &pos, [this] {
+      return !running_.load(std::memory_order_relaxed) || job_.hdr()->shutdown.load(std::memory_order_relaxed);
+    });
+    QueueState* qs = job_.queue(queue);
+    if (!s) {  // dropped: still leaves the queue's ongoing count
+      qs->errors.fetch_add(1, std::memory_order_relaxed);
+      qs->completed.fetch_add(1, std::memory_order_release);
+      cmp_dropped_.fetch_add(1, std::memory_order_relaxed);
+      return;
     }
     if (len > c.max_payload()) { status = ST_TOO_LARGE; len = 0; }
     s->req_id = req->req_id;
@@ -408,7 +416,6 @@ class Engine {
     s->status = status;
     s->t_aux_ns = t_done;
     if (len) memcpy(c.payload(s), data, len);
-    QueueState* qs = job_.queue(queue);
     const int64_t e2e = t_done - req->t_submit_ns;
     if (status == ST_OK) {
       qs->hist_e2e.record((uint64_t)std::max<int64_t>(0, e2e));
@@ -648,7 +655,7 @@ class Engine {
   std::atomic<bool> running_{false};
   bool stopping_completer_ = false;
   std::string error_;
-  std::atomic<uint64_t> batches_{0}, requests_{0}, dropped_{0}, padded_{0};
+  std::atomic<uint64_t> batches_{0}, requests_{0}, dropped_{0}, padded_{0}, cmp_dropped_{0};
   std::atomic<double> gpu_busy_ms_{0.0};
 };
 

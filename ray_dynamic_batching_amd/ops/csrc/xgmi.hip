@@ -64,6 +64,8 @@ struct XgArgs {
   int world, rank, T, D;
   long long slot_elems;           // elements per receive slot
   unsigned long long timeout_ticks;
+  unsigned long long* dbg;        // optional per-block launch-view record (8 x u64 per block)
+  int norm_store;                 // out_norm stores: 0 plain, 1 nontemporal, 2 sc1 (write-through)
 };
 
 template <typename T> struct Vec8;
@@ -72,6 +74,18 @@ template <> struct Vec8<f16> { typedef f16x8 type; };
 
 __device__ __forceinline__ u32x4 ld16(const char* p) { return *reinterpret_cast<const u32x4*>(p); }
 __device__ __forceinline__ void st16(char* p, u32x4 v) { *reinterpret_cast<u32x4*>(p) = v; }
+// Store of the fused-norm output (mode chosen per call, uniform branch).
+__device__ __forceinline__ void st_norm(char* p, u32x4 v, int mode) {
+  if (mode == 0) {
+    st16(p, v);
+  } else if (mode == 1) {
+    __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(p));
+  } else {
+    uint32_t* q = reinterpret_cast<uint32_t*>(p);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) __hip_atomic_store(q + i, v[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
 
 template <typename T>
 __device__ __forceinline__ void acc8(float (&a)[8], u32x4 raw) {
@@ -164,7 +178,7 @@ __device__ __forceinline__ void norm_row(const XgArgs& a, float (&x)[VPT][8], in
       float y[8];
 #pragma unroll
       for (int e = 0; e < 8; ++e) y[e] = x[v][e] * rstd * g[e];
-      st16(dst + (size_t)idx * 16, pack8<T>(y));
+      st_norm(dst + (size_t)idx * 16, pack8<T>(y), a.norm_store);
     }
   }
 }
@@ -181,6 +195,26 @@ __global__ void __launch_bounds__(kXgThreads) xgmi_allreduce_kernel(XgArgs a) {
   __syncthreads();
   const uint32_t epoch = s_epoch;
   const int par = epoch & 1;
+  if (a.dbg && tid == 0) {  // what this block sees of its launch (kernarg / graph-replay diagnostics)
+    unsigned long long* d = a.dbg + (size_t)blk * 8;
+    d[0] = (unsigned long long)a.out_norm;
+    d[1] = (unsigned long long)a.gamma;
+    d[2] = (unsigned long long)a.in;
+    d[3] = (unsigned long long)a.gather[r];
+    d[4] = (unsigned long long)a.sig[r];
+    d[5] = ((unsigned long long)a.T << 32) | (unsigned)a.D;
+    d[6] = epoch;
+    unsigned xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    d[7] = xcc & 0xf;
+  }
+  // A timed-out barrier still advances this block's epoch (below), so the
+  // rank stays in step with its peers; the sticky error flag poisons the
+  // communicator on the host side (XgmiCommunicator.check()).
+  auto finish = [&]() {
+    __syncthreads();
+    if (tid == 0) __hip_atomic_store(&me->counter[blk], epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  };
   const size_t rowb = (size_t)a.D * sizeof(T);
   const int nvec = a.D / 8;
   const size_t slotb = (size_t)a.slot_elems * sizeof(T);
@@ -208,7 +242,7 @@ __global__ void __launch_bounds__(kXgThreads) xgmi_allreduce_kernel(XgArgs a) {
         }
       }
     }
-    if (!xg_barrier(a, 0, epoch, blk, &s_fail)) return;
+    if (!xg_barrier(a, 0, epoch, blk, &s_fail)) { finish(); return; }
     // ---- B: reduce own chunk, all-gather the reduced rows ----
     const int my_rows = min(C, a.T - r * C);
     for (int l = blk; l < my_rows; l += G) {
@@ -241,7 +275,7 @@ __global__ void __launch_bounds__(kXgThreads) xgmi_allreduce_kernel(XgArgs a) {
         }
       }
     }
-    if (!xg_barrier(a, 1, epoch, blk, &s_fail)) return;
+    if (!xg_barrier(a, 1, epoch, blk, &s_fail)) { finish(); return; }
     // ---- C: RMSNorm over the gathered rows this block's peers pushed ----
     if constexpr (NORM) {
       for (int p = 0; p < N; ++p) {
@@ -278,7 +312,7 @@ __global__ void __launch_bounds__(kXgThreads) xgmi_allreduce_kernel(XgArgs a) {
         }
       }
     }
-    if (!xg_barrier(a, 0, epoch, blk, &s_fail)) return;
+    if (!xg_barrier(a, 0, epoch, blk, &s_fail)) { finish(); return; }
     // ---- B: every rank reduces every row (same order on all ranks) ----
     for (int row = blk; row < a.T; row += G) {
       float acc[VPT][8];
@@ -310,8 +344,7 @@ __global__ void __launch_bounds__(kXgThreads) xgmi_allreduce_kernel(XgArgs a) {
       if constexpr (NORM) norm_row<T, VPT>(a, x, nvec, a.out_norm + off, s_red);
     }
   }
-  __syncthreads();
-  if (tid == 0) __hip_atomic_store(&me->counter[blk], epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  finish();
 }
 
 template <typename T, int VPT>
@@ -340,7 +373,8 @@ size_t xgmi_signal_bytes() { return sizeof(XgSignal); }
 void xgmi_allreduce(int dtype, const std::vector<uintptr_t>& recv, const std::vector<uintptr_t>& gather,
                     const std::vector<uintptr_t>& sig, int rank, uintptr_t in, uintptr_t out_norm,
                     uintptr_t gamma, float eps, int T, int D, long long slot_elems, int two_shot,
-                    int grid, unsigned long long timeout_ticks, uintptr_t stream) {
+                    int grid, unsigned long long timeout_ticks, uintptr_t stream, uintptr_t dbg,
+                    int norm_store) {
   const int N = (int)recv.size();
   if (N < 1 || N > kXgMaxRanks || (int)gather.size() != N || (int)sig.size() != N)
     throw std::invalid_argument("xgmi_allreduce: 1..8 ranks with one recv/gather/signal buffer each");
@@ -369,6 +403,9 @@ void xgmi_allreduce(int dtype, const std::vector<uintptr_t>& recv, const std::ve
   a.D = D;
   a.slot_elems = slot_elems;
   a.timeout_ticks = timeout_ticks;
+  a.dbg = reinterpret_cast<unsigned long long*>(dbg);
+  if (norm_store < 0 || norm_store > 2) throw std::invalid_argument("xgmi_allreduce: norm_store 0..2");
+  a.norm_store = norm_store;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const bool norm = out_norm != 0;
   if (dtype == 0) launch_t<bf16>(a, two_shot != 0, norm, grid, s);

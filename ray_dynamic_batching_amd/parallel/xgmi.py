@@ -90,6 +90,18 @@ class XgmiCommunicator:
         self._opened = list(opened)
         self._owns = owns
         self.calls = 0
+        self.poisoned = False
+        # Store flavour of the fused-norm output: 0 plain, 1 nontemporal, 2 write-through (sc1).
+        # Write-through is the default: with plain (L2 write-back) stores a graph-replayed call
+        # left most of its norm rows unwritten as seen by a following device->host copy, on
+        # every XCD, while the bit-exact sum (uncached gather buffer) was fine; nontemporal
+        # stores failed the same way; write-through fixed it (tools/gpu_xgmi_diag.sh, the
+        # per-block launch records show every block ran with the right pointers).  The
+        # write-through store costs the same as a plain 16-B store (MI355X_MICROARCH.md).
+        import os
+
+        self.norm_store = int(os.environ.get("RDB_XGMI_NORM_STORE", "2"))
+        self.debug_ptr = 0          # set by enable_debug(): per-block launch-view records
 
     # -- construction ---------------------------------------------------------
     @staticmethod
@@ -150,6 +162,8 @@ class XgmiCommunicator:
 
     def _launch(self, x: torch.Tensor, gamma: Optional[torch.Tensor], eps: float,
                 norm_out: Optional[torch.Tensor], two_shot: Optional[bool]) -> None:
+        if self.poisoned:
+            raise RuntimeError("xgmi: communicator poisoned by an earlier barrier timeout; rebuild the group")
         if x.dtype != self.dtype or not x.is_cuda or not x.is_contiguous() or x.dim() != 2:
             raise ValueError("xgmi: x must be a contiguous 2-D tensor of the communicator dtype on the GPU")
         T, D = x.shape
@@ -163,7 +177,8 @@ class XgmiCommunicator:
         _ops().xgmi_allreduce(_DT[self.dtype], self.recv, self.gather, self.sig, self.rank, x.data_ptr(),
                               norm_out.data_ptr() if norm_out is not None else 0,
                               gamma.data_ptr() if gamma is not None else 0, float(eps), T, D, self.slot_elems,
-                              int(two_shot), grid, self.timeout_ticks, _stream())
+                              int(two_shot), grid, self.timeout_ticks, _stream(), self.debug_ptr,
+                              self.norm_store)
         self.calls += 1
 
     def all_reduce(self, x: torch.Tensor, two_shot: Optional[bool] = None) -> torch.Tensor:
@@ -187,8 +202,38 @@ class XgmiCommunicator:
         """Nonzero when a barrier of this rank timed out (a peer never arrived)."""
         return _ops().xgmi_read_error(self.mine.sig)
 
+    def check(self) -> None:
+        """Raise (and poison the communicator) if any barrier of this rank timed
+        out.  A timed-out call returned partial sums; the kernel still advanced
+        its epochs so the protocol stays in step, but the results of that call
+        (and of the captured graph replay it was part of) are garbage.
+        Synchronises with the device (reads the signal block)."""
+        if self.poisoned:
+            raise RuntimeError("xgmi: communicator poisoned by an earlier barrier timeout")
+        e = self.error()
+        if e:
+            self.poisoned = True
+            raise RuntimeError(f"xgmi: barrier {'A' if e == 1 else 'B'} timed out on rank {self.rank} "
+                               f"(a peer never arrived); communicator poisoned")
+
+    def enable_debug(self, max_blocks: int = 256) -> None:
+        """Every later launch records, per block, the pointers / shape / epoch /
+        XCC id it actually ran with (``debug_records``)."""
+        if not self.debug_ptr:
+            self._dbg_bytes = max_blocks * 64
+            self.debug_ptr = _ops().xgmi_alloc_uncached(self._dbg_bytes)
+
+    def debug_records(self, blocks: int) -> List[Tuple[int, ...]]:
+        if not self.debug_ptr:
+            return []
+        t = torch.as_tensor(_PtrArray(self.debug_ptr, (blocks * 8,), "<i8"), device=self.device).cpu()
+        return [tuple(int(v) for v in t[b * 8:(b + 1) * 8]) for b in range(blocks)]
+
     def close(self) -> None:
         o = _ops()
+        if self.debug_ptr:
+            o.xgmi_free(self.debug_ptr)
+            self.debug_ptr = 0
         for p in self._opened:
             o.xgmi_ipc_close(p)
         self._opened = []

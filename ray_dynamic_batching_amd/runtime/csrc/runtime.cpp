@@ -219,6 +219,11 @@ class JobHandle {
     d["cmp_payload_bytes"] = h->cmp_slot_bytes - (uint32_t)sizeof(SlotHeader);
     d["total_bytes"] = h->total_bytes;
     d["clients_registered"] = h->clients_registered.load();
+    d["completions_dropped"] = h->cmp_dropped.load();
+    py::list stalled;
+    for (uint32_t c = 0; c < std::min<uint32_t>(h->n_clients, kMaxClientFlags); ++c)
+      if (h->client_stalled[c].load()) stalled.append(c);
+    d["stalled_clients"] = stalled;
     return d;
   }
   uintptr_t base() { return reinterpret_cast<uintptr_t>(job_.base()); }
@@ -339,6 +344,7 @@ class Client {
   template <typename F>
   size_t poll_into(size_t max_n, int64_t timeout_ns, F&& fn) {
     size_t n = 0;
+    clear_client_stalled(job_, (uint32_t)id_);  // polling = alive: producers may block on us again
     if (!cmp_.peek(cmp_pos_)) {
       if (timeout_ns == 0 || !cmp_.wait_for(cmp_pos_, timeout_ns, 200)) return 0;
     }
@@ -552,10 +558,13 @@ class EchoServer {
       for (SlotHeader* s : batch) {
         Ring c = job_.cmp_ring(s->client);
         uint64_t cpos;
-        SlotHeader* o;
-        while ((o = c.reserve(&cpos)) == nullptr) {
+        SlotHeader* o = reserve_completion(job_, s->client, &cpos,
+                                           [this] { return stop_.load() || job_.hdr()->shutdown.load(); });
+        if (!o) {
           if (stop_.load() || job_.hdr()->shutdown.load()) return;
-          std::this_thread::yield();
+          qs->completed.fetch_add(1, std::memory_order_relaxed);  // stalled client: dropped
+          qs->errors.fetch_add(1, std::memory_order_relaxed);
+          continue;
         }
         const uint32_t n = std::min<uint32_t>({s->len, out_bytes_, c.max_payload()});
         o->req_id = s->req_id;
@@ -645,10 +654,15 @@ class Consumer {
     {
       py::gil_scoped_release nogil;
       uint64_t pos;
-      SlotHeader* s;
-      while ((s = c.reserve(&pos)) == nullptr) {
+      SlotHeader* s = reserve_completion(job_, client, &pos, [this] { return job_.hdr()->shutdown.load() != 0; });
+      if (!s) {
         if (job_.hdr()->shutdown.load()) return false;
-        usleep(50);
+        if (kind != 2) {  // stalled client: the terminal completion is dropped but leaves the queue
+          QueueState* qs = job_.queue(queue);
+          qs->completed.fetch_add(1, std::memory_order_relaxed);
+          qs->errors.fetch_add(1, std::memory_order_relaxed);
+        }
+        return false;
       }
       s->req_id = req_id;
       s->t_submit_ns = t_submit_ns;

@@ -25,6 +25,7 @@
 #include <cerrno>
 #include <climits>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <ctime>
 #include <fcntl.h>
@@ -40,7 +41,8 @@ namespace rdb {
 namespace rt {
 
 constexpr uint64_t kMagic = 0x3130424F4A424452ULL;  // "RDBJOB01"
-constexpr uint32_t kVersion = 4;
+constexpr uint32_t kVersion = 5;
+constexpr uint32_t kMaxClientFlags = 512;     // clients with a liveness flag (ids beyond share none)
 constexpr uint32_t kTraceCap = 8192;          // trace events per replica (power of two)
 constexpr uint32_t kSnapshotBytes = 1 << 16;  // seqlock-published snapshot (routing table / plan)
 constexpr int kHistSub = 32;       // sub-buckets per power of two (~3% wide)
@@ -379,7 +381,14 @@ struct alignas(4096) JobHeader {
   std::atomic<uint64_t> next_req_id;
   std::atomic<int64_t> created_ns;
   char name[128];
+  // Completion-side liveness: a client whose completion ring stayed full for a
+  // whole completion timeout is marked stalled; producers then drop (and count)
+  // its completions instead of blocking, until the client polls again.  One
+  // wedged proxy can therefore never stall the replica's completer for others.
+  std::atomic<uint64_t> cmp_dropped;
+  std::atomic<uint32_t> client_stalled[kMaxClientFlags];
 };
+static_assert(sizeof(JobHeader) == 4096, "job header must stay one page");
 
 struct JobConfig {
   uint32_t n_replicas = 1, n_queues = 1, n_clients = 8;
@@ -538,6 +547,54 @@ class Job {
   bool unlink_on_close_ = true;
 };
 
+// How long a completion producer waits on a FULL completion ring before it
+// declares that client stalled (RDB_COMPLETION_TIMEOUT_MS, default 2000).
+// Read on the slow path only (a full ring), so tests may change it at run time.
+inline int64_t completion_timeout_ns() {
+  const char* e = getenv("RDB_COMPLETION_TIMEOUT_MS");
+  const long long ms = e ? atoll(e) : 2000;
+  return (int64_t)(ms > 0 ? ms : 2000) * 1000000LL;
+}
+
+inline bool client_stalled(const Job& job, uint32_t client) {
+  return client < kMaxClientFlags && job.hdr()->client_stalled[client].load(std::memory_order_relaxed) != 0;
+}
+// Called by a client whenever it drains its completion ring: it is alive again.
+inline void clear_client_stalled(Job& job, uint32_t client) {
+  if (client < kMaxClientFlags && job.hdr()->client_stalled[client].load(std::memory_order_relaxed))
+    job.hdr()->client_stalled[client].store(0, std::memory_order_relaxed);
+}
+
+// Reserve a slot on `client`'s completion ring.  Waits (spin, then yield /
+// sleep) while the ring is full, but never unboundedly: after `timeout_ns` the
+// client is marked stalled and nullptr is returned (the caller drops that
+// completion and must still account for it).  A client already marked stalled
+// gets exactly one non-blocking attempt per completion.  Also returns nullptr
+// as soon as `abort()` becomes true (replica stopping / job shutdown).
+template <typename Abort>
+inline SlotHeader* reserve_completion(Job& job, uint32_t client, uint64_t* pos, Abort&& abort,
+                                      int64_t timeout_ns = -1) {
+  Ring c = job.cmp_ring(client);
+  if (SlotHeader* s = c.reserve(pos)) return s;
+  if (client_stalled(job, client)) {
+    job.hdr()->cmp_dropped.fetch_add(1, std::memory_order_relaxed);
+    return nullptr;
+  }
+  const int64_t t0 = now_ns();
+  const int64_t limit = timeout_ns >= 0 ? timeout_ns : completion_timeout_ns();
+  for (int i = 0;; ++i) {
+    if (SlotHeader* s = c.reserve(pos)) return s;
+    if (abort()) return nullptr;
+    if (now_ns() - t0 > limit) {
+      if (client < kMaxClientFlags) job.hdr()->client_stalled[client].store(1, std::memory_order_relaxed);
+      job.hdr()->cmp_dropped.fetch_add(1, std::memory_order_relaxed);
+      return nullptr;
+    }
+    if (i < 256) cpu_relax();
+    else usleep(i < 4096 ? 0 : 50);
+  }
+}
+
 // Complete every request still in queue q's ring (unconsumed, or consumed but
 // not yet committed by a replica that died) with `status`, so its clients can
 // retry elsewhere.  Used by the router on drain and by the node agent when a
@@ -550,8 +607,12 @@ inline uint64_t fail_pending(Job& job, uint32_t q, uint32_t status) {
   while (SlotHeader* s = ring.peek(pos)) {
     Ring c = job.cmp_ring(s->client);
     uint64_t cpos;
-    SlotHeader* out = nullptr;
-    while ((out = c.reserve(&cpos)) == nullptr) usleep(100);
+    SlotHeader* out = reserve_completion(job, s->client, &cpos, [] { return false; });
+    if (!out) {  // stalled client: the failure notice is dropped, the request still leaves the queue
+      ++pos;
+      ++n;
+      continue;
+    }
     out->req_id = s->req_id;
     out->t_submit_ns = s->t_submit_ns;
     out->deadline_ns = s->deadline_ns;

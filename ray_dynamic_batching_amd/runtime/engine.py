@@ -95,6 +95,8 @@ class EngineRunner:
                 # LayerNorm kernels already hide under the other stream's GEMMs
                 # (profiles/bert_fold_ln_ab.json)
                 m.fold_ln = self.compute_streams == 1
+            if hasattr(m, "refresh_folded_weights"):
+                m.refresh_folded_weights()   # graphs capture weights derived from the CURRENT ones
             buckets = sorted(set(s.buckets or default_buckets(s.max_batch)))
             if buckets[-1] != s.max_batch:
                 buckets.append(s.max_batch)

@@ -109,6 +109,11 @@ class TPReplica:
         if self.world > 1:
             self.col.broadcast(self.ids[b], 0, self.group)
         self.graphs[b].replay()
+        xg = self.col.get_xgmi(self.group) if self.world > 1 else None
+        if xg is not None:
+            # a timed-out xGMI barrier leaves partial sums in this replay's output:
+            # fail loudly (and poison the communicator) rather than answer with them
+            xg.check()
         if self.rank == 0:
             out = self.out[b][:n].cpu().numpy()
             for r, o in zip(reqs, out):

@@ -112,3 +112,38 @@ def test_seqlock_snapshot_publish_read():
         other.close()
     finally:
         j.close()
+
+
+def test_stalled_client_cannot_wedge_the_replica(monkeypatch):
+    """A client whose completion ring fills (crashed / wedged proxy) is marked
+    stalled after RDB_COMPLETION_TIMEOUT_MS and loses its completions; the
+    replica keeps answering every other client and stops cleanly."""
+    import time
+
+    monkeypatch.setenv("RDB_COMPLETION_TIMEOUT_MS", "100")
+    j = rjob.Job(rjob.unique_job_name("stall"), create=True, n_replicas=1, n_queues=1, n_clients=2,
+                 req_capacity=1024, req_slot_bytes=128, cmp_capacity=16, cmp_slot_bytes=64)
+    j.configure_queue(0, 0, 0, 0, 0.0, True)
+    s = rjob.EchoServer(j, 0, [0], max_batch=4, out_bytes=8)
+    s.start()
+    try:
+        dead, live = rjob.Client(j, 0), rjob.Client(j, 1)
+        for i in range(64):                 # 4x its completion ring; never polled
+            assert dead.submit(0, b"d" * 16) > 0
+        rids = {live.submit(0, bytes([i]) * 16) for i in range(40)}
+        got, t_end = set(), time.time() + 20
+        while len(got) < len(rids) and time.time() < t_end:
+            for rid, st, *_ in live.poll(64, 0.2):
+                assert st == 0
+                got.add(rid)
+        assert got == rids
+        info = j.info()
+        assert info["stalled_clients"] == [0] and info["completions_dropped"] >= 64 - 16
+        assert j.queue_depth(0) == 0       # dropped completions still left the queue
+        dead.poll(64, 0.0)                  # polling clears the stall
+        assert j.info()["stalled_clients"] == []
+    finally:
+        t0 = time.time()
+        s.stop()
+        assert time.time() - t0 < 5
+        j.close()

@@ -1,0 +1,12 @@
+# xGMI graph-replay diagnosis: the order-dependent failure shows only after the
+# ops kernel tests in the same process; run it once per norm-store flavour.
+set -o pipefail
+mkdir -p gpurun_out
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+for m in 0 1 2; do
+  RDB_XGMI_DIAG_FILE=gpurun_out/xgmi_diag.jsonl RDB_XGMI_NORM_STORE=$m timeout -k 10 300 python -u -m pytest tests/test_ops_gpu.py tests/test_xgmi_gpu.py -x -q \
+    --timeout 120 --timeout-method thread -p no:cacheprovider -rxX > gpurun_out/xgmi_diag_$m.log 2>&1
+  rc=$?
+  echo "norm_store=$m rc=$rc"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+done
