@@ -51,7 +51,8 @@ def _aligned(t: torch.Tensor, n: int = 16) -> bool:
 # while a hipGraph is being captured (those calls use the cached choice, or the
 # on-device heuristic if the shape was never seen eagerly).
 # ---------------------------------------------------------------------------
-NUM_TILE_CFGS = 19   # gemm_core.h kTileBM/BN: 0..12 4-wave (GEMM and conv), 13..18 8-wave (GEMM only)
+NUM_TILE_CFGS = 22   # gemm_core.h kTileBM/BN: 0..12 4-wave (GEMM and conv), 13..18 8-wave, 19..21 ping-pong (GEMM only)
+NUM_LN_TILE_CFGS = 19  # the deferred-LayerNorm epilogues run on tiles 0..18
 NUM_CONV_TILE_CFGS = 13
 FORCE_TILED = 99      # tile_cfg value that bypasses the skinny-M GEMM (M <= 64)
 SKINNY_MAX_M = 64
@@ -311,7 +312,7 @@ def linear_ln(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = N
     if tile_cfg < 0:
         key = ("gemm_ln", x.dtype, M, N, K, lda, act, mode)
         tuned = key in _TUNE
-        tile_cfg = _tuned_cfg(key, lambda c: fn(*args, _stream(), c))
+        tile_cfg = _tuned_cfg(key, lambda c: fn(*args, _stream(), c), range(NUM_LN_TILE_CFGS))
         if not tuned and out_stats is not None and not torch.cuda.is_current_stream_capturing():
             out_stats.zero_()        # the tuning launches accumulated into it
     fn(*args, _stream(), int(tile_cfg))

@@ -204,6 +204,88 @@ __device__ __forceinline__ void ln_row_stats(float2 v, float inv_d, float eps, f
   rstd = rsqrtf(fmaxf(v.y * inv_d - mu * mu, 0.f) + eps);
 }
 
+// ---- LDS-staged, row-coalesced epilogue ----------------------------------------
+// The MFMA accumulator layout gives each lane 4 consecutive columns of one row,
+// so a direct store is 8 B per lane and one wave-instruction touches 16 rows x
+// 32 B: the epilogue then runs store-issue bound (measured 6.7k of a 256x128
+// tile's 30k cycles at K = 768, bench/gemm_lab).  Instead every lane parks
+// alpha*acc + bias (f32) in the now idle staging LDS, and the block re-reads it
+// row-major: each lane owns 8 consecutive columns of a row, adds the residual
+// with one 16-B load, applies the activation and writes 16 B -- a wave stores
+// whole 128-B lines.  Tiles taller than the LDS are done in row chunks.
+// Requirements (host/caller-checked): N % 8 == 0, ldc % 8 == 0, C (and R,
+// ldr) 16-B aligned, 2-byte OutT.
+template <int BM, int BN, int SMEM_BYTES>
+struct StagedEpi {
+  static constexpr int ROWB = BN * 4 + 16;                   // f32 row + 16 B (bank rotation)
+  static constexpr int RC_MAX = (SMEM_BYTES / ROWB) / 16 * 16;
+  static constexpr int pick() {
+    int rc = RC_MAX < BM ? RC_MAX : BM;
+    while (rc > 16 && BM % rc) rc -= 16;
+    return rc;
+  }
+  static constexpr int RC = pick();                          // rows per chunk
+  static constexpr int NV = BN / 8;                          // 8-column vectors per row
+  static_assert(BN % 8 == 0 && RC >= 16 && BM % RC == 0, "staged epilogue geometry");
+};
+
+template <typename T, typename OutT, int BM, int BN, int SMEM_BYTES, int NT, int TM, int TN, bool HAS_RES, typename ActF>
+__device__ __forceinline__ void staged_epilogue(char* smem, const f32x4 (&acc)[TN][TM], const float (&bv)[TN][4],
+                                                int row_base, int col_base, int m0, int n0, int M, int N,
+                                                OutT* __restrict__ C, int ldc, const T* __restrict__ R, int ldr,
+                                                float alpha, ActF actf) {
+  typedef StagedEpi<BM, BN, SMEM_BYTES> E;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int fr = lane & 15, fg = lane >> 4;
+#pragma unroll 1
+  for (int c = 0; c < BM / E::RC; ++c) {
+#pragma unroll
+    for (int j = 0; j < TM; ++j) {
+      const int rt = row_base + j * 16 + fr - c * E::RC;    // row inside this chunk
+      if (rt >= 0 && rt < E::RC) {
+#pragma unroll
+        for (int i = 0; i < TN; ++i) {
+          const int nt = col_base + i * 16 + fg * 4;
+          f32x4 v;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) v[q] = alpha * acc[i][j][q] + bv[i][q];
+          *reinterpret_cast<f32x4*>(smem + rt * E::ROWB + nt * 4) = v;
+        }
+      }
+    }
+    __syncthreads();
+#pragma unroll 2
+    for (int idx = tid; idx < E::RC * E::NV; idx += NT) {
+      const int r = idx / E::NV, vcol = idx - r * E::NV;
+      const int m = m0 + c * E::RC + r, n = n0 + vcol * 8;
+      if (m < M && n < N) {
+        const f32x4 a = *reinterpret_cast<const f32x4*>(smem + r * E::ROWB + vcol * 32);
+        const f32x4 b = *reinterpret_cast<const f32x4*>(smem + r * E::ROWB + vcol * 32 + 16);
+        float x[8] = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+        if constexpr (HAS_RES) {
+          const u32x4 raw = *reinterpret_cast<const u32x4*>(R + (size_t)m * ldr + n);
+          const T* e = reinterpret_cast<const T*>(&raw);
+#pragma unroll
+          for (int q = 0; q < 8; ++q) x[q] += (float)e[q];
+        }
+        OutT o[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) o[q] = (OutT)actf(x[q]);
+        *reinterpret_cast<u32x4*>(C + (size_t)m * ldc + n) = *reinterpret_cast<const u32x4*>(o);
+      }
+    }
+    __syncthreads();
+  }
+}
+
+template <typename T, typename OutT, bool HAS_RES>
+__device__ __forceinline__ bool staged_epilogue_ok(int N, const OutT* C, int ldc, const T* R, int ldr) {
+  if constexpr (sizeof(OutT) != 2) return false;
+  bool ok = (N & 7) == 0 && (ldc & 7) == 0 && (reinterpret_cast<uintptr_t>(C) & 15) == 0;
+  if constexpr (HAS_RES) ok = ok && (ldr & 7) == 0 && (reinterpret_cast<uintptr_t>(R) & 15) == 0;
+  return ok;
+}
+
 // ---- the kernel ---------------------------------------------------------------
 // 4 waves per block laid out WGM (along M) x 4/WGM (along N).  BN only has to
 // be a multiple of 16 x (4/WGM): the W tile is DMA'd in whole 32-row wave
@@ -364,6 +446,42 @@ mfma_gemm_kernel(typename LoaderT<T, 1>::Params ap, const T* __restrict__ W, int
     __syncthreads();
   }
 
+  // ---- LDS-staged coalesced epilogue (plain modes; LN / SwiGLU keep the direct one) ----
+  if constexpr (EPI == 0 && sizeof(OutT) == 2) {
+    if (act != ACT_SWIGLU && staged_epilogue_ok<T, OutT, HAS_RES>(N, C, ldc, R, ldr)) {
+      float bv[TN][4];
+#pragma unroll
+      for (int i = 0; i < TN; ++i) {
+        const int n = n0 + wn * WN + i * 16 + fg * 4;
+        if constexpr (HAS_BIAS) {
+          const __amdgpu_buffer_rsrc_t bsrc = make_rsrc(bias, (uint32_t)(N * sizeof(T)));
+          const u32x2 raw = bload8(bsrc, (uint32_t)(n * sizeof(T)));
+          const T* e = reinterpret_cast<const T*>(&raw);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) bv[i][q] = (float)e[q];
+        } else {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) bv[i][q] = 0.f;
+        }
+      }
+      constexpr int SB = kStages * kStage;
+      auto go = [&](auto actf) {
+        staged_epilogue<T, OutT, BM, BN, SB, NT, TM, TN, HAS_RES>(smem, acc, bv, wm * WM, wn * WN, m0, n0, M, N, C,
+                                                                  ldc, R, ldr, alpha, actf);
+      };
+      switch (act) {
+        case ACT_GELU: go([](float x) { return apply_act<ACT_GELU>(x); }); break;
+        case ACT_RELU: go([](float x) { return apply_act<ACT_RELU>(x); }); break;
+        case ACT_TANH: go([](float x) { return apply_act<ACT_TANH>(x); }); break;
+        case ACT_SILU: go([](float x) { return apply_act<ACT_SILU>(x); }); break;
+        case ACT_GELU_TANH: go([](float x) { return apply_act<ACT_GELU_TANH>(x); }); break;
+        case ACT_SIGMOID: go([](float x) { return apply_act<ACT_SIGMOID>(x); }); break;
+        default: go([](float x) { return x; }); break;
+      }
+      return;
+    }
+  }
+
   // ---- fused epilogue: lane holds C[m][n..n+3] ----
   // All bias / residual loads are issued up front as vector buffer loads (OOB ->
   // 0, no per-element branch or wait), then the activation is applied in a loop
@@ -520,6 +638,10 @@ mfma_gemm_kernel(typename LoaderT<T, 1>::Params ap, const T* __restrict__ W, int
   }
 }
 
+}  // namespace rdb
+#include "gemm_pp.h"
+namespace rdb {
+
 // Tile table (index = the `cfg` argument): BM x BN with WGM waves along M.
 // LDS = 2 stages x (BM + BN rounded to 32) x 64 x 2 B.  The host picks the
 // entry (autotuned per shape from Python, or the heuristic below): for the
@@ -527,14 +649,16 @@ mfma_gemm_kernel(typename LoaderT<T, 1>::Params ap, const T* __restrict__ W, int
 // CUs x blocks/CU -- hence the non-power-of-two tiles: 128x192 (N = 3072),
 // 128x144 (N = 2304), 64x96 / 128x48 (N = 768) each give exactly 512 tiles
 // at M = 4096 (BERT-base, batch 32).
-constexpr int kNumTiles = 19;
-//                                 0    1    2    3    4    5    6    7    8    9   10   11   12 | 8-wave tiles: 13   14   15   16   17   18
-constexpr int kTileBM[kNumTiles] = {128, 64, 128, 64, 128, 192, 256, 128, 128, 64, 128, 256, 128, 256, 128, 256, 256, 128, 256};
-constexpr int kTileBN[kNumTiles] = {128, 128, 64, 64, 192, 128, 128, 256, 144, 96, 96, 144, 48, 128, 256, 192, 144, 96, 96};
-constexpr int kTileWGM[kNumTiles] = {2, 2, 2, 2, 2, 2, 2, 2, 4, 2, 2, 4, 4, 4, 2, 4, 8, 4, 8};
-constexpr int kTileNW[kNumTiles] = {4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 8, 8, 8, 8, 8, 8};
+// 19..21 are the ping-pong kernel (gemm_pp.h, 8 waves in two staggered groups).
+constexpr int kNumTiles = 22;
+//                                 0    1    2    3    4    5    6    7    8    9   10   11   12 | 8-wave: 13   14   15   16   17   18 | pp: 19   20   21
+constexpr int kTileBM[kNumTiles] = {128, 64, 128, 64, 128, 192, 256, 128, 128, 64, 128, 256, 128, 256, 128, 256, 256, 128, 256, 256, 256, 128};
+constexpr int kTileBN[kNumTiles] = {128, 128, 64, 64, 192, 128, 128, 256, 144, 96, 96, 144, 48, 128, 256, 192, 144, 96, 96, 128, 144, 256};
+constexpr int kTileWGM[kNumTiles] = {2, 2, 2, 2, 2, 2, 2, 2, 4, 2, 2, 4, 4, 4, 2, 4, 8, 4, 8, 4, 8, 2};
+constexpr int kTileNW[kNumTiles] = {4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 8, 8, 8, 8, 8, 8, 8, 8, 8};
 
 inline int tile_blocks_per_cu(int cfg) {
+  if (cfg >= 19) return 1;
   const int q = 8 * kTileNW[cfg];
   const int bnp = (kTileBN[cfg] + q - 1) / q * q;
   const int lds = 2 * (kTileBM[cfg] + bnp) * 64 * 2;
@@ -545,7 +669,7 @@ constexpr int kNumTiles4 = 13;  // tiles 0..12 are 4-wave (every loader); 13.. a
 inline int pick_tile_cfg(int M, int N, bool dense) {
   int best = 3;
   double best_t = 1e30;
-  for (int c = 0; c < (dense ? kNumTiles : kNumTiles4); ++c) {
+  for (int c = 0; c < (dense ? 19 : kNumTiles4); ++c) {   // the pp tiles (19..) are chosen by tuning only
     const int bm = kTileBM[c], bn = kTileBN[c];
     const long tiles = (long)((M + bm - 1) / bm) * ((N + bn - 1) / bn);
     const long slots = 256L * tile_blocks_per_cu(c);
@@ -605,6 +729,21 @@ void launch_mfma_gemm_t(const P& ap, const T* W, int ldw, OutT* C, int ldc, cons
         RDB_TILE(17, 128, 96, 4, 8)
         RDB_TILE(18, 256, 96, 8, 8)
         default: break;
+      }
+      if constexpr (EPI == 0) {
+        // ping-pong kernel: plain epilogues only (the deferred-LN modes stay on the tiles above)
+        switch (cfg) {
+          case 19: launch_gemm_pp<T, OutT, 8, 256, 128, 2, 2, 3>(static_cast<const T*>(ap.A), ap.lda, W, ldw, C, ldc,
+                                                                  bias, R, ldr, M, N, K, alpha, act, s);
+            return;
+          case 20: launch_gemm_pp<T, OutT, 8, 256, 144, 4, 1, 3>(static_cast<const T*>(ap.A), ap.lda, W, ldw, C, ldc,
+                                                                  bias, R, ldr, M, N, K, alpha, act, s);
+            return;
+          case 21: launch_gemm_pp<T, OutT, 8, 128, 256, 1, 4, 3>(static_cast<const T*>(ap.A), ap.lda, W, ldw, C, ldc,
+                                                                  bias, R, ldr, M, N, K, alpha, act, s);
+            return;
+          default: break;
+        }
       }
     }
     launch_one<T, OutT, LoaderT, HB, HR, 64, 64, 2, 4, EPI>(ap, W, ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act, s,

@@ -1,0 +1,386 @@
+// "Ping-pong" MFMA GEMM for gfx950: the serving GEMMs of BERT / ViT / Llama
+// prefill (M = 1k..8k rows, N, K = 768..4096) at one or two blocks per CU.
+//
+//   C[m, n] = act(alpha * sum_k A[m, k] * W[n, k] + bias[n] + R[m, n])
+//
+// Why a second GEMM body next to gemm_core.h: that kernel reads every K-tile's
+// fragments and runs its MFMAs in the same wave, so a SIMD's matrix pipe idles
+// while its waves wait on LDS reads and barriers (PMC: 14-22 % of the MFMA peak
+// on the BERT shapes).  Here the block's waves form TWO GROUPS that split the
+// tile's rows, and group 1 runs one barrier interval behind group 0
+// (MI355X_MICROARCH.md "Two waves per SIMD": each SIMD alternates one wave in a
+// matrix segment with its partner in a load segment):
+//
+//   interval i   : group 0 = MFMAs of tile k      | group 1 = LDS reads of tile k (+ DMA issue)
+//   interval i+1 : group 0 = reads of tile k+1    | group 1 = MFMAs of tile k
+//
+// Each group owns (BM/2) x BN of the output; its GM x GN waves own
+// (BM/2/GM) x (BN/GN) each.  Staging: both operands by LDS-DMA (buffer_load ...
+// lds, 16 B per lane, source-side XOR swizzle, out-of-range -> 0), STAGES LDS
+// buffers, tile k+STAGES-1 issued during tile k's read interval, retired with a
+// counted vmcnt (never 0 in steady state) and raw s_barrier (no __syncthreads:
+// its fence would drain the DMA).  Hazard bookkeeping (per wave, interval =
+// between two consecutive block barriers):
+//   RAW: every wave retires ITS pieces of tile k+1 at the end of its read
+//        interval of tile k (vmcnt((STAGES-2) * loads)); group 1 does that one
+//        interval later than group 0, i.e. before the barrier after which
+//        group 0 reads tile k+1.
+//   WAR: tile k+STAGES-1 overwrites buffer (k-1) % STAGES; its last reader
+//        (group 1, read interval of tile k-1) drained its ds_reads (lgkmcnt(0))
+//        before the barrier that starts group 0's read interval of tile k, in
+//        which the first overwrite is issued.
+// Both groups execute the same number of s_barrier: group 1 one extra at the
+// start, group 0 one extra at the end.
+#pragma once
+// Included by gemm_core.h (after the shared helpers, before the tile table);
+// not meant to be included on its own.
+
+namespace rdb {
+
+#ifdef RDB_PP_STAMPS
+__device__ unsigned long long* rdb_pp_stamps;
+#endif
+
+template <int NW, int BM, int BN>
+struct PPGeom {
+  static constexpr int BK = 64;
+  static constexpr int NT = 64 * NW;
+  static constexpr int A_PIECES = BM / 8;                    // 1-KiB DMA pieces (8 rows x 128 B)
+  static constexpr int W_PIECES = (BN + 7) / 8;
+  static constexpr int A_PW = A_PIECES / NW;                 // pieces per wave
+  static constexpr int W_PW = (W_PIECES + NW - 1) / NW;      // rounded up: surplus pieces go to a dummy slot
+  static constexpr bool DUMMY = W_PW * NW != W_PIECES;       // (every wave issues the same count: one vmcnt)
+  static constexpr int LOADS = A_PW + W_PW;                  // DMA instructions per wave per tile
+  static constexpr int W_OFF = BM * BK * 2;
+  static constexpr int DUMMY_OFF = W_OFF + W_PIECES * 1024;
+  static constexpr int STAGE_BYTES = DUMMY_OFF + (DUMMY ? 1024 : 0);
+  static_assert(BM % (8 * NW) == 0, "A tile must split into whole pieces per wave");
+};
+
+template <typename T, typename OutT, int NW, int BM, int BN, int GM, int GN, int STAGES, bool HAS_BIAS, bool HAS_RES>
+__global__ void __launch_bounds__(64 * NW, 2)
+gemm_pp_kernel(const T* __restrict__ A, int lda, const T* __restrict__ W, int ldw, OutT* __restrict__ C, int ldc,
+               const T* __restrict__ bias, const T* __restrict__ R, int ldr, int M, int N, int K, float alpha,
+               int act) {
+  typedef PPGeom<NW, BM, BN> G;
+  constexpr int BK = G::BK;
+  constexpr int GW = NW / 2;                 // waves per group
+  static_assert(GM * GN == GW, "group wave layout");
+  constexpr int GBM = BM / 2;                // rows per group
+  constexpr int WM = GBM / GM, WN = BN / GN;
+  constexpr int TM = WM / 16, TN = WN / 16;
+  static_assert(WM % 16 == 0 && WN % 16 == 0, "wave tile must be whole 16x16 fragments");
+  constexpr int L = G::LOADS;
+  static_assert(STAGES >= 3 && (STAGES - 2) * L < 64, "pipeline depth / vmcnt field");
+  typedef typename MfmaOp<T>::frag frag;
+
+  __shared__ __attribute__((aligned(16))) char smem[STAGES * G::STAGE_BYTES];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int grp = wid / GW, gw = wid % GW;
+  const int wm = gw / GN, wn = gw % GN;
+  const int wid_u = __builtin_amdgcn_readfirstlane(wid);
+
+  const int tiles_n = (N + BN - 1) / BN, tiles_m = (M + BM - 1) / BM;
+  const int t = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+  const int tile_m = t / tiles_n, tile_n = t - tile_m * tiles_n;
+  const int m0 = tile_m * BM, n0 = tile_n * BN;
+
+  // ---- DMA addressing (wave wid_u owns A pieces [wid*A_PW, ...) and W pieces [wid*W_PW, ...)) ----
+  const __amdgpu_buffer_rsrc_t asrc = make_rsrc(A, (uint32_t)((size_t)(M - 1) * lda * sizeof(T) + (size_t)K * sizeof(T)));
+  const __amdgpu_buffer_rsrc_t wsrc = make_rsrc(W, (uint32_t)((size_t)(N - 1) * ldw * sizeof(T) + (size_t)K * sizeof(T)));
+  uint32_t aoff[G::A_PW], woff[G::W_PW];
+  int ach[G::A_PW], wch[G::W_PW];
+#pragma unroll
+  for (int i = 0; i < G::A_PW; ++i) {
+    const int row = (wid * G::A_PW + i) * 8 + (lane >> 3);
+    ach[i] = (lane & 7) ^ ((row >> 1) & 7);
+    const int gm = m0 + row;
+    aoff[i] = gm < M ? (uint32_t)((size_t)gm * lda * sizeof(T)) : kOOB;
+  }
+#pragma unroll
+  for (int i = 0; i < G::W_PW; ++i) {
+    const int row = (wid * G::W_PW + i) * 8 + (lane >> 3);
+    wch[i] = (lane & 7) ^ ((row >> 1) & 7);
+    const int gn = n0 + row;
+    woff[i] = (row < BN && gn < N) ? (uint32_t)((size_t)gn * ldw * sizeof(T)) : kOOB;
+  }
+  auto wdst = [&](char* base, int i) -> char* {   // surplus pieces land in the dummy slot
+    const int piece = wid_u * G::W_PW + i;
+    return base + (piece < G::W_PIECES ? G::W_OFF + piece * 1024 : G::DUMMY_OFF);
+  };
+  auto stage = [&](int buf, int k0) {
+    char* base = smem + buf * G::STAGE_BYTES;
+#pragma unroll
+    for (int i = 0; i < G::A_PW; ++i) {
+      const int gk = k0 + ach[i] * 8;
+      dma16(asrc, base + (wid_u * G::A_PW + i) * 1024, (gk < K && aoff[i] != kOOB) ? aoff[i] + (uint32_t)(gk * sizeof(T)) : kOOB);
+    }
+#pragma unroll
+    for (int i = 0; i < G::W_PW; ++i) {
+      const int gk = k0 + wch[i] * 8;
+      dma16(wsrc, wdst(base, i), (gk < K && woff[i] != kOOB) ? woff[i] + (uint32_t)(gk * sizeof(T)) : kOOB);
+    }
+  };
+
+  f32x4 acc[TN][TM];
+#pragma unroll
+  for (int i = 0; i < TN; ++i)
+#pragma unroll
+    for (int j = 0; j < TM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int fr = lane & 15, fg = lane >> 4;
+  const int arow0 = grp * GBM + wm * WM + fr;   // this lane's fragment rows in the A / W tiles
+  const int wrow0 = wn * WN + fr;
+  frag af[2][TM], wf[2][TN];
+  auto read_tile = [&](int buf) {
+    const char* sa = smem + buf * G::STAGE_BYTES;
+    const char* sw = sa + G::W_OFF;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int chunk = ks * 4 + fg;
+#pragma unroll
+      for (int i = 0; i < TN; ++i) wf[ks][i] = *reinterpret_cast<const frag*>(sw + swz_off(wrow0 + i * 16, chunk));
+#pragma unroll
+      for (int j = 0; j < TM; ++j) af[ks][j] = *reinterpret_cast<const frag*>(sa + swz_off(arow0 + j * 16, chunk));
+    }
+  };
+  auto mfma_tile = [&]() {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < TN; ++i)
+#pragma unroll
+        for (int j = 0; j < TM; ++j) acc[i][j] = MfmaOp<T>::mma(wf[ks][i], af[ks][j], acc[i][j]);
+  };
+  // sched_barrier(0) pins the intervals: no MFMA may be hoisted into a read
+  // interval (or LDS read sunk into a matrix interval) across a block barrier
+  auto barrier = [] {
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  // s_waitcnt immediates (gfx9 encoding: vmcnt lo[3:0] hi[15:14], expcnt[6:4], lgkmcnt[11:8])
+  constexpr int kVmSteady = (((STAGES - 2) * L) & 15) | ((((STAGES - 2) * L) >> 4) << 14) | 0x70 | 0xF00;
+  constexpr int kVm0 = 0x70 | 0xF00;
+  constexpr int kLgkm0 = 0xC07F;            // lgkmcnt(0), vmcnt and expcnt at max
+
+  const int nk = (K + BK - 1) / BK;
+#ifdef RDB_PP_STAMPS
+  // diagnostic build only (bench/gemm_lab): per-block cycle stamps
+  unsigned long long* stp = rdb_pp_stamps + (size_t)blockIdx.x * 8;
+  const unsigned long long t_start = __builtin_amdgcn_s_memtime();
+#endif
+  // prologue: tiles 0 .. STAGES-2 in flight, tile 0 retired and visible
+#pragma unroll
+  for (int s = 0; s < STAGES - 1; ++s)
+    if (s < nk) stage(s, s * BK);
+  if (nk >= STAGES - 1) __builtin_amdgcn_s_waitcnt(kVmSteady);
+  else __builtin_amdgcn_s_waitcnt(kVm0);
+  barrier();
+#ifdef RDB_PP_STAMPS
+  const unsigned long long t_pro = __builtin_amdgcn_s_memtime();
+#endif
+  if (grp == 1) barrier();   // stagger: group 1 one interval behind
+
+  int buf = 0;
+  for (int kt = 0; kt < nk; ++kt) {
+    // ---- read interval: fragments of tile kt, DMA of tile kt+STAGES-1 ----
+    read_tile(buf);
+    const bool steady = kt + STAGES - 1 < nk;
+    if (steady) stage((kt + STAGES - 1) % STAGES, (kt + STAGES - 1) * BK);
+    __builtin_amdgcn_s_waitcnt(kLgkm0);           // my reads of this buffer are done (WAR)
+    if (steady) __builtin_amdgcn_s_waitcnt(kVmSteady);  // my pieces of tile kt+1 landed (RAW)
+    else __builtin_amdgcn_s_waitcnt(kVm0);
+    barrier();
+    // ---- matrix interval ----
+    __builtin_amdgcn_s_setprio(1);
+    mfma_tile();
+    __builtin_amdgcn_s_setprio(0);
+    barrier();
+    buf = buf == STAGES - 1 ? 0 : buf + 1;
+  }
+  if (grp == 0) barrier();
+#ifdef RDB_PP_STAMPS
+  const unsigned long long t_loop = __builtin_amdgcn_s_memtime();
+#endif
+
+  // ---- epilogue ----
+  if constexpr (sizeof(OutT) == 2) {
+    if (act != ACT_SWIGLU && staged_epilogue_ok<T, OutT, HAS_RES>(N, C, ldc, R, ldr)) {
+      float bv[TN][4];
+#pragma unroll
+      for (int i = 0; i < TN; ++i) {
+        const int n = n0 + wn * WN + i * 16 + fg * 4;
+        if constexpr (HAS_BIAS) {
+          const __amdgpu_buffer_rsrc_t bsrc = make_rsrc(bias, (uint32_t)(N * sizeof(T)));
+          const u32x2 raw = bload8(bsrc, (uint32_t)(n * sizeof(T)));
+          const T* e = reinterpret_cast<const T*>(&raw);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) bv[i][q] = (float)e[q];
+        } else {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) bv[i][q] = 0.f;
+        }
+      }
+      constexpr int SB = STAGES * G::STAGE_BYTES;
+      auto go = [&](auto actf) {
+        staged_epilogue<T, OutT, BM, BN, SB, G::NT, TM, TN, HAS_RES>(smem, acc, bv, grp * GBM + wm * WM, wn * WN, m0,
+                                                                     n0, M, N, C, ldc, R, ldr, alpha, actf);
+      };
+      switch (act) {
+        case ACT_GELU: go([](float x) { return apply_act<ACT_GELU>(x); }); break;
+        case ACT_RELU: go([](float x) { return apply_act<ACT_RELU>(x); }); break;
+        case ACT_TANH: go([](float x) { return apply_act<ACT_TANH>(x); }); break;
+        case ACT_SILU: go([](float x) { return apply_act<ACT_SILU>(x); }); break;
+        case ACT_GELU_TANH: go([](float x) { return apply_act<ACT_GELU_TANH>(x); }); break;
+        case ACT_SIGMOID: go([](float x) { return apply_act<ACT_SIGMOID>(x); }); break;
+        default: go([](float x) { return x; }); break;
+      }
+#ifdef RDB_PP_STAMPS
+      if (tid == 0) {
+        stp[0] = t_start;
+        stp[1] = t_pro;
+        stp[2] = t_loop;
+        stp[3] = __builtin_amdgcn_s_memtime();
+      }
+#endif
+      return;
+    }
+  }
+  // direct epilogue: lane holds C[m][n..n+3] of every fragment
+  const bool swiglu = act == ACT_SWIGLU;
+  const int n_out = swiglu ? (N >> 1) : N;
+  float bv[TN][4];
+#pragma unroll
+  for (int i = 0; i < TN; ++i) {
+    const int n = n0 + wn * WN + i * 16 + fg * 4;
+    if constexpr (HAS_BIAS) {
+      const __amdgpu_buffer_rsrc_t bsrc = make_rsrc(bias, (uint32_t)(N * sizeof(T)));
+      const u32x2 raw = bload8(bsrc, (uint32_t)(n * sizeof(T)));
+      const T* e = reinterpret_cast<const T*>(&raw);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) bv[i][q] = (float)e[q];
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) bv[i][q] = 0.f;
+    }
+  }
+  u32x2 rraw[TM][TN];
+  if constexpr (HAS_RES) {
+    const __amdgpu_buffer_rsrc_t rsrc = make_rsrc(R, (uint32_t)((size_t)(M - 1) * ldr * sizeof(T) + (size_t)n_out * sizeof(T)));
+#pragma unroll
+    for (int j = 0; j < TM; ++j) {
+      const int m = m0 + grp * GBM + wm * WM + j * 16 + fr;
+#pragma unroll
+      for (int i = 0; i < TN; ++i) {
+        const int n = n0 + wn * WN + i * 16 + fg * 4;
+        if (!swiglu) {
+          const uint32_t off = (m < M && n < N) ? (uint32_t)(((size_t)m * ldr + n) * sizeof(T)) : kOOB;
+          rraw[j][i] = bload8(rsrc, off);
+        } else {
+          const uint32_t off = (m < M && n < N) ? (uint32_t)(((size_t)m * ldr + (n >> 1)) * sizeof(T)) : kOOB;
+          rraw[j][i] = u32x2{bload4(rsrc, off), 0u};
+        }
+      }
+    }
+  }
+  auto rv = [&](int j, int i, int q) -> float {
+    const T* e = reinterpret_cast<const T*>(&rraw[j][i]);
+    return (float)e[q];
+  };
+  if (swiglu) {
+#pragma unroll
+    for (int j = 0; j < TM; ++j) {
+      const int m = m0 + grp * GBM + wm * WM + j * 16 + fr;
+#pragma unroll
+      for (int i = 0; i < TN; ++i) {
+        const int n = n0 + wn * WN + i * 16 + fg * 4;
+        float x[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) x[q] = alpha * acc[i][j][q] + bv[i][q];
+        float r0 = apply_act<ACT_SILU>(x[0]) * x[1];
+        float r1 = apply_act<ACT_SILU>(x[2]) * x[3];
+        if constexpr (HAS_RES) { r0 += rv(j, i, 0); r1 += rv(j, i, 1); }
+        if (m < M && n < N) {
+          OutT* cp = C + (size_t)m * ldc + (n >> 1);
+          cp[0] = (OutT)r0;
+          cp[1] = (OutT)r1;
+        }
+      }
+    }
+    return;
+  }
+  const bool vec_ok = ((ldc & 3) == 0);
+  auto store_tile = [&](auto actf) {
+#pragma unroll
+    for (int j = 0; j < TM; ++j) {
+      const int m = m0 + grp * GBM + wm * WM + j * 16 + fr;
+#pragma unroll
+      for (int i = 0; i < TN; ++i) {
+        const int n = n0 + wn * WN + i * 16 + fg * 4;
+        float y[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          float x = alpha * acc[i][j][q] + bv[i][q];
+          if constexpr (HAS_RES) x += rv(j, i, q);
+          y[q] = actf(x);
+        }
+        if (m >= M || n >= N) continue;
+        OutT* cp = C + (size_t)m * ldc + n;
+        if (n + 3 < N && vec_ok) {
+          store4<OutT>(cp, y[0], y[1], y[2], y[3]);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (n + e < N) cp[e] = (OutT)y[e];
+        }
+      }
+    }
+  };
+  switch (act) {
+    case ACT_GELU: store_tile([](float x) { return apply_act<ACT_GELU>(x); }); break;
+    case ACT_RELU: store_tile([](float x) { return apply_act<ACT_RELU>(x); }); break;
+    case ACT_TANH: store_tile([](float x) { return apply_act<ACT_TANH>(x); }); break;
+    case ACT_SILU: store_tile([](float x) { return apply_act<ACT_SILU>(x); }); break;
+    case ACT_GELU_TANH: store_tile([](float x) { return apply_act<ACT_GELU_TANH>(x); }); break;
+    case ACT_SIGMOID: store_tile([](float x) { return apply_act<ACT_SIGMOID>(x); }); break;
+    default: store_tile([](float x) { return x; }); break;
+  }
+#ifdef RDB_PP_STAMPS
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (tid == 0) {
+    unsigned xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    stp[0] = t_start;
+    stp[1] = t_pro;
+    stp[2] = t_loop;
+    stp[3] = __builtin_amdgcn_s_memtime();
+    stp[4] = xcc & 0xf;
+    stp[5] = __builtin_amdgcn_s_memrealtime();
+  }
+#endif
+}
+
+template <typename T, typename OutT, int NW, int BM, int BN, int GM, int GN, int STAGES>
+void launch_gemm_pp(const T* A, int lda, const T* W, int ldw, OutT* C, int ldc, const T* bias, const T* R, int ldr,
+                    int M, int N, int K, float alpha, int act, hipStream_t s) {
+  const int nwg = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  const dim3 grid(nwg), block(64 * NW);
+  if (bias && R)
+    hipLaunchKernelGGL((gemm_pp_kernel<T, OutT, NW, BM, BN, GM, GN, STAGES, true, true>), grid, block, 0, s, A, lda, W,
+                       ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act);
+  else if (bias)
+    hipLaunchKernelGGL((gemm_pp_kernel<T, OutT, NW, BM, BN, GM, GN, STAGES, true, false>), grid, block, 0, s, A, lda, W,
+                       ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act);
+  else if (R)
+    hipLaunchKernelGGL((gemm_pp_kernel<T, OutT, NW, BM, BN, GM, GN, STAGES, false, true>), grid, block, 0, s, A, lda, W,
+                       ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act);
+  else
+    hipLaunchKernelGGL((gemm_pp_kernel<T, OutT, NW, BM, BN, GM, GN, STAGES, false, false>), grid, block, 0, s, A, lda,
+                       W, ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act);
+}
+
+}  // namespace rdb

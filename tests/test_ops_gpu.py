@@ -31,7 +31,7 @@ def test_linear_plain(M, N, K, dtype):
     _close(y, ops.linear_ref(x, w), 2e-2, 2e-2)
 
 
-@pytest.mark.parametrize("cfg", list(range(19)))
+@pytest.mark.parametrize("cfg", list(range(22)))
 def test_linear_tile_configs_asymmetric(cfg):
     """A = I with an asymmetric W catches a transposed C-write (guide §3)."""
     ops = _ops()
@@ -200,16 +200,28 @@ def test_image_to_nhwc_and_gather():
     assert torch.equal(dst.cpu(), exp)
 
 
-@pytest.mark.parametrize("cfg", list(range(19)))
-def test_linear_all_tiles_random(cfg):
+@pytest.mark.parametrize("N", [392, 388])   # 388 % 8 != 0: the direct (unstaged) epilogue
+@pytest.mark.parametrize("cfg", list(range(22)))
+def test_linear_all_tiles_random(cfg, N):
     ops = _ops()
     torch.manual_seed(11)
     x = torch.randn(300, 520, device="cuda", dtype=torch.bfloat16)
-    w = torch.randn(392, 520, device="cuda", dtype=torch.bfloat16) * 0.05
-    b = torch.randn(392, device="cuda", dtype=torch.bfloat16)
-    r = torch.randn(300, 392, device="cuda", dtype=torch.bfloat16)
+    w = torch.randn(N, 520, device="cuda", dtype=torch.bfloat16) * 0.05
+    b = torch.randn(N, device="cuda", dtype=torch.bfloat16)
+    r = torch.randn(300, N, device="cuda", dtype=torch.bfloat16)
     _close(ops.linear(x, w, b, act="gelu", residual=r, tile_cfg=cfg),
            ops.linear_ref(x, w, b, act="gelu", residual=r), 3e-2, 2e-2)
+
+
+@pytest.mark.parametrize("cfg", [0, 8, 15, 19, 20, 21])
+def test_linear_swiglu_and_f16_tiles(cfg):
+    """SwiGLU pairing epilogue and f16 on the 8-wave and ping-pong tiles."""
+    ops = _ops()
+    torch.manual_seed(12)
+    x = torch.randn(272, 256, device="cuda", dtype=torch.float16)
+    w = torch.randn(512, 256, device="cuda", dtype=torch.float16) * 0.05
+    _close(ops.linear(x, w, act="swiglu", tile_cfg=cfg), ops.linear_ref(x, w, act="swiglu"), 3e-2, 2e-2)
+    _close(ops.linear(x, w, tile_cfg=cfg), ops.linear_ref(x, w), 3e-2, 2e-2)
 
 
 @pytest.mark.parametrize("cfg", list(range(13)))
