@@ -5,8 +5,11 @@
 // causal masking and GQA (Hkv divides H).  Used by BERT-base (S=128, D=64,
 // bidirectional) and Llama-3 prefill (D=128, causal, GQA).
 //
-// One workgroup = 4 waves = 128 query rows of one (batch, head); each wave owns
-// 32 query rows.  K/V blocks of 128 keys are staged in LDS:
+// One workgroup = 4 waves = 64 * QT query rows of one (batch, head); each wave
+// owns 16 * QT query rows.  QT = 1 when the QT = 2 grid would not give every CU
+// two blocks (BERT: B32 x H12 x S128 is 384 blocks at QT = 2, i.e. 1.5 per CU
+// and no overlap of one block's K/V load latency with another's math; 768 at
+// QT = 1, at the price of staging each K/V block twice).  K/V blocks of 128 keys are staged in LDS:
 //   * K row-major [key][D] with the 16-B chunk XOR swizzle (ds_read_b128 frags);
 //   * V transposed [D][128 + 8] (the +8 element pad makes the 8-byte fragment
 //     reads of 16 d-rows x 2 key groups conflict-free).
@@ -18,6 +21,7 @@
 //        accumulator registers with a permuted-but-consistent k order, §3)
 //        -> each lane holds 4 consecutive d of one query: 8-byte stores.
 #include "common.h"
+#include <cstdlib>
 #include <stdexcept>
 
 namespace rdb {
@@ -52,8 +56,8 @@ __device__ __forceinline__ int kswz(int row, int chunk) {
   else return row * (CPR * 16) + ((chunk ^ (row & 15)) << 4);
 }
 
-template <typename T, int D>
-__global__ void __launch_bounds__(256, 2)
+template <typename T, int D, int QT>
+__global__ void __launch_bounds__(256, QT == 1 ? 3 : 2)
 attn_fwd_kernel(const T* __restrict__ qkv, int ld_qkv, int q_off, int k_off, int v_off,
                 int H, int Hkv, int S, const int* __restrict__ lens, int causal,
                 T* __restrict__ out, int ld_out, float scale_log2e) {
@@ -72,7 +76,8 @@ attn_fwd_kernel(const T* __restrict__ qkv, int ld_qkv, int q_off, int k_off, int
   const int fr = lane & 15, fg = lane >> 4;
   const int b = blockIdx.z, h = blockIdx.y;
   const int hk = h / (H / Hkv);
-  const int q0 = blockIdx.x * 128 + wid * 32;  // this wave's first query row
+  constexpr int QROWS = 64 * QT;                 // query rows per block
+  const int q0 = blockIdx.x * QROWS + wid * 16 * QT;  // this wave's first query row
   const size_t tok0 = (size_t)b * S;
 
   // K/V staging: EVERY load of a block is issued before the first LDS write
@@ -128,9 +133,9 @@ attn_fwd_kernel(const T* __restrict__ qkv, int ld_qkv, int q_off, int k_off, int
   load_kv(0, 0);
 
   // Q fragments (B operand): lane holds Q[q][ks*32 + 8*fg + j].
-  frag8 qf[2][NKS];
+  frag8 qf[QT][NKS];
 #pragma unroll
-  for (int qt = 0; qt < 2; ++qt) {
+  for (int qt = 0; qt < QT; ++qt) {
     const int q = min(q0 + qt * 16 + fr, S - 1);  // rows past S are computed, never stored
 #pragma unroll
     for (int ks = 0; ks < NKS; ++ks)
@@ -139,16 +144,20 @@ attn_fwd_kernel(const T* __restrict__ qkv, int ld_qkv, int q_off, int k_off, int
   int kv_len = lens ? lens[b] : S;
   kv_len = kv_len > S ? S : kv_len;
 
-  f32x4 o[NDT][2];
+  f32x4 o[NDT][QT];
 #pragma unroll
-  for (int i = 0; i < NDT; ++i) o[i][0] = o[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int i = 0; i < NDT; ++i)
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt) o[i][qt] = f32x4{0.f, 0.f, 0.f, 0.f};
   // running max in the SCALED (log2) domain; raw scores are scaled inside exp2's FMA
-  float m_run[2] = {-INFINITY, -INFINITY}, l_run[2] = {0.f, 0.f};
+  float m_run[QT], l_run[QT];
+#pragma unroll
+  for (int qt = 0; qt < QT; ++qt) { m_run[qt] = -INFINITY; l_run[qt] = 0.f; }
 
   // Causal: keys beyond the block's last query are never needed.
   int key_end = kv_len;
   if (causal) {
-    const int qlast = blockIdx.x * 128 + 127;
+    const int qlast = blockIdx.x * QROWS + QROWS - 1;
     key_end = key_end < qlast + 1 ? key_end : qlast + 1;
   }
   const int nblk = (key_end + KB - 1) / KB;
@@ -165,15 +174,16 @@ attn_fwd_kernel(const T* __restrict__ qkv, int ld_qkv, int q_off, int k_off, int
     __syncthreads();
 
     // ---- S^T = K . Q^T ----
-    f32x4 s[NKT][2];
+    f32x4 s[NKT][QT];
 #pragma unroll
     for (int kt = 0; kt < NKT; ++kt) {
-      s[kt][0] = s[kt][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int qt = 0; qt < QT; ++qt) s[kt][qt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int ks = 0; ks < NKS; ++ks) {
         const frag8 kf = *reinterpret_cast<const frag8*>(Ks + kswz<C::CPR>(kt * 16 + fr, ks * 4 + fg));
-        s[kt][0] = mma16<T>(kf, qf[0][ks], s[kt][0]);
-        s[kt][1] = mma16<T>(kf, qf[1][ks], s[kt][1]);
+#pragma unroll
+        for (int qt = 0; qt < QT; ++qt) s[kt][qt] = mma16<T>(kf, qf[qt][ks], s[kt][qt]);
       }
     }
 
@@ -181,7 +191,7 @@ attn_fwd_kernel(const T* __restrict__ qkv, int ld_qkv, int q_off, int k_off, int
     // (lane-local query q = q0 + qt*16 + fr) ----
     const bool need_mask = key0 + KB > kv_len || (causal && key0 + KB - 1 > q0);
 #pragma unroll
-    for (int qt = 0; qt < 2; ++qt) {
+    for (int qt = 0; qt < QT; ++qt) {
       const int q = q0 + qt * 16 + fr;
       float mx = -INFINITY;
       if (need_mask) {
@@ -226,9 +236,9 @@ attn_fwd_kernel(const T* __restrict__ qkv, int ld_qkv, int q_off, int k_off, int
     // ---- O^T += V^T . P^T over 4 chunks of 32 keys ----
 #pragma unroll
     for (int c = 0; c < KB / 32; ++c) {
-      frag8 pf[2];
+      frag8 pf[QT];
 #pragma unroll
-      for (int qt = 0; qt < 2; ++qt) {
+      for (int qt = 0; qt < QT; ++qt) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           pf[qt][e] = (T)s[2 * c][qt][e];
@@ -241,15 +251,15 @@ attn_fwd_kernel(const T* __restrict__ qkv, int ld_qkv, int q_off, int k_off, int
         const frag4 lo = *reinterpret_cast<const frag4*>(vr);
         const frag4 hi = *reinterpret_cast<const frag4*>(vr + 16);
         const frag8 vf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        o[dt][0] = mma16<T>(vf, pf[0], o[dt][0]);
-        o[dt][1] = mma16<T>(vf, pf[1], o[dt][1]);
+#pragma unroll
+        for (int qt = 0; qt < QT; ++qt) o[dt][qt] = mma16<T>(vf, pf[qt], o[dt][qt]);
       }
     }
   }
 
   // ---- normalise and store: lane holds O[q][dt*16 + 4*fg + e] ----
 #pragma unroll
-  for (int qt = 0; qt < 2; ++qt) {
+  for (int qt = 0; qt < QT; ++qt) {
     float l = l_run[qt];
     l += __shfl_xor(l, 16, 64);
     l += __shfl_xor(l, 32, 64);
@@ -274,11 +284,19 @@ void attn_fwd(int dtype, uintptr_t qkv, int ld_qkv, int q_off, int k_off, int v_
     throw std::invalid_argument("attn: strides/offsets must be 16-byte aligned");
   if (B <= 0 || S <= 0) return;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  dim3 grid((S + 127) / 128, H, B), blk(256);
+  // QT = 2 (128 query rows per block) unless that leaves fewer than 2 blocks per CU
+  const long blocks2 = (long)((S + 127) / 128) * H * B;
+  int qt = blocks2 < 512 ? 1 : 2;
+  if (const char* e = getenv("RDB_ATTN_QT")) qt = atoi(e) == 1 ? 1 : 2;   // A/B override
+  dim3 grid((S + 64 * qt - 1) / (64 * qt), H, B), blk(256);
   const float sl2e = scale * 1.4426950408889634f;
-#define RDB_ATTN(T, DD)                                                                          \
-  hipLaunchKernelGGL((attn_fwd_kernel<T, DD>), grid, blk, 0, s, (const T*)qkv, ld_qkv, q_off, k_off, \
-                     v_off, H, Hkv, S, (const int*)lens, causal, (T*)out, ld_out, sl2e)
+#define RDB_ATTN(T, DD)                                                                              \
+  if (qt == 1)                                                                                       \
+    hipLaunchKernelGGL((attn_fwd_kernel<T, DD, 1>), grid, blk, 0, s, (const T*)qkv, ld_qkv, q_off, k_off, \
+                       v_off, H, Hkv, S, (const int*)lens, causal, (T*)out, ld_out, sl2e);             \
+  else                                                                                               \
+    hipLaunchKernelGGL((attn_fwd_kernel<T, DD, 2>), grid, blk, 0, s, (const T*)qkv, ld_qkv, q_off, k_off, \
+                       v_off, H, Hkv, S, (const int*)lens, causal, (T*)out, ld_out, sl2e)
   if (D != 64 && D != 128) throw std::invalid_argument("attn: head dim must be 64 or 128");
   if (dtype == 0) { if (D == 64) RDB_ATTN(bf16, 64); else RDB_ATTN(bf16, 128); }
   else if (dtype == 1) { if (D == 64) RDB_ATTN(f16, 64); else RDB_ATTN(f16, 128); }

@@ -229,16 +229,34 @@ struct StagedEpi {
   static_assert(BN % 8 == 0 && RC >= 16 && BM % RC == 0, "staged epilogue geometry");
 };
 
-template <typename T, typename OutT, int BM, int BN, int SMEM_BYTES, int NT, int TM, int TN, bool HAS_RES, typename ActF>
-__device__ __forceinline__ void staged_epilogue(char* smem, const f32x4 (&acc)[TN][TM], const float (&bv)[TN][4],
-                                                int row_base, int col_base, int m0, int n0, int M, int N,
-                                                OutT* __restrict__ C, int ldc, const T* __restrict__ R, int ldr,
+template <typename T, typename OutT, int BM, int BN, int SMEM_BYTES, int NT, int TM, int TN, bool HAS_BIAS,
+          bool HAS_RES, typename ActF>
+__device__ __forceinline__ void staged_epilogue(char* smem, const f32x4 (&acc)[TN][TM], int row_base, int col_base,
+                                                int m0, int n0, int M, int N, OutT* __restrict__ C, int ldc,
+                                                const T* __restrict__ bias, const T* __restrict__ R, int ldr,
                                                 float alpha, ActF actf) {
   typedef StagedEpi<BM, BN, SMEM_BYTES> E;
   const int tid = threadIdx.x, lane = tid & 63;
   const int fr = lane & 15, fg = lane >> 4;
+  // bias in the fragment layout (TN x 8 B per lane), fetched once for all chunks
+  float bv[TN][4];
+#pragma unroll
+  for (int i = 0; i < TN; ++i) {
+    const int n = n0 + col_base + i * 16 + fg * 4;
+    if constexpr (HAS_BIAS) {
+      const __amdgpu_buffer_rsrc_t bsrc = make_rsrc(bias, (uint32_t)(N * sizeof(T)));
+      const u32x2 raw = bload8(bsrc, (uint32_t)(n * sizeof(T)));
+      const T* e = reinterpret_cast<const T*>(&raw);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) bv[i][q] = (float)e[q];
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) bv[i][q] = 0.f;
+    }
+  }
 #pragma unroll 1
   for (int c = 0; c < BM / E::RC; ++c) {
+    // phase 1: alpha * acc + bias -> LDS (f32)
 #pragma unroll
     for (int j = 0; j < TM; ++j) {
       const int rt = row_base + j * 16 + fr - c * E::RC;    // row inside this chunk
@@ -254,17 +272,20 @@ __device__ __forceinline__ void staged_epilogue(char* smem, const f32x4 (&acc)[T
       }
     }
     __syncthreads();
-#pragma unroll 2
+    // phase 2: row-major, 8 columns per lane, 16-B residual loads and stores of
+    // whole lines; unrolled 4x so four residual loads are in flight at once
+#pragma unroll 4
     for (int idx = tid; idx < E::RC * E::NV; idx += NT) {
       const int r = idx / E::NV, vcol = idx - r * E::NV;
       const int m = m0 + c * E::RC + r, n = n0 + vcol * 8;
       if (m < M && n < N) {
+        u32x4 rraw;
+        if constexpr (HAS_RES) rraw = *reinterpret_cast<const u32x4*>(R + (size_t)m * ldr + n);
         const f32x4 a = *reinterpret_cast<const f32x4*>(smem + r * E::ROWB + vcol * 32);
         const f32x4 b = *reinterpret_cast<const f32x4*>(smem + r * E::ROWB + vcol * 32 + 16);
         float x[8] = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
         if constexpr (HAS_RES) {
-          const u32x4 raw = *reinterpret_cast<const u32x4*>(R + (size_t)m * ldr + n);
-          const T* e = reinterpret_cast<const T*>(&raw);
+          const T* e = reinterpret_cast<const T*>(&rraw);
 #pragma unroll
           for (int q = 0; q < 8; ++q) x[q] += (float)e[q];
         }
@@ -279,7 +300,7 @@ __device__ __forceinline__ void staged_epilogue(char* smem, const f32x4 (&acc)[T
 }
 
 template <typename T, typename OutT, bool HAS_RES>
-__device__ __forceinline__ bool staged_epilogue_ok(int N, const OutT* C, int ldc, const T* R, int ldr) {
+__device__ __forceinline__ bool staged_epilogue_ok(int N, const OutT* C, int ldc, const T* bias, const T* R, int ldr) {
   if constexpr (sizeof(OutT) != 2) return false;
   bool ok = (N & 7) == 0 && (ldc & 7) == 0 && (reinterpret_cast<uintptr_t>(C) & 15) == 0;
   if constexpr (HAS_RES) ok = ok && (ldr & 7) == 0 && (reinterpret_cast<uintptr_t>(R) & 15) == 0;
@@ -448,26 +469,11 @@ mfma_gemm_kernel(typename LoaderT<T, 1>::Params ap, const T* __restrict__ W, int
 
   // ---- LDS-staged coalesced epilogue (plain modes; LN / SwiGLU keep the direct one) ----
   if constexpr (EPI == 0 && sizeof(OutT) == 2) {
-    if (act != ACT_SWIGLU && staged_epilogue_ok<T, OutT, HAS_RES>(N, C, ldc, R, ldr)) {
-      float bv[TN][4];
-#pragma unroll
-      for (int i = 0; i < TN; ++i) {
-        const int n = n0 + wn * WN + i * 16 + fg * 4;
-        if constexpr (HAS_BIAS) {
-          const __amdgpu_buffer_rsrc_t bsrc = make_rsrc(bias, (uint32_t)(N * sizeof(T)));
-          const u32x2 raw = bload8(bsrc, (uint32_t)(n * sizeof(T)));
-          const T* e = reinterpret_cast<const T*>(&raw);
-#pragma unroll
-          for (int q = 0; q < 4; ++q) bv[i][q] = (float)e[q];
-        } else {
-#pragma unroll
-          for (int q = 0; q < 4; ++q) bv[i][q] = 0.f;
-        }
-      }
+    if (act != ACT_SWIGLU && staged_epilogue_ok<T, OutT, HAS_RES>(N, C, ldc, bias, R, ldr)) {
       constexpr int SB = kStages * kStage;
       auto go = [&](auto actf) {
-        staged_epilogue<T, OutT, BM, BN, SB, NT, TM, TN, HAS_RES>(smem, acc, bv, wm * WM, wn * WN, m0, n0, M, N, C,
-                                                                  ldc, R, ldr, alpha, actf);
+        staged_epilogue<T, OutT, BM, BN, SB, NT, TM, TN, HAS_BIAS, HAS_RES>(smem, acc, wm * WM, wn * WN, m0, n0, M, N,
+                                                                            C, ldc, bias, R, ldr, alpha, actf);
       };
       switch (act) {
         case ACT_GELU: go([](float x) { return apply_act<ACT_GELU>(x); }); break;

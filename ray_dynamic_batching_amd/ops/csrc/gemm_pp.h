@@ -57,7 +57,8 @@ struct PPGeom {
   static_assert(BM % (8 * NW) == 0, "A tile must split into whole pieces per wave");
 };
 
-template <typename T, typename OutT, int NW, int BM, int BN, int GM, int GN, int STAGES, bool HAS_BIAS, bool HAS_RES>
+template <typename T, typename OutT, int NW, int BM, int BN, int GM, int GN, int STAGES, bool HAS_BIAS, bool HAS_RES,
+          bool DIM = false>
 __global__ void __launch_bounds__(64 * NW, 2)
 gemm_pp_kernel(const T* __restrict__ A, int lda, const T* __restrict__ W, int ldw, OutT* __restrict__ C, int ldc,
                const T* __restrict__ bias, const T* __restrict__ R, int ldr, int M, int N, int K, float alpha,
@@ -123,6 +124,19 @@ gemm_pp_kernel(const T* __restrict__ A, int lda, const T* __restrict__ W, int ld
     }
   };
 
+  // one DMA piece (p < A_PW: A, else W) of tile k0 into buffer buf
+  auto stage_piece = [&](int buf, int k0, int p) {
+    char* base = smem + buf * G::STAGE_BYTES;
+    if (p < G::A_PW) {
+      const int gk = k0 + ach[p] * 8;
+      dma16(asrc, base + (wid_u * G::A_PW + p) * 1024, (gk < K && aoff[p] != kOOB) ? aoff[p] + (uint32_t)(gk * sizeof(T)) : kOOB);
+    } else {
+      const int i = p - G::A_PW;
+      const int gk = k0 + wch[i] * 8;
+      dma16(wsrc, wdst(base, i), (gk < K && woff[i] != kOOB) ? woff[i] + (uint32_t)(gk * sizeof(T)) : kOOB);
+    }
+  };
+
   f32x4 acc[TN][TM];
 #pragma unroll
   for (int i = 0; i < TN; ++i)
@@ -152,6 +166,26 @@ gemm_pp_kernel(const T* __restrict__ A, int lda, const T* __restrict__ W, int ld
       for (int i = 0; i < TN; ++i)
 #pragma unroll
         for (int j = 0; j < TM; ++j) acc[i][j] = MfmaOp<T>::mma(wf[ks][i], af[ks][j], acc[i][j]);
+  };
+  // DIM: the next tile's DMA pieces are issued BETWEEN this tile's MFMAs (evenly
+  // spread), so the read interval carries only the ds_reads
+  constexpr int NMF = 2 * TN * TM;
+  constexpr int EVERY = NMF / L > 0 ? NMF / L : 1;
+  auto mfma_tile_dma = [&](int dbuf, int dk0) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < TN; ++i)
+#pragma unroll
+        for (int j = 0; j < TM; ++j) {
+          acc[i][j] = MfmaOp<T>::mma(wf[ks][i], af[ks][j], acc[i][j]);
+          const int c = (ks * TN + i) * TM + j;
+          if (c % EVERY == EVERY - 1 && c / EVERY < L) stage_piece(dbuf, dk0, c / EVERY);
+        }
+    if constexpr (EVERY * L > NMF) {   // pieces left over (L > NMF): after the last MFMA
+#pragma unroll
+      for (int p = NMF / EVERY; p < L; ++p) stage_piece(dbuf, dk0, p);
+    }
   };
   // sched_barrier(0) pins the intervals: no MFMA may be hoisted into a read
   // interval (or LDS read sunk into a matrix interval) across a block barrier
@@ -186,21 +220,53 @@ gemm_pp_kernel(const T* __restrict__ A, int lda, const T* __restrict__ W, int ld
   if (grp == 1) barrier();   // stagger: group 1 one interval behind
 
   int buf = 0;
-  for (int kt = 0; kt < nk; ++kt) {
-    // ---- read interval: fragments of tile kt, DMA of tile kt+STAGES-1 ----
-    read_tile(buf);
-    const bool steady = kt + STAGES - 1 < nk;
-    if (steady) stage((kt + STAGES - 1) % STAGES, (kt + STAGES - 1) * BK);
-    __builtin_amdgcn_s_waitcnt(kLgkm0);           // my reads of this buffer are done (WAR)
-    if (steady) __builtin_amdgcn_s_waitcnt(kVmSteady);  // my pieces of tile kt+1 landed (RAW)
-    else __builtin_amdgcn_s_waitcnt(kVm0);
-    barrier();
-    // ---- matrix interval ----
-    __builtin_amdgcn_s_setprio(1);
-    mfma_tile();
-    __builtin_amdgcn_s_setprio(0);
-    barrier();
-    buf = buf == STAGES - 1 ? 0 : buf + 1;
+  if constexpr (!DIM) {
+    for (int kt = 0; kt < nk; ++kt) {
+      // ---- read interval: fragments of tile kt, DMA of tile kt+STAGES-1 ----
+      read_tile(buf);
+      const bool steady = kt + STAGES - 1 < nk;
+      if (steady) stage((kt + STAGES - 1) % STAGES, (kt + STAGES - 1) * BK);
+      __builtin_amdgcn_s_waitcnt(kLgkm0);           // my reads of this buffer are done (WAR)
+      if (steady) __builtin_amdgcn_s_waitcnt(kVmSteady);  // my pieces of tile kt+1 landed (RAW)
+      else __builtin_amdgcn_s_waitcnt(kVm0);
+      barrier();
+      // ---- matrix interval ----
+      __builtin_amdgcn_s_setprio(1);
+      mfma_tile();
+      __builtin_amdgcn_s_setprio(0);
+      barrier();
+      buf = buf == STAGES - 1 ? 0 : buf + 1;
+    }
+  } else {
+    // DMA of tile kt+STAGES-1 rides tile kt's matrix interval.  RAW: every wave
+    // retires its pieces of tile kt+1 before the barrier that opens group 0's
+    // read of it -- group 0 at the end of its matrix interval of tile kt
+    // (STAGES-2 younger tiles may stay in flight), group 1 at the end of its
+    // read interval of tile kt (its matrix interval of kt comes later: STAGES-3).
+    // WAR: buffer (kt-1)%STAGES was last read in the read intervals of tile
+    // kt-1, both of which end (lgkmcnt(0)) before the first matrix interval of
+    // tile kt starts.
+    constexpr int kVmG1 = (((STAGES - 3) * L) & 15) | ((((STAGES - 3) * L) >> 4) << 14) | 0x70 | 0xF00;
+    for (int kt = 0; kt < nk; ++kt) {
+      const bool steady = kt + STAGES - 1 < nk;
+      read_tile(buf);
+      __builtin_amdgcn_s_waitcnt(kLgkm0);
+      if (grp == 1) {
+        if (steady) __builtin_amdgcn_s_waitcnt(kVmG1);
+        else __builtin_amdgcn_s_waitcnt(kVm0);
+      }
+      barrier();
+      __builtin_amdgcn_s_setprio(1);
+      if (steady) mfma_tile_dma((kt + STAGES - 1) % STAGES, (kt + STAGES - 1) * BK);
+      else mfma_tile();
+      __builtin_amdgcn_s_setprio(0);
+      if (grp == 0) {
+        if (steady) __builtin_amdgcn_s_waitcnt(kVmSteady);
+        else __builtin_amdgcn_s_waitcnt(kVm0);
+      }
+      barrier();
+      buf = buf == STAGES - 1 ? 0 : buf + 1;
+    }
   }
   if (grp == 0) barrier();
 #ifdef RDB_PP_STAMPS
@@ -209,26 +275,12 @@ gemm_pp_kernel(const T* __restrict__ A, int lda, const T* __restrict__ W, int ld
 
   // ---- epilogue ----
   if constexpr (sizeof(OutT) == 2) {
-    if (act != ACT_SWIGLU && staged_epilogue_ok<T, OutT, HAS_RES>(N, C, ldc, R, ldr)) {
-      float bv[TN][4];
-#pragma unroll
-      for (int i = 0; i < TN; ++i) {
-        const int n = n0 + wn * WN + i * 16 + fg * 4;
-        if constexpr (HAS_BIAS) {
-          const __amdgpu_buffer_rsrc_t bsrc = make_rsrc(bias, (uint32_t)(N * sizeof(T)));
-          const u32x2 raw = bload8(bsrc, (uint32_t)(n * sizeof(T)));
-          const T* e = reinterpret_cast<const T*>(&raw);
-#pragma unroll
-          for (int q = 0; q < 4; ++q) bv[i][q] = (float)e[q];
-        } else {
-#pragma unroll
-          for (int q = 0; q < 4; ++q) bv[i][q] = 0.f;
-        }
-      }
+    if (act != ACT_SWIGLU && staged_epilogue_ok<T, OutT, HAS_RES>(N, C, ldc, bias, R, ldr)) {
       constexpr int SB = STAGES * G::STAGE_BYTES;
       auto go = [&](auto actf) {
-        staged_epilogue<T, OutT, BM, BN, SB, G::NT, TM, TN, HAS_RES>(smem, acc, bv, grp * GBM + wm * WM, wn * WN, m0,
-                                                                     n0, M, N, C, ldc, R, ldr, alpha, actf);
+        staged_epilogue<T, OutT, BM, BN, SB, G::NT, TM, TN, HAS_BIAS, HAS_RES>(smem, acc, grp * GBM + wm * WM, wn * WN,
+                                                                               m0, n0, M, N, C, ldc, bias, R, ldr, alpha,
+                                                                               actf);
       };
       switch (act) {
         case ACT_GELU: go([](float x) { return apply_act<ACT_GELU>(x); }); break;
@@ -364,22 +416,22 @@ gemm_pp_kernel(const T* __restrict__ A, int lda, const T* __restrict__ W, int ld
 #endif
 }
 
-template <typename T, typename OutT, int NW, int BM, int BN, int GM, int GN, int STAGES>
+template <typename T, typename OutT, int NW, int BM, int BN, int GM, int GN, int STAGES, bool DIM = false>
 void launch_gemm_pp(const T* A, int lda, const T* W, int ldw, OutT* C, int ldc, const T* bias, const T* R, int ldr,
                     int M, int N, int K, float alpha, int act, hipStream_t s) {
   const int nwg = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
   const dim3 grid(nwg), block(64 * NW);
   if (bias && R)
-    hipLaunchKernelGGL((gemm_pp_kernel<T, OutT, NW, BM, BN, GM, GN, STAGES, true, true>), grid, block, 0, s, A, lda, W,
+    hipLaunchKernelGGL((gemm_pp_kernel<T, OutT, NW, BM, BN, GM, GN, STAGES, true, true, DIM>), grid, block, 0, s, A, lda, W,
                        ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act);
   else if (bias)
-    hipLaunchKernelGGL((gemm_pp_kernel<T, OutT, NW, BM, BN, GM, GN, STAGES, true, false>), grid, block, 0, s, A, lda, W,
+    hipLaunchKernelGGL((gemm_pp_kernel<T, OutT, NW, BM, BN, GM, GN, STAGES, true, false, DIM>), grid, block, 0, s, A, lda, W,
                        ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act);
   else if (R)
-    hipLaunchKernelGGL((gemm_pp_kernel<T, OutT, NW, BM, BN, GM, GN, STAGES, false, true>), grid, block, 0, s, A, lda, W,
+    hipLaunchKernelGGL((gemm_pp_kernel<T, OutT, NW, BM, BN, GM, GN, STAGES, false, true, DIM>), grid, block, 0, s, A, lda, W,
                        ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act);
   else
-    hipLaunchKernelGGL((gemm_pp_kernel<T, OutT, NW, BM, BN, GM, GN, STAGES, false, false>), grid, block, 0, s, A, lda,
+    hipLaunchKernelGGL((gemm_pp_kernel<T, OutT, NW, BM, BN, GM, GN, STAGES, false, false, DIM>), grid, block, 0, s, A, lda,
                        W, ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act);
 }
 

@@ -256,6 +256,90 @@ class GpuAllocator {
     allocs_[owner] = a;
     return to_py(a);
   }
+  // Placement group (python/ray/util/placement_group.py:145, serve
+  // deployment_scheduler.py:494-620): reserve ALL bundles or none (gang).
+  // bundles = [(num_gpus, hbm_gb), ...]; strategy PACK / SPREAD (best effort:
+  // prefer GPUs this group already uses / does not use yet), STRICT_PACK (every
+  // bundle on one GPU), STRICT_SPREAD (every GPU-holding bundle on its own GPU).
+  // Returns {gpus: distinct GPUs in first-use order, bundle_gpus: [[...] per
+  // bundle], fraction} or None.
+  py::object allocate_bundles(const std::string& owner, const std::vector<std::pair<double, double>>& bundles,
+                              const std::string& strategy) {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (allocs_.count(owner)) throw std::invalid_argument(owner + " already holds GPUs");
+    const bool spread = strategy == "SPREAD" || strategy == "STRICT_SPREAD";
+    const bool strict_spread = strategy == "STRICT_SPREAD", strict_pack = strategy == "STRICT_PACK";
+    if (!spread && !strict_pack && strategy != "PACK")
+      throw std::invalid_argument("placement strategy must be PACK, SPREAD, STRICT_PACK or STRICT_SPREAD");
+    std::vector<int64_t> used = used_, hbm_used = hbm_used_;   // simulate, commit only if all fit
+    Alloc a;
+    std::vector<std::vector<int>> per_bundle;
+    std::vector<int> mine;                                        // GPUs this group holds so far
+    auto is_mine = [&](int g) { return std::find(mine.begin(), mine.end(), g) != mine.end(); };
+    int pack_gpu = -1;
+    for (const auto& b : bundles) {
+      const int64_t units = (int64_t)std::llround(b.first * kUnit);
+      const int64_t hbm = (int64_t)std::llround(b.second * 1e9);
+      std::vector<int> got;
+      if (units <= 0) {
+        per_bundle.push_back(got);
+        continue;
+      }
+      if (units >= kUnit) {
+        if (units % kUnit) throw std::invalid_argument("bundle GPU > 1 must be an integer");
+        const int need = (int)(units / kUnit);
+        if (strict_pack && (bundles.size() > 1 || need > 1)) return py::none();
+        const int64_t per = hbm / need;
+        for (size_t g = 0; g < used.size() && (int)got.size() < need; ++g)
+          if (used[g] == 0 && hbm_total_ - hbm_used[g] >= per) got.push_back((int)g);
+        if ((int)got.size() < need) return py::none();
+        for (int g : got) {
+          used[g] = kUnit;
+          hbm_used[g] += per;
+          a.gpus.push_back(g);
+          a.units.push_back(kUnit);
+          a.hbm.push_back(per);
+          if (!is_mine(g)) mine.push_back(g);
+        }
+      } else {
+        int best = -1;
+        double best_key = 1e300;
+        for (size_t g = 0; g < used.size(); ++g) {
+          const int64_t left = kUnit - used[g] - units;
+          if (left < 0 || hbm_total_ - hbm_used[g] < hbm) continue;
+          if (strict_pack && pack_gpu >= 0 && (int)g != pack_gpu) continue;
+          if (strict_spread && is_mine((int)g)) continue;
+          // best fit, with the group's own GPUs first (PACK) or last (SPREAD)
+          const double pref = is_mine((int)g) ? (spread ? 1.0 : 0.0) : (spread ? 0.0 : 1.0);
+          const double key = pref * 2.0 * kUnit + (double)left;
+          if (key < best_key) {
+            best_key = key;
+            best = (int)g;
+          }
+        }
+        if (best < 0) return py::none();
+        used[best] += units;
+        hbm_used[best] += hbm;
+        a.gpus.push_back(best);
+        a.units.push_back(units);
+        a.hbm.push_back(hbm);
+        got.push_back(best);
+        if (!is_mine(best)) mine.push_back(best);
+        if (strict_pack) pack_gpu = best;
+      }
+      per_bundle.push_back(got);
+    }
+    used_ = used;
+    hbm_used_ = hbm_used;
+    allocs_[owner] = a;
+    py::dict d;
+    d["gpus"] = mine;
+    d["bundle_gpus"] = per_bundle;
+    double frac = 0;
+    for (auto u : a.units) frac += (double)u / kUnit;
+    d["fraction"] = mine.size() == 1 ? std::min(1.0, frac) : (mine.empty() ? 0.0 : 1.0);
+    return d;
+  }
   bool release(const std::string& owner) {
     std::lock_guard<std::mutex> lk(mu_);
     auto it = allocs_.find(owner);
@@ -281,7 +365,11 @@ class GpuAllocator {
       py::dict holders;
       for (auto& kv : allocs_)
         for (size_t i = 0; i < kv.second.gpus.size(); ++i)
-          if (kv.second.gpus[i] == (int)g) holders[py::str(kv.first)] = (double)kv.second.units[i] / kUnit;
+          if (kv.second.gpus[i] == (int)g) {
+            const py::str k(kv.first);
+            const double prev = holders.contains(k) ? holders[k].cast<double>() : 0.0;
+            holders[k] = prev + (double)kv.second.units[i] / kUnit;
+          }
       d["holders"] = holders;
       l.append(d);
     }
@@ -864,6 +952,8 @@ void register_node_agent(py::module_& m) {
   py::class_<GpuAllocator>(m, "GpuAllocator")
       .def(py::init<int, double>(), py::arg("num_gpus"), py::arg("hbm_gb_per_gpu") = 288.0)
       .def("allocate", &GpuAllocator::allocate, py::arg("owner"), py::arg("num_gpus"), py::arg("hbm_gb") = 0.0)
+      .def("allocate_bundles", &GpuAllocator::allocate_bundles, py::arg("owner"), py::arg("bundles"),
+           py::arg("strategy") = "PACK")
       .def("release", &GpuAllocator::release)
       .def("snapshot", &GpuAllocator::snapshot)
       .def_property_readonly("num_gpus", &GpuAllocator::num_gpus);
@@ -886,6 +976,10 @@ void register_node_agent(py::module_& m) {
       .def("allocate", [](NodeAgent& a, const std::string& o, double g, double h) { return a.allocator().allocate(o, g, h); },
            py::arg("owner"), py::arg("num_gpus"), py::arg("hbm_gb") = 0.0)
       .def("release", [](NodeAgent& a, const std::string& o) { return a.allocator().release(o); })
+      .def("allocate_bundles",
+           [](NodeAgent& a, const std::string& o, const std::vector<std::pair<double, double>>& b,
+              const std::string& st) { return a.allocator().allocate_bundles(o, b, st); },
+           py::arg("owner"), py::arg("bundles"), py::arg("strategy") = "PACK")
       .def("resources", [](NodeAgent& a) { return a.allocator().snapshot(); })
       .def("kv_put", [](NodeAgent& a, const std::string& k, py::bytes v) { a.kv().put(k, std::string(v)); })
       .def("kv_get", [](NodeAgent& a, const std::string& k) -> py::object {

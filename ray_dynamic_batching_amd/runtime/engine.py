@@ -75,6 +75,15 @@ class EngineRunner:
 
         self.tune_in_context = os.environ.get("RDB_TUNE_IN_CONTEXT", "1") == "1"
         self.tuning_changes = {}
+        # RDB_TUNE_FILE: replay a saved tile table (A/B runs, profiling passes) instead
+        # of tuning; written after tuning when the file does not exist yet
+        self.tune_file = os.environ.get("RDB_TUNE_FILE", "")
+        self._tune_loaded = False
+        if self.tune_file and os.path.exists(self.tune_file):
+            from .. import ops
+
+            ops.load_tuning(self.tune_file)
+            self._tune_loaded = True
 
     def _bytes(self, shape, dtype) -> int:
         n = 1
@@ -122,7 +131,7 @@ class EngineRunner:
                         m.forward(s.inputs[0][:b])
             torch.cuda.current_stream().wait_stream(side)
             torch.cuda.synchronize()
-            if self.tune_in_context:
+            if self.tune_in_context and not self._tune_loaded:
                 self.tuning_changes.update(self._tune_in_context(m, s.inputs[0][:buckets[-1]], dev))
             s.graphs = [[None] * self.depth for _ in buckets]
             s.outputs = [[None] * self.depth for _ in buckets]
@@ -147,6 +156,10 @@ class EngineRunner:
                 torch.cuda.synchronize()
                 self.engine.set_latency_estimate(s.sid, bi, (time.perf_counter() - t) / 3 * 1e3)
         torch.cuda.synchronize()
+        if self.tune_file and not self._tune_loaded:
+            from .. import ops
+
+            ops.save_tuning(self.tune_file)
         self.capture_s = time.perf_counter() - t0
         return self
 

@@ -114,13 +114,47 @@ class DeploymentConfig(BaseModel):
             raise ValueError("ray_actor_options.num_gpus must be a non-negative number")
         if g > 1 and g != int(g):
             raise ValueError("fractional num_gpus must be < 1")
+        # placement groups (serve/api.py:299-303 + deployment_scheduler.py validation)
+        if self.placement_group_strategy is not None and self.placement_group_bundles is None:
+            raise ValueError("placement_group_strategy needs placement_group_bundles")
+        if self.placement_group_bundles is not None:
+            b = self.placement_group_bundles
+            if not isinstance(b, list) or not b or not all(isinstance(x, dict) and x for x in b):
+                raise ValueError("placement_group_bundles must be a non-empty list of non-empty dicts")
+            for x in b:
+                for k, v in x.items():
+                    if not isinstance(v, (int, float)) or v < 0:
+                        raise ValueError(f"bundle resource {k} must be a non-negative number")
+                gb = float(x.get("GPU", 0))
+                if gb > 1 and gb != int(gb):
+                    raise ValueError("fractional bundle GPU must be < 1")
+            if g > float(b[0].get("GPU", 0)) + 1e-9:
+                raise ValueError("the replica (ray_actor_options.num_gpus) must fit in the first bundle")
+            st = self.placement_group_strategy or "PACK"
+            if st not in ("PACK", "SPREAD", "STRICT_PACK", "STRICT_SPREAD"):
+                raise ValueError("placement_group_strategy must be PACK, SPREAD, STRICT_PACK or STRICT_SPREAD")
+        if self.max_replicas_per_node is not None and not (1 <= self.max_replicas_per_node <= 100):
+            raise ValueError("max_replicas_per_node must be in [1, 100]")
         return self
 
     def initial_num_replicas(self) -> int:
         if self.autoscaling_config is not None:
             a = self.autoscaling_config
-            return a.initial_replicas if a.initial_replicas is not None else a.min_replicas
-        return int(self.num_replicas or 0)
+            n = a.initial_replicas if a.initial_replicas is not None else a.min_replicas
+        else:
+            n = int(self.num_replicas or 0)
+        return self.cap_replicas(n)
+
+    def cap_replicas(self, n: int) -> int:
+        """One node: ``max_replicas_per_node`` caps the whole deployment."""
+        return min(n, self.max_replicas_per_node) if self.max_replicas_per_node else n
+
+    def placement_bundles(self):
+        """[(num_gpus, hbm_gb), ...] of the placement group, or None."""
+        if not self.placement_group_bundles:
+            return None
+        return [(float(b.get("GPU", 0)), float(b.get("hbm_gb", b.get("memory_gb", 0)) or 0))
+                for b in self.placement_group_bundles]
 
     @property
     def num_gpus(self) -> float:

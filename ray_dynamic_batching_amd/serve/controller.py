@@ -286,9 +286,15 @@ class ServeController:
 
         owner = f"{st.app_name}#{st.name}#{rep.slot}"
         self.agent.release(owner)
-        alloc = self.agent.allocate(owner, float(st.config.num_gpus), float(st.config.hbm_gb or 0.0))
+        bundles = st.config.placement_bundles()
+        if bundles is not None:
+            # gang reservation of every bundle (placement group); the replica
+            # process sees all of the group's GPUs (e.g. a TP replica's ranks)
+            alloc = self.agent.allocate_bundles(owner, bundles, st.config.placement_group_strategy or "PACK")
+        else:
+            alloc = self.agent.allocate(owner, float(st.config.num_gpus), float(st.config.hbm_gb or 0.0))
         if alloc is None:
-            logger.warning("no GPU capacity for %s (num_gpus=%s)", owner, st.config.num_gpus)
+            logger.warning("no GPU capacity for %s (num_gpus=%s, bundles=%s)", owner, st.config.num_gpus, bundles)
             return False
         rep.alloc = alloc
         gpus = list(alloc["gpus"])
@@ -485,7 +491,7 @@ class ServeController:
             live = [r for r in st.proc_replicas if not r.draining]
             total = sum(job.queue_depth(r.slot) for r in live) + st.router.num_queued()
             running = sum(1 for r in live if r.ready)
-        new_target = st.autoscaler.step(total, running, st.target)
+        new_target = st.config.cap_replicas(st.autoscaler.step(total, running, st.target))
         if new_target != st.target:
             logger.info("autoscaling %s: %d -> %d (ongoing=%s)", st.name, st.target, new_target, total)
             st.target = new_target

@@ -36,6 +36,50 @@ def test_allocator_whole_first_fit_fractional_best_fit_and_hbm():
         a.shutdown()
 
 
+def test_allocator_placement_group_bundles_gang_and_strategies():
+    """Placement-group bundles are reserved all-or-nothing with the Ray
+    strategies: PACK fills the group's own GPU first, SPREAD / STRICT_SPREAD use
+    distinct GPUs, STRICT_PACK one GPU, and a failed gang leaves nothing held."""
+    a = ragent.NodeAgent(4, 288.0)
+    try:
+        tp = a.allocate_bundles("tp", [(1, 0), (1, 0)], "STRICT_SPREAD")
+        assert tp["gpus"] == [0, 1] and tp["bundle_gpus"] == [[0], [1]]
+        pk = a.allocate_bundles("pk", [(0.25, 0), (0.25, 0), (0.25, 0)], "PACK")
+        assert pk["gpus"] == [2] and pk["bundle_gpus"] == [[2], [2], [2]] and abs(pk["fraction"] - 0.75) < 1e-9
+        sp = a.allocate_bundles("sp", [(0.25, 0), (0.25, 0)], "SPREAD")
+        assert sorted(sp["gpus"]) == [2, 3]          # GPU 2 has 0.25 left, then the group's second bundle spreads
+        # STRICT_SPREAD that cannot be met (3 distinct GPUs with 0.5 free: only GPU 3 has it) -> nothing held
+        before = [g["used"] for g in a.resources()]
+        assert a.allocate_bundles("bad", [(0.5, 0), (0.5, 0), (0.5, 0)], "STRICT_SPREAD") is None
+        assert [g["used"] for g in a.resources()] == before
+        assert a.allocate_bundles("sp2", [(0.9, 0), (0.9, 0)], "STRICT_PACK") is None
+        sk = a.allocate_bundles("sk", [(0.3, 0), (0.4, 0)], "STRICT_PACK")
+        assert len(sk["gpus"]) == 1
+        assert a.allocate_bundles("hbm", [(0.01, 290.0)], "PACK") is None   # HBM budget per GPU
+        assert a.release("tp") and a.release("pk")
+        assert a.allocate_bundles("tp2", [(2, 0)], "PACK")["gpus"] == [0, 1]
+        with pytest.raises(ValueError):
+            a.allocate_bundles("x", [(1, 0)], "NOPE")
+    finally:
+        a.shutdown()
+
+
+def test_placement_group_config_validation():
+    from ray_dynamic_batching_amd.serve.config import DeploymentConfig
+
+    c = DeploymentConfig(ray_actor_options={"num_gpus": 1}, placement_group_bundles=[{"GPU": 1}, {"GPU": 1}],
+                         placement_group_strategy="STRICT_SPREAD", num_replicas=4, max_replicas_per_node=2)
+    assert c.placement_bundles() == [(1.0, 0.0), (1.0, 0.0)]
+    assert c.initial_num_replicas() == 2 and c.cap_replicas(7) == 2
+    for bad in [dict(placement_group_strategy="PACK"),                                   # strategy without bundles
+                dict(placement_group_bundles=[]),
+                dict(placement_group_bundles=[{"GPU": 1}], placement_group_strategy="RANDOM"),
+                dict(ray_actor_options={"num_gpus": 1}, placement_group_bundles=[{"CPU": 1}, {"GPU": 1}]),
+                dict(max_replicas_per_node=0)]:
+        with pytest.raises(ValueError):
+            DeploymentConfig(**bad)
+
+
 def test_kv_store_persists_atomically(tmp_path):
     p = str(tmp_path / "kv.bin")
     k = ragent.KvStore(p)

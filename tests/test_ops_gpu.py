@@ -369,6 +369,33 @@ def test_linear_ln_stats_and_lnr_all_tiles(cfg):
     assert torch.allclose(st2, _ln_stats(y2), rtol=1e-4, atol=1e-2)
 
 
+@pytest.mark.parametrize("offset", [0.0, 8.0, 32.0])
+def test_deferred_ln_large_row_mean(offset):
+    """Deferred LayerNorm with rows far from zero mean: the variance
+    comes from E[y^2] - mean^2 of f32 atomic sums, which cancels as |mean|/std
+    grows.  Up to |mean| = 32 std -- beyond which bf16 activations cannot hold a
+    unit-variance row anyway (their ulp at 32 is 0.25) -- the folded GEMM must
+    still match LayerNorm-then-GEMM."""
+    ops = _ops()
+    torch.manual_seed(5)
+    M, N, K = 512, 768, 768
+    x = (torch.randn(M, K, device="cuda") + offset).to(torch.bfloat16)
+    w = (torch.randn(N, K, device="cuda") * K ** -0.5).to(torch.bfloat16)
+    b = (torch.randn(N, device="cuda") * 0.1).to(torch.bfloat16)
+    g = (1 + 0.2 * torch.randn(K, device="cuda")).to(torch.bfloat16)
+    be = (0.1 * torch.randn(K, device="cuda")).to(torch.bfloat16)
+    # the statistics as the producing GEMM's STATS epilogue accumulates them (f32 atomics)
+    st = torch.zeros(M, 2, device="cuda")
+    eye = torch.eye(K, device="cuda", dtype=torch.bfloat16)
+    zb = torch.zeros(K, device="cuda", dtype=torch.bfloat16)
+    zr = torch.zeros(M, K, device="cuda", dtype=torch.bfloat16)
+    xr = ops.linear_ln(x, eye, zb, residual=zr, out_stats=st)   # y = x, stats of y accumulated in the epilogue
+    assert torch.equal(xr, x)
+    w2, cs, b2 = ops.fold_ln_weights(w, b, g, be)
+    y = ops.linear_ln(x, w2, lna=(st, cs, b2, K, 1e-12))
+    _close(y, ops.linear_ln_ref(x, w, b, ln_x=(g, be)), 3e-2, 3e-2)
+
+
 def test_layer_norm_row_strided_view_and_embed_zeroes_stats():
     ops = _ops()
     torch.manual_seed(1)
