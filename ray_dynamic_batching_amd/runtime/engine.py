@@ -92,6 +92,8 @@ class EngineRunner:
         return n * torch.empty((), dtype=dtype).element_size()
 
     def build(self) -> "EngineRunner":
+        import os
+
         t0 = time.perf_counter()
         dev = torch.device("cuda", self.device)
         self.pools = [torch.cuda.graph_pool_handle() for _ in range(self.compute_streams)]
@@ -132,7 +134,8 @@ class EngineRunner:
             torch.cuda.current_stream().wait_stream(side)
             torch.cuda.synchronize()
             if self.tune_in_context and not self._tune_loaded:
-                self.tuning_changes.update(self._tune_in_context(m, s.inputs[0][:buckets[-1]], dev))
+                ctx_streams = int(os.environ.get("RDB_TUNE_CONTEXT_STREAMS", self.compute_streams))
+                self.tuning_changes.update(self._tune_in_context(m, s.inputs[0][:buckets[-1]], dev, ctx_streams))
             s.graphs = [[None] * self.depth for _ in buckets]
             s.outputs = [[None] * self.depth for _ in buckets]
             for bi, b in enumerate(buckets):
@@ -164,7 +167,11 @@ class EngineRunner:
         return self
 
     @staticmethod
-    def _tune_in_context(m, x, dev) -> dict:
+    def _tune_in_context(m, x, dev, streams: int = 1) -> dict:
+        """Coordinate-descent tile choice on the WHOLE forward, timed the way the
+        engine runs it: ``streams`` captured forwards replayed concurrently on
+        ``streams`` streams (the throughput regime of a multi-stream replica),
+        so tiles that trade single-batch latency for CU efficiency can win."""
         from .. import ops
 
         with ops.record_tuning_keys() as keys:
@@ -173,28 +180,42 @@ class EngineRunner:
         torch.cuda.synchronize()
         if not keys:
             return {}
-        pool = torch.cuda.graph_pool_handle()
+        streams = max(1, streams)
+        pools = [torch.cuda.graph_pool_handle() for _ in range(streams)]
+        sts = [torch.cuda.Stream(device=dev) for _ in range(streams)]
 
         def time_forward() -> float:
-            g = torch.cuda.CUDAGraph()
-            side = torch.cuda.Stream(device=dev)
-            side.wait_stream(torch.cuda.current_stream())
-            with torch.cuda.stream(side):
-                with torch.cuda.graph(g, pool=pool, stream=side):
-                    m.forward(x)
+            gs = []
+            for i in range(streams):
+                g = torch.cuda.CUDAGraph()
+                sts[i].wait_stream(torch.cuda.current_stream())
+                with torch.cuda.stream(sts[i]):
+                    with torch.cuda.graph(g, pool=pools[i], stream=sts[i]):
+                        m.forward(x)
+                gs.append(g)
             torch.cuda.synchronize()
-            for _ in range(3):
-                g.replay()
+            cur = torch.cuda.current_stream()
+
+            def burst(n):
+                for st in sts:
+                    st.wait_stream(cur)
+                for _ in range(n):
+                    for g, st in zip(gs, sts):
+                        with torch.cuda.stream(st):
+                            g.replay()
+                for st in sts:
+                    cur.wait_stream(st)
+
+            burst(3)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             best = float("inf")
             for _ in range(3):
                 e0.record()
-                for _ in range(10):
-                    g.replay()
+                burst(10)
                 e1.record()
                 torch.cuda.synchronize()
-                best = min(best, e0.elapsed_time(e1) / 10)
-            del g
+                best = min(best, e0.elapsed_time(e1) / (10 * streams))
+            del gs
             return best
 
         return ops.tune_in_context(time_forward, keys=list(keys), min_gain=0.02)

@@ -10,8 +10,8 @@
     handle = serve.run(Model.bind())
     handle.remote(x).result()
 """
-from .api import Application, Deployment, delete, deployment, get_app_handle, get_deployment_handle, http_port, \
-    metrics_text, run, shutdown, start, status
+from .api import Application, Deployment, delete, deployment, get_app_handle, get_deployment_handle, grpc_port, \
+    http_port, metrics_text, run, shutdown, start, status
 from .batching import batch
 from .config import AutoscalingConfig, DeploymentConfig, EngineConfig
 from .context import get_replica_context
@@ -26,5 +26,5 @@ __all__ = [
     "get_app_handle", "get_deployment_handle", "get_replica_context", "multiplexed", "get_multiplexed_model_id",
     "DeploymentHandle", "DeploymentResponse", "DeploymentResponseGenerator", "AutoscalingConfig",
     "DeploymentConfig", "EngineConfig", "BackPressureError", "RayServeException", "RequestCancelledError",
-    "RequestDroppedError", "model_deployment", "TensorCodec", "HTTPRequest", "http_port", "metrics_text",
+    "RequestDroppedError", "model_deployment", "TensorCodec", "HTTPRequest", "http_port", "grpc_port", "metrics_text",
 ]

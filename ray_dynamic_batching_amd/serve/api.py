@@ -155,16 +155,24 @@ def _controller(create: bool = True):
     return get_controller(create)
 
 
-def start(http_options: Optional[Dict[str, Any]] = None, **kwargs) -> None:
+def start(http_options: Optional[Dict[str, Any]] = None, grpc_options: Optional[Dict[str, Any]] = None,
+          **kwargs) -> None:
     """Start the (in-process) serve controller.  kwargs: mode="auto"|"local"|"process";
     ``http_options={"host": ..., "port": ...}`` also starts the HTTP proxy
-    (port 0 = pick a free port; see ``serve.http_port()``)."""
-    _controller().configure(http_options=http_options, **kwargs)
+    (port 0 = pick a free port; see ``serve.http_port()``); ``grpc_options=
+    {"host", "port", "request_types": {"/pkg.Svc/Method": MsgClass}, "streaming_methods": [...]}``
+    starts the gRPC proxy (``serve.grpc_port()``)."""
+    _controller().configure(http_options=http_options, grpc_options=grpc_options, **kwargs)
 
 
 def http_port() -> Optional[int]:
     ctrl = _controller(create=False)
     return ctrl.proxy.port if ctrl is not None and ctrl.proxy is not None else None
+
+
+def grpc_port() -> Optional[int]:
+    ctrl = _controller(create=False)
+    return ctrl.grpc_proxy.port if ctrl is not None and ctrl.grpc_proxy is not None else None
 
 
 def run(target: Application, blocking: bool = False, name: str = "default", route_prefix: Optional[str] = "/",

@@ -128,10 +128,12 @@ def main(argv=None) -> int:
     r.add_argument("--mode", default=None)
     r.add_argument("--duration", type=float, default=0)
     r.add_argument("--http-port", type=int, default=-1, help="start the HTTP proxy on this port (-1 = off)")
+    r.add_argument("--grpc-port", type=int, default=-1, help="start the gRPC proxy on this port (-1 = off)")
     d = sub.add_parser("deploy")
     d.add_argument("config")
     d.add_argument("--duration", type=float, default=0)
     d.add_argument("--http-port", type=int, default=-1)
+    d.add_argument("--grpc-port", type=int, default=-1)
     b = sub.add_parser("build")
     b.add_argument("import_path")
     b.add_argument("-o", "--output", default="-")
@@ -142,6 +144,7 @@ def main(argv=None) -> int:
     s.add_argument("--socket", default="", help="node agent control socket (default: discovered)")
     st = sub.add_parser("start")
     st.add_argument("--http-port", type=int, default=-1)
+    st.add_argument("--grpc-port", type=int, default=-1)
     st.add_argument("--duration", type=float, default=0)
     sh = sub.add_parser("shutdown")
     sh.add_argument("--socket", default="")
@@ -168,10 +171,17 @@ def main(argv=None) -> int:
         ok = _remote_shutdown(sock, a.timeout)
         print("shut down" if ok else "shutdown timed out", flush=True)
         return 0 if ok else 1
-    if a.cmd in ("run", "deploy", "start") and a.http_port >= 0:
+    if a.cmd in ("run", "deploy", "start"):
         from .api import start
 
-        start(http_options={"host": "127.0.0.1", "port": a.http_port})
+        http = {"host": "127.0.0.1", "port": a.http_port} if a.http_port >= 0 else None
+        grpc_ = {"host": "127.0.0.1", "port": a.grpc_port} if a.grpc_port >= 0 else None
+        if a.cmd == "deploy":   # proxies named in the config file (port flags win)
+            sch = ServeDeploySchema.from_yaml(a.config)
+            http = http or sch.http_options
+            grpc_ = grpc_ or sch.grpc_options
+        if http or grpc_:
+            start(http_options=http, grpc_options=grpc_)
     if a.cmd == "start":
         from .controller import get_controller
 

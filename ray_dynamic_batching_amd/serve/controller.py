@@ -144,6 +144,7 @@ class ServeController:
         self.ingress: Dict[str, str] = {}
         self.route_prefixes: Dict[str, Optional[str]] = {}
         self.proxy = None
+        self.grpc_proxy = None
         self.jobs: Dict[str, Any] = {}            # app -> job segment handle (process mode)
         self.lock = threading.RLock()
         self.workdir = tempfile.mkdtemp(prefix="rdb_serve_")
@@ -163,7 +164,8 @@ class ServeController:
         self._thread.start()
         atexit.register(self.shutdown)
 
-    def configure(self, mode: str = None, http_options: Optional[Dict[str, Any]] = None, **_):
+    def configure(self, mode: str = None, http_options: Optional[Dict[str, Any]] = None,
+                  grpc_options: Optional[Dict[str, Any]] = None, **_):
         if mode:
             self.default_mode = mode
         if http_options is not None and self.proxy is None:
@@ -171,6 +173,14 @@ class ServeController:
 
             self.proxy = HTTPProxy(self, http_options.get("host", "127.0.0.1"),
                                    int(http_options.get("port", 8000))).start()
+        if grpc_options is not None and self.grpc_proxy is None:
+            from .grpc_proxy import GRPCProxy
+
+            o = dict(grpc_options)
+            self.grpc_proxy = GRPCProxy(self, o.get("host", "127.0.0.1"), int(o.get("port", 9000)),
+                                        request_types=o.get("request_types"),
+                                        streaming_methods=o.get("streaming_methods", ()),
+                                        timeout_s=float(o.get("request_timeout_s", 600.0))).start()
 
     # ------------------------------------------------------------------ deploy
     def _resolve_mode(self, app: Application, mode: Optional[str]) -> str:
@@ -610,6 +620,9 @@ class ServeController:
         if self.proxy is not None:
             self.proxy.stop()
             self.proxy = None
+        if self.grpc_proxy is not None:
+            self.grpc_proxy.stop()
+            self.grpc_proxy = None
         self._stop.set()
         if self._thread.is_alive() and threading.current_thread() is not self._thread:
             self._thread.join(5.0)

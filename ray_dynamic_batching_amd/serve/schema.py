@@ -56,6 +56,9 @@ class ServeApplicationSchema(BaseModel):
 
 class ServeDeploySchema(BaseModel):
     applications: List[ServeApplicationSchema]
+    # proxies (serve/schema.py ServeDeploySchema.http_options / grpc_options)
+    http_options: Optional[Dict[str, Any]] = None     # {"host": ..., "port": ...}
+    grpc_options: Optional[Dict[str, Any]] = None     # {"host": ..., "port": ..., "streaming_methods": [...]}
 
     @classmethod
     def from_yaml(cls, path: str) -> "ServeDeploySchema":
