@@ -52,11 +52,11 @@ __global__ void fill_rand(bf16* p, size_t n, uint32_t seed, float scale) {
 struct Shape { int M, N, K; const char* name; };
 struct Variant { std::string name; std::function<void(const bf16*, const bf16*, const bf16*, bf16*, int, int, int, hipStream_t)> run; };
 
-template <int NW, int BM, int BN, int GM, int GN, int S, bool DIM = false>
+template <int NW, int BM, int BN, int GM, int GN, int S, int BK = 64>
 Variant pp(const char* nm) {
   return {nm, [](const bf16* A, const bf16* W, const bf16* b, bf16* C, int M, int N, int K, hipStream_t s) {
-            launch_gemm_pp<bf16, bf16, NW, BM, BN, GM, GN, S, DIM>(A, K, W, K, C, N, b, nullptr, 0, M, N, K, 1.f,
-                                                                    ACT_NONE, s);
+            launch_gemm_pp<bf16, bf16, NW, BM, BN, GM, GN, S, BK>(A, K, W, K, C, N, b, nullptr, 0, M, N, K, 1.f,
+                                                                   ACT_NONE, s);
           }};
 }
 Variant core(int cfg) {

@@ -229,8 +229,10 @@ struct StagedEpi {
   static_assert(BN % 8 == 0 && RC >= 16 && BM % RC == 0, "staged epilogue geometry");
 };
 
+// BIAS_LDS >= 0: the tile's bias was staged (f32) at smem + BIAS_LDS by the
+// kernel's prologue, so no bias registers stay live across the epilogue.
 template <typename T, typename OutT, int BM, int BN, int SMEM_BYTES, int NT, int TM, int TN, bool HAS_BIAS,
-          bool HAS_RES, typename ActF>
+          bool HAS_RES, typename ActF, int BIAS_LDS = -1>
 __device__ __forceinline__ void staged_epilogue(char* smem, const f32x4 (&acc)[TN][TM], int row_base, int col_base,
                                                 int m0, int n0, int M, int N, OutT* __restrict__ C, int ldc,
                                                 const T* __restrict__ bias, const T* __restrict__ R, int ldr,
@@ -239,11 +241,12 @@ __device__ __forceinline__ void staged_epilogue(char* smem, const f32x4 (&acc)[T
   const int tid = threadIdx.x, lane = tid & 63;
   const int fr = lane & 15, fg = lane >> 4;
   // bias in the fragment layout (TN x 8 B per lane), fetched once for all chunks
-  float bv[TN][4];
+  constexpr bool BREG = HAS_BIAS && BIAS_LDS < 0;
+  float bv[BREG ? TN : 1][4];
 #pragma unroll
-  for (int i = 0; i < TN; ++i) {
+  for (int i = 0; i < (BREG ? TN : 0); ++i) {
     const int n = n0 + col_base + i * 16 + fg * 4;
-    if constexpr (HAS_BIAS) {
+    if constexpr (BREG) {
       const __amdgpu_buffer_rsrc_t bsrc = make_rsrc(bias, (uint32_t)(N * sizeof(T)));
       const u32x2 raw = bload8(bsrc, (uint32_t)(n * sizeof(T)));
       const T* e = reinterpret_cast<const T*>(&raw);
@@ -264,9 +267,13 @@ __device__ __forceinline__ void staged_epilogue(char* smem, const f32x4 (&acc)[T
 #pragma unroll
         for (int i = 0; i < TN; ++i) {
           const int nt = col_base + i * 16 + fg * 4;
-          f32x4 v;
+          f32x4 v = acc[i][j] * alpha;
+          if constexpr (BREG) {
 #pragma unroll
-          for (int q = 0; q < 4; ++q) v[q] = alpha * acc[i][j][q] + bv[i][q];
+            for (int q = 0; q < 4; ++q) v[q] += bv[i][q];
+          } else if constexpr (HAS_BIAS) {
+            v += *reinterpret_cast<const f32x4*>(smem + BIAS_LDS + nt * 4);
+          }
           *reinterpret_cast<f32x4*>(smem + rt * E::ROWB + nt * 4) = v;
         }
       }
@@ -655,13 +662,15 @@ namespace rdb {
 // CUs x blocks/CU -- hence the non-power-of-two tiles: 128x192 (N = 3072),
 // 128x144 (N = 2304), 64x96 / 128x48 (N = 768) each give exactly 512 tiles
 // at M = 4096 (BERT-base, batch 32).
-// 19..21 are the ping-pong kernel (gemm_pp.h, 8 waves in two staggered groups).
-constexpr int kNumTiles = 22;
-//                                 0    1    2    3    4    5    6    7    8    9   10   11   12 | 8-wave: 13   14   15   16   17   18 | pp: 19   20   21
-constexpr int kTileBM[kNumTiles] = {128, 64, 128, 64, 128, 192, 256, 128, 128, 64, 128, 256, 128, 256, 128, 256, 256, 128, 256, 256, 256, 128};
-constexpr int kTileBN[kNumTiles] = {128, 128, 64, 64, 192, 128, 128, 256, 144, 96, 96, 144, 48, 128, 256, 192, 144, 96, 96, 128, 144, 256};
-constexpr int kTileWGM[kNumTiles] = {2, 2, 2, 2, 2, 2, 2, 2, 4, 2, 2, 4, 4, 4, 2, 4, 8, 4, 8, 4, 8, 2};
-constexpr int kTileNW[kNumTiles] = {4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 8, 8, 8, 8, 8, 8, 8, 8, 8};
+// 19..22 are the ping-pong kernel (gemm_pp.h, 8 waves in two staggered groups;
+// 22 = 256x256 at BK = 32 with 4 LDS stages, the best tile on large GEMMs:
+// 1.06 PF/s at 4096^3 vs 0.90 for 19, bench/gemm_lab).
+constexpr int kNumTiles = 23;
+//                                 0    1    2    3    4    5    6    7    8    9   10   11   12 | 8-wave: 13   14   15   16   17   18 | pp: 19   20   21   22
+constexpr int kTileBM[kNumTiles] = {128, 64, 128, 64, 128, 192, 256, 128, 128, 64, 128, 256, 128, 256, 128, 256, 256, 128, 256, 256, 256, 128, 256};
+constexpr int kTileBN[kNumTiles] = {128, 128, 64, 64, 192, 128, 128, 256, 144, 96, 96, 144, 48, 128, 256, 192, 144, 96, 96, 128, 144, 256, 256};
+constexpr int kTileWGM[kNumTiles] = {2, 2, 2, 2, 2, 2, 2, 2, 4, 2, 2, 4, 4, 4, 2, 4, 8, 4, 8, 4, 8, 2, 4};
+constexpr int kTileNW[kNumTiles] = {4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 8, 8, 8, 8, 8, 8, 8, 8, 8, 8};
 
 inline int tile_blocks_per_cu(int cfg) {
   if (cfg >= 19) return 1;
@@ -710,6 +719,9 @@ void launch_mfma_gemm_t(const P& ap, const T* W, int ldw, OutT* C, int ldc, cons
     // f32 output is only used by small heads: one tile shape
     launch_one<T, OutT, LoaderT, HB, HR, 64, 64>(ap, W, ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act, s);
   } else {
+    // the ping-pong tiles (19..) take plain staged epilogues only: deferred-LN modes,
+    // SwiGLU and unaligned / N % 8 != 0 outputs run the 8-wave 256x192 tile instead
+    if (cfg >= 19 && (EPI != 0 || !gemm_pp_ok(N, ldc, ldr, C, bias, R, act))) cfg = 15;
     switch (cfg) {
       RDB_TILE(0, 128, 128, 2, 4)
       RDB_TILE(1, 64, 128, 2, 4)
@@ -736,8 +748,7 @@ void launch_mfma_gemm_t(const P& ap, const T* W, int ldw, OutT* C, int ldc, cons
         RDB_TILE(18, 256, 96, 8, 8)
         default: break;
       }
-      if constexpr (EPI == 0) {
-        // ping-pong kernel: plain epilogues only (the deferred-LN modes stay on the tiles above)
+      if constexpr (EPI == 0 && sizeof(OutT) == 2) {
         switch (cfg) {
           case 19: launch_gemm_pp<T, OutT, 8, 256, 128, 2, 2, 3>(static_cast<const T*>(ap.A), ap.lda, W, ldw, C, ldc,
                                                                   bias, R, ldr, M, N, K, alpha, act, s);
@@ -747,6 +758,9 @@ void launch_mfma_gemm_t(const P& ap, const T* W, int ldw, OutT* C, int ldc, cons
             return;
           case 21: launch_gemm_pp<T, OutT, 8, 128, 256, 1, 4, 3>(static_cast<const T*>(ap.A), ap.lda, W, ldw, C, ldc,
                                                                   bias, R, ldr, M, N, K, alpha, act, s);
+            return;
+          case 22: launch_gemm_pp<T, OutT, 8, 256, 256, 2, 2, 4, 32>(static_cast<const T*>(ap.A), ap.lda, W, ldw, C,
+                                                                      ldc, bias, R, ldr, M, N, K, alpha, act, s);
             return;
           default: break;
         }

@@ -41,30 +41,41 @@ namespace rdb {
 __device__ unsigned long long* rdb_pp_stamps;
 #endif
 
-template <int NW, int BM, int BN>
+template <int NW, int BM, int BN, int BK_>
 struct PPGeom {
-  static constexpr int BK = 64;
+  static constexpr int BK = BK_;                             // 32 or 64
   static constexpr int NT = 64 * NW;
-  static constexpr int A_PIECES = BM / 8;                    // 1-KiB DMA pieces (8 rows x 128 B)
-  static constexpr int W_PIECES = (BN + 7) / 8;
+  static constexpr int ROWB = BK * 2;                        // LDS bytes per tile row
+  static constexpr int CPR = BK / 8;                         // 16-B chunks per row
+  static constexpr int PR = 1024 / ROWB;                     // rows per 1-KiB DMA piece
+  static constexpr int A_PIECES = BM / PR;
+  static constexpr int W_PIECES = (BN + PR - 1) / PR;
   static constexpr int A_PW = A_PIECES / NW;                 // pieces per wave
   static constexpr int W_PW = (W_PIECES + NW - 1) / NW;      // rounded up: surplus pieces go to a dummy slot
   static constexpr bool DUMMY = W_PW * NW != W_PIECES;       // (every wave issues the same count: one vmcnt)
   static constexpr int LOADS = A_PW + W_PW;                  // DMA instructions per wave per tile
-  static constexpr int W_OFF = BM * BK * 2;
+  static constexpr int W_OFF = BM * ROWB;
   static constexpr int DUMMY_OFF = W_OFF + W_PIECES * 1024;
   static constexpr int STAGE_BYTES = DUMMY_OFF + (DUMMY ? 1024 : 0);
-  static_assert(BM % (8 * NW) == 0, "A tile must split into whole pieces per wave");
+  static_assert(BK == 32 || BK == 64, "BK 32 or 64");
+  static_assert(BM % (PR * NW) == 0, "A tile must split into whole pieces per wave");
+  // XOR swizzle of the 16-B chunk index so each 16-lane group of ds_read_b128
+  // (16 consecutive rows, one logical chunk) hits 16 distinct bank quads:
+  // 128-B rows pair up per bank row -> chunk ^ ((row>>1)&7); 64-B rows come
+  // four per bank row -> chunk ^ ((row>>2)&3).
+  static __device__ __forceinline__ int swz(int row) { return BK == 64 ? ((row >> 1) & 7) : ((row >> 2) & 3); }
+  static __device__ __forceinline__ int off(int row, int chunk) { return row * ROWB + ((chunk ^ swz(row)) << 4); }
 };
 
 template <typename T, typename OutT, int NW, int BM, int BN, int GM, int GN, int STAGES, bool HAS_BIAS, bool HAS_RES,
-          bool DIM = false>
+          int BK_ = 64>
 __global__ void __launch_bounds__(64 * NW, 2)
 gemm_pp_kernel(const T* __restrict__ A, int lda, const T* __restrict__ W, int ldw, OutT* __restrict__ C, int ldc,
                const T* __restrict__ bias, const T* __restrict__ R, int ldr, int M, int N, int K, float alpha,
                int act) {
-  typedef PPGeom<NW, BM, BN> G;
+  typedef PPGeom<NW, BM, BN, BK_> G;
   constexpr int BK = G::BK;
+  constexpr int KS = BK / 32;                // MFMA k-steps per tile
   constexpr int GW = NW / 2;                 // waves per group
   static_assert(GM * GN == GW, "group wave layout");
   constexpr int GBM = BM / 2;                // rows per group
@@ -75,7 +86,9 @@ gemm_pp_kernel(const T* __restrict__ A, int lda, const T* __restrict__ W, int ld
   static_assert(STAGES >= 3 && (STAGES - 2) * L < 64, "pipeline depth / vmcnt field");
   typedef typename MfmaOp<T>::frag frag;
 
-  __shared__ __attribute__((aligned(16))) char smem[STAGES * G::STAGE_BYTES];
+  // staging buffers, then the tile's bias as f32 (read by the epilogue)
+  constexpr int BIAS_OFF = STAGES * G::STAGE_BYTES;
+  __shared__ __attribute__((aligned(16))) char smem[BIAS_OFF + (HAS_BIAS ? BN * 4 : 0)];
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int grp = wid / GW, gw = wid % GW;
@@ -94,15 +107,15 @@ gemm_pp_kernel(const T* __restrict__ A, int lda, const T* __restrict__ W, int ld
   int ach[G::A_PW], wch[G::W_PW];
 #pragma unroll
   for (int i = 0; i < G::A_PW; ++i) {
-    const int row = (wid * G::A_PW + i) * 8 + (lane >> 3);
-    ach[i] = (lane & 7) ^ ((row >> 1) & 7);
+    const int row = (wid * G::A_PW + i) * G::PR + lane / G::CPR;
+    ach[i] = (lane % G::CPR) ^ G::swz(row);
     const int gm = m0 + row;
     aoff[i] = gm < M ? (uint32_t)((size_t)gm * lda * sizeof(T)) : kOOB;
   }
 #pragma unroll
   for (int i = 0; i < G::W_PW; ++i) {
-    const int row = (wid * G::W_PW + i) * 8 + (lane >> 3);
-    wch[i] = (lane & 7) ^ ((row >> 1) & 7);
+    const int row = (wid * G::W_PW + i) * G::PR + lane / G::CPR;
+    wch[i] = (lane % G::CPR) ^ G::swz(row);
     const int gn = n0 + row;
     woff[i] = (row < BN && gn < N) ? (uint32_t)((size_t)gn * ldw * sizeof(T)) : kOOB;
   }
@@ -124,19 +137,6 @@ gemm_pp_kernel(const T* __restrict__ A, int lda, const T* __restrict__ W, int ld
     }
   };
 
-  // one DMA piece (p < A_PW: A, else W) of tile k0 into buffer buf
-  auto stage_piece = [&](int buf, int k0, int p) {
-    char* base = smem + buf * G::STAGE_BYTES;
-    if (p < G::A_PW) {
-      const int gk = k0 + ach[p] * 8;
-      dma16(asrc, base + (wid_u * G::A_PW + p) * 1024, (gk < K && aoff[p] != kOOB) ? aoff[p] + (uint32_t)(gk * sizeof(T)) : kOOB);
-    } else {
-      const int i = p - G::A_PW;
-      const int gk = k0 + wch[i] * 8;
-      dma16(wsrc, wdst(base, i), (gk < K && woff[i] != kOOB) ? woff[i] + (uint32_t)(gk * sizeof(T)) : kOOB);
-    }
-  };
-
   f32x4 acc[TN][TM];
 #pragma unroll
   for (int i = 0; i < TN; ++i)
@@ -146,46 +146,26 @@ gemm_pp_kernel(const T* __restrict__ A, int lda, const T* __restrict__ W, int ld
   const int fr = lane & 15, fg = lane >> 4;
   const int arow0 = grp * GBM + wm * WM + fr;   // this lane's fragment rows in the A / W tiles
   const int wrow0 = wn * WN + fr;
-  frag af[2][TM], wf[2][TN];
+  frag af[KS][TM], wf[KS][TN];
   auto read_tile = [&](int buf) {
     const char* sa = smem + buf * G::STAGE_BYTES;
     const char* sw = sa + G::W_OFF;
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
+    for (int ks = 0; ks < KS; ++ks) {
       const int chunk = ks * 4 + fg;
 #pragma unroll
-      for (int i = 0; i < TN; ++i) wf[ks][i] = *reinterpret_cast<const frag*>(sw + swz_off(wrow0 + i * 16, chunk));
+      for (int i = 0; i < TN; ++i) wf[ks][i] = *reinterpret_cast<const frag*>(sw + G::off(wrow0 + i * 16, chunk));
 #pragma unroll
-      for (int j = 0; j < TM; ++j) af[ks][j] = *reinterpret_cast<const frag*>(sa + swz_off(arow0 + j * 16, chunk));
+      for (int j = 0; j < TM; ++j) af[ks][j] = *reinterpret_cast<const frag*>(sa + G::off(arow0 + j * 16, chunk));
     }
   };
   auto mfma_tile = [&]() {
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
+    for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
       for (int i = 0; i < TN; ++i)
 #pragma unroll
         for (int j = 0; j < TM; ++j) acc[i][j] = MfmaOp<T>::mma(wf[ks][i], af[ks][j], acc[i][j]);
-  };
-  // DIM: the next tile's DMA pieces are issued BETWEEN this tile's MFMAs (evenly
-  // spread), so the read interval carries only the ds_reads
-  constexpr int NMF = 2 * TN * TM;
-  constexpr int EVERY = NMF / L > 0 ? NMF / L : 1;
-  auto mfma_tile_dma = [&](int dbuf, int dk0) {
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-      for (int i = 0; i < TN; ++i)
-#pragma unroll
-        for (int j = 0; j < TM; ++j) {
-          acc[i][j] = MfmaOp<T>::mma(wf[ks][i], af[ks][j], acc[i][j]);
-          const int c = (ks * TN + i) * TM + j;
-          if (c % EVERY == EVERY - 1 && c / EVERY < L) stage_piece(dbuf, dk0, c / EVERY);
-        }
-    if constexpr (EVERY * L > NMF) {   // pieces left over (L > NMF): after the last MFMA
-#pragma unroll
-      for (int p = NMF / EVERY; p < L; ++p) stage_piece(dbuf, dk0, p);
-    }
   };
   // sched_barrier(0) pins the intervals: no MFMA may be hoisted into a read
   // interval (or LDS read sunk into a matrix interval) across a block barrier
@@ -207,6 +187,17 @@ gemm_pp_kernel(const T* __restrict__ A, int lda, const T* __restrict__ W, int ld
   unsigned long long* stp = rdb_pp_stamps + (size_t)blockIdx.x * 8;
   const unsigned long long t_start = __builtin_amdgcn_s_memtime();
 #endif
+  if constexpr (HAS_BIAS) {
+    // bias -> LDS (f32), visible after the prologue barrier.  Issued BEFORE the
+    // first DMA: hipcc waits vmcnt(0) at the use of an ordinary load while an
+    // LDS-DMA is in flight, which here would drain the prologue tiles.
+    for (int q = tid; q < BN / 4; q += G::NT) {
+      const __amdgpu_buffer_rsrc_t bsrc = make_rsrc(bias, (uint32_t)(N * sizeof(T)));
+      const u32x2 raw = bload8(bsrc, (uint32_t)((n0 + q * 4 < N ? n0 + q * 4 : N) * sizeof(T)));
+      const T* e = reinterpret_cast<const T*>(&raw);
+      *reinterpret_cast<f32x4*>(smem + BIAS_OFF + q * 16) = f32x4{(float)e[0], (float)e[1], (float)e[2], (float)e[3]};
+    }
+  }
   // prologue: tiles 0 .. STAGES-2 in flight, tile 0 retired and visible
 #pragma unroll
   for (int s = 0; s < STAGES - 1; ++s)
@@ -220,218 +211,76 @@ gemm_pp_kernel(const T* __restrict__ A, int lda, const T* __restrict__ W, int ld
   if (grp == 1) barrier();   // stagger: group 1 one interval behind
 
   int buf = 0;
-  if constexpr (!DIM) {
-    for (int kt = 0; kt < nk; ++kt) {
-      // ---- read interval: fragments of tile kt, DMA of tile kt+STAGES-1 ----
-      read_tile(buf);
-      const bool steady = kt + STAGES - 1 < nk;
-      if (steady) stage((kt + STAGES - 1) % STAGES, (kt + STAGES - 1) * BK);
-      __builtin_amdgcn_s_waitcnt(kLgkm0);           // my reads of this buffer are done (WAR)
-      if (steady) __builtin_amdgcn_s_waitcnt(kVmSteady);  // my pieces of tile kt+1 landed (RAW)
-      else __builtin_amdgcn_s_waitcnt(kVm0);
-      barrier();
-      // ---- matrix interval ----
-      __builtin_amdgcn_s_setprio(1);
-      mfma_tile();
-      __builtin_amdgcn_s_setprio(0);
-      barrier();
-      buf = buf == STAGES - 1 ? 0 : buf + 1;
-    }
-  } else {
-    // DMA of tile kt+STAGES-1 rides tile kt's matrix interval.  RAW: every wave
-    // retires its pieces of tile kt+1 before the barrier that opens group 0's
-    // read of it -- group 0 at the end of its matrix interval of tile kt
-    // (STAGES-2 younger tiles may stay in flight), group 1 at the end of its
-    // read interval of tile kt (its matrix interval of kt comes later: STAGES-3).
-    // WAR: buffer (kt-1)%STAGES was last read in the read intervals of tile
-    // kt-1, both of which end (lgkmcnt(0)) before the first matrix interval of
-    // tile kt starts.
-    constexpr int kVmG1 = (((STAGES - 3) * L) & 15) | ((((STAGES - 3) * L) >> 4) << 14) | 0x70 | 0xF00;
-    for (int kt = 0; kt < nk; ++kt) {
-      const bool steady = kt + STAGES - 1 < nk;
-      read_tile(buf);
-      __builtin_amdgcn_s_waitcnt(kLgkm0);
-      if (grp == 1) {
-        if (steady) __builtin_amdgcn_s_waitcnt(kVmG1);
-        else __builtin_amdgcn_s_waitcnt(kVm0);
-      }
-      barrier();
-      __builtin_amdgcn_s_setprio(1);
-      if (steady) mfma_tile_dma((kt + STAGES - 1) % STAGES, (kt + STAGES - 1) * BK);
-      else mfma_tile();
-      __builtin_amdgcn_s_setprio(0);
-      if (grp == 0) {
-        if (steady) __builtin_amdgcn_s_waitcnt(kVmSteady);
-        else __builtin_amdgcn_s_waitcnt(kVm0);
-      }
-      barrier();
-      buf = buf == STAGES - 1 ? 0 : buf + 1;
-    }
+  for (int kt = 0; kt < nk; ++kt) {
+    // ---- read interval: fragments of tile kt, DMA of tile kt+STAGES-1 ----
+    read_tile(buf);
+    const bool steady = kt + STAGES - 1 < nk;
+    if (steady) stage((kt + STAGES - 1) % STAGES, (kt + STAGES - 1) * BK);
+    __builtin_amdgcn_s_waitcnt(kLgkm0);           // my reads of this buffer are done (WAR)
+    if (steady) __builtin_amdgcn_s_waitcnt(kVmSteady);  // my pieces of tile kt+1 landed (RAW)
+    else __builtin_amdgcn_s_waitcnt(kVm0);
+    barrier();
+    // ---- matrix interval ----
+    __builtin_amdgcn_s_setprio(1);
+    mfma_tile();
+    __builtin_amdgcn_s_setprio(0);
+    barrier();
+    buf = buf == STAGES - 1 ? 0 : buf + 1;
   }
   if (grp == 0) barrier();
 #ifdef RDB_PP_STAMPS
   const unsigned long long t_loop = __builtin_amdgcn_s_memtime();
 #endif
 
-  // ---- epilogue ----
-  if constexpr (sizeof(OutT) == 2) {
-    if (act != ACT_SWIGLU && staged_epilogue_ok<T, OutT, HAS_RES>(N, C, ldc, bias, R, ldr)) {
-      constexpr int SB = STAGES * G::STAGE_BYTES;
-      auto go = [&](auto actf) {
-        staged_epilogue<T, OutT, BM, BN, SB, G::NT, TM, TN, HAS_BIAS, HAS_RES>(smem, acc, grp * GBM + wm * WM, wn * WN,
-                                                                               m0, n0, M, N, C, ldc, bias, R, ldr, alpha,
-                                                                               actf);
-      };
-      switch (act) {
-        case ACT_GELU: go([](float x) { return apply_act<ACT_GELU>(x); }); break;
-        case ACT_RELU: go([](float x) { return apply_act<ACT_RELU>(x); }); break;
-        case ACT_TANH: go([](float x) { return apply_act<ACT_TANH>(x); }); break;
-        case ACT_SILU: go([](float x) { return apply_act<ACT_SILU>(x); }); break;
-        case ACT_GELU_TANH: go([](float x) { return apply_act<ACT_GELU_TANH>(x); }); break;
-        case ACT_SIGMOID: go([](float x) { return apply_act<ACT_SIGMOID>(x); }); break;
-        default: go([](float x) { return x; }); break;
-      }
-#ifdef RDB_PP_STAMPS
-      if (tid == 0) {
-        stp[0] = t_start;
-        stp[1] = t_pro;
-        stp[2] = t_loop;
-        stp[3] = __builtin_amdgcn_s_memtime();
-      }
-#endif
-      return;
-    }
-  }
-  // direct epilogue: lane holds C[m][n..n+3] of every fragment
-  const bool swiglu = act == ACT_SWIGLU;
-  const int n_out = swiglu ? (N >> 1) : N;
-  float bv[TN][4];
-#pragma unroll
-  for (int i = 0; i < TN; ++i) {
-    const int n = n0 + wn * WN + i * 16 + fg * 4;
-    if constexpr (HAS_BIAS) {
-      const __amdgpu_buffer_rsrc_t bsrc = make_rsrc(bias, (uint32_t)(N * sizeof(T)));
-      const u32x2 raw = bload8(bsrc, (uint32_t)(n * sizeof(T)));
-      const T* e = reinterpret_cast<const T*>(&raw);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) bv[i][q] = (float)e[q];
-    } else {
-#pragma unroll
-      for (int q = 0; q < 4; ++q) bv[i][q] = 0.f;
-    }
-  }
-  u32x2 rraw[TM][TN];
-  if constexpr (HAS_RES) {
-    const __amdgpu_buffer_rsrc_t rsrc = make_rsrc(R, (uint32_t)((size_t)(M - 1) * ldr * sizeof(T) + (size_t)n_out * sizeof(T)));
-#pragma unroll
-    for (int j = 0; j < TM; ++j) {
-      const int m = m0 + grp * GBM + wm * WM + j * 16 + fr;
-#pragma unroll
-      for (int i = 0; i < TN; ++i) {
-        const int n = n0 + wn * WN + i * 16 + fg * 4;
-        if (!swiglu) {
-          const uint32_t off = (m < M && n < N) ? (uint32_t)(((size_t)m * ldr + n) * sizeof(T)) : kOOB;
-          rraw[j][i] = bload8(rsrc, off);
-        } else {
-          const uint32_t off = (m < M && n < N) ? (uint32_t)(((size_t)m * ldr + (n >> 1)) * sizeof(T)) : kOOB;
-          rraw[j][i] = u32x2{bload4(rsrc, off), 0u};
-        }
-      }
-    }
-  }
-  auto rv = [&](int j, int i, int q) -> float {
-    const T* e = reinterpret_cast<const T*>(&rraw[j][i]);
-    return (float)e[q];
-  };
-  if (swiglu) {
-#pragma unroll
-    for (int j = 0; j < TM; ++j) {
-      const int m = m0 + grp * GBM + wm * WM + j * 16 + fr;
-#pragma unroll
-      for (int i = 0; i < TN; ++i) {
-        const int n = n0 + wn * WN + i * 16 + fg * 4;
-        float x[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) x[q] = alpha * acc[i][j][q] + bv[i][q];
-        float r0 = apply_act<ACT_SILU>(x[0]) * x[1];
-        float r1 = apply_act<ACT_SILU>(x[2]) * x[3];
-        if constexpr (HAS_RES) { r0 += rv(j, i, 0); r1 += rv(j, i, 1); }
-        if (m < M && n < N) {
-          OutT* cp = C + (size_t)m * ldc + (n >> 1);
-          cp[0] = (OutT)r0;
-          cp[1] = (OutT)r1;
-        }
-      }
-    }
-    return;
-  }
-  const bool vec_ok = ((ldc & 3) == 0);
-  auto store_tile = [&](auto actf) {
-#pragma unroll
-    for (int j = 0; j < TM; ++j) {
-      const int m = m0 + grp * GBM + wm * WM + j * 16 + fr;
-#pragma unroll
-      for (int i = 0; i < TN; ++i) {
-        const int n = n0 + wn * WN + i * 16 + fg * 4;
-        float y[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          float x = alpha * acc[i][j][q] + bv[i][q];
-          if constexpr (HAS_RES) x += rv(j, i, q);
-          y[q] = actf(x);
-        }
-        if (m >= M || n >= N) continue;
-        OutT* cp = C + (size_t)m * ldc + n;
-        if (n + 3 < N && vec_ok) {
-          store4<OutT>(cp, y[0], y[1], y[2], y[3]);
-        } else {
-#pragma unroll
-          for (int e = 0; e < 4; ++e)
-            if (n + e < N) cp[e] = (OutT)y[e];
-        }
-      }
-    }
+  // ---- epilogue: LDS-staged, row-coalesced (launch_gemm_pp's caller guarantees
+  // its requirements: 16-bit output, N % 8 == 0, no SwiGLU, 16-B alignment) ----
+  static_assert(sizeof(OutT) == 2, "ping-pong GEMM stores 16-bit outputs");
+  constexpr int SB = STAGES * G::STAGE_BYTES;
+  auto go = [&](auto actf) {
+    staged_epilogue<T, OutT, BM, BN, SB, G::NT, TM, TN, HAS_BIAS, HAS_RES, decltype(actf), BIAS_OFF>(
+        smem, acc, grp * GBM + wm * WM, wn * WN, m0, n0, M, N, C, ldc, bias, R, ldr, alpha, actf);
   };
   switch (act) {
-    case ACT_GELU: store_tile([](float x) { return apply_act<ACT_GELU>(x); }); break;
-    case ACT_RELU: store_tile([](float x) { return apply_act<ACT_RELU>(x); }); break;
-    case ACT_TANH: store_tile([](float x) { return apply_act<ACT_TANH>(x); }); break;
-    case ACT_SILU: store_tile([](float x) { return apply_act<ACT_SILU>(x); }); break;
-    case ACT_GELU_TANH: store_tile([](float x) { return apply_act<ACT_GELU_TANH>(x); }); break;
-    case ACT_SIGMOID: store_tile([](float x) { return apply_act<ACT_SIGMOID>(x); }); break;
-    default: store_tile([](float x) { return x; }); break;
+    case ACT_GELU: go([](float x) { return apply_act<ACT_GELU>(x); }); break;
+    case ACT_RELU: go([](float x) { return apply_act<ACT_RELU>(x); }); break;
+    case ACT_TANH: go([](float x) { return apply_act<ACT_TANH>(x); }); break;
+    case ACT_SILU: go([](float x) { return apply_act<ACT_SILU>(x); }); break;
+    case ACT_GELU_TANH: go([](float x) { return apply_act<ACT_GELU_TANH>(x); }); break;
+    case ACT_SIGMOID: go([](float x) { return apply_act<ACT_SIGMOID>(x); }); break;
+    default: go([](float x) { return x; }); break;
   }
 #ifdef RDB_PP_STAMPS
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (tid == 0) {
-    unsigned xcc;
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
     stp[0] = t_start;
     stp[1] = t_pro;
     stp[2] = t_loop;
     stp[3] = __builtin_amdgcn_s_memtime();
-    stp[4] = xcc & 0xf;
-    stp[5] = __builtin_amdgcn_s_memrealtime();
   }
 #endif
 }
 
-template <typename T, typename OutT, int NW, int BM, int BN, int GM, int GN, int STAGES, bool DIM = false>
+// Host-side precondition of the ping-pong kernels' staged epilogue.
+inline bool gemm_pp_ok(int N, int ldc, int ldr, const void* C, const void* bias, const void* R, int act) {
+  auto al = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+  return act != ACT_SWIGLU && N % 8 == 0 && ldc % 8 == 0 && al(C) && (R == nullptr || (ldr % 8 == 0 && al(R)));
+}
+
+template <typename T, typename OutT, int NW, int BM, int BN, int GM, int GN, int STAGES, int BK = 64>
 void launch_gemm_pp(const T* A, int lda, const T* W, int ldw, OutT* C, int ldc, const T* bias, const T* R, int ldr,
                     int M, int N, int K, float alpha, int act, hipStream_t s) {
   const int nwg = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
   const dim3 grid(nwg), block(64 * NW);
   if (bias && R)
-    hipLaunchKernelGGL((gemm_pp_kernel<T, OutT, NW, BM, BN, GM, GN, STAGES, true, true, DIM>), grid, block, 0, s, A, lda, W,
+    hipLaunchKernelGGL((gemm_pp_kernel<T, OutT, NW, BM, BN, GM, GN, STAGES, true, true, BK>), grid, block, 0, s, A, lda, W,
                        ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act);
   else if (bias)
-    hipLaunchKernelGGL((gemm_pp_kernel<T, OutT, NW, BM, BN, GM, GN, STAGES, true, false, DIM>), grid, block, 0, s, A, lda, W,
+    hipLaunchKernelGGL((gemm_pp_kernel<T, OutT, NW, BM, BN, GM, GN, STAGES, true, false, BK>), grid, block, 0, s, A, lda, W,
                        ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act);
   else if (R)
-    hipLaunchKernelGGL((gemm_pp_kernel<T, OutT, NW, BM, BN, GM, GN, STAGES, false, true, DIM>), grid, block, 0, s, A, lda, W,
+    hipLaunchKernelGGL((gemm_pp_kernel<T, OutT, NW, BM, BN, GM, GN, STAGES, false, true, BK>), grid, block, 0, s, A, lda, W,
                        ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act);
   else
-    hipLaunchKernelGGL((gemm_pp_kernel<T, OutT, NW, BM, BN, GM, GN, STAGES, false, false, DIM>), grid, block, 0, s, A, lda,
+    hipLaunchKernelGGL((gemm_pp_kernel<T, OutT, NW, BM, BN, GM, GN, STAGES, false, false, BK>), grid, block, 0, s, A, lda,
                        W, ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act);
 }
 

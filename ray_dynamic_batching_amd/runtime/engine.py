@@ -106,6 +106,8 @@ class EngineRunner:
                 # LayerNorm kernels already hide under the other stream's GEMMs
                 # (profiles/bert_fold_ln_ab.json)
                 m.fold_ln = self.compute_streams == 1
+                if os.environ.get("RDB_FOLD_LN") in ("0", "1"):      # A/B override
+                    m.fold_ln = os.environ["RDB_FOLD_LN"] == "1"
             if hasattr(m, "refresh_folded_weights"):
                 m.refresh_folded_weights()   # graphs capture weights derived from the CURRENT ones
             buckets = sorted(set(s.buckets or default_buckets(s.max_batch)))
