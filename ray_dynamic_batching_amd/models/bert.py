@@ -4,13 +4,15 @@ The north-star serving model (BASELINE.json: "BERT-base seq128 bf16").  The
 ``hip`` backend runs every op of the batched forward on the hand-written
 kernels of :mod:`ray_dynamic_batching_amd.ops`:
 
-  embed_ln (gather + LN fused) -> 12 x [ QKV GEMM(+bias) -> fused attention
-  (reads the packed QKV, key-padding mask from per-row lengths) -> out GEMM
+  embed_ln (gather + LN fused) -> 12 x [ QKV GEMM(+bias) + attention in ONE
+  kernel per layer (ops.qkv_attention: each (sequence, head) block projects
+  its q/k/v tile and attends in LDS, key-padding mask from per-row lengths;
+  S > 128 falls back to GEMM -> ops.attention) -> out GEMM
   (+bias +residual) -> LN -> FFN1 GEMM(+bias +GELU) -> FFN2 GEMM(+bias
   +residual) -> LN ] -> pooler GEMM(+tanh) on the strided CLS rows ->
   classifier GEMM (f32 logits)
 
-so one layer is 7 kernel launches and the whole forward is 87; it is captured
+so one layer is 6 kernel launches; it is captured
 once per batch bucket into a hipGraph by the replica engine.  The ``torch``
 backend is the eager PyTorch baseline (what the reference's serving path
 runs: ``model(inputs)`` at scheduler.py:450).
@@ -69,10 +71,15 @@ class BertForSequenceClassification:
         # carry it, no LayerNorm kernel runs inside the layer stack
         # (RDB_BERT_FOLD_LN=1/0 forces it; by default a replica engine enables it
         # only with one compute stream -- see EngineRunner.build)
+        # fused QKV projection + attention (ops.qkv_attention, S <= 128): the QKV
+        # activation is never materialised; RDB_BERT_FUSED_ATTN=0 runs the
+        # two-kernel path (GEMM -> ops.attention)
+        self.fuse_qkv_attn = os.environ.get("RDB_BERT_FUSED_ATTN", "1") != "0"
         env = os.environ.get("RDB_BERT_FOLD_LN", "")
-        self.fold_ln = env != "0"
         self.fold_ln_auto = env == ""
+        self.fold_ln = env == "1" or (env == "" and self.auto_fold_ln(1))
         self._folded = None
+        self._packed = None
         g = torch.Generator(device="cpu").manual_seed(seed)
         D, I = cfg.hidden, cfg.intermediate
 
@@ -131,6 +138,17 @@ class BertForSequenceClassification:
             return self._forward_hip(ids)
         return self._forward_torch(ids)
 
+    def auto_fold_ln(self, compute_streams: int) -> bool:
+        """Default for ``fold_ln``.  The deferred-LN forward shortens a lone
+        batch's forward only against the two-kernel attention path (-1.5 % at
+        bs32 seq128, bench/bert_breakdown.py); the fused projection+attention
+        kernel (S <= 128) beats it by 12 %, and with several compute streams the
+        LayerNorm kernels hide under the other stream's GEMMs anyway
+        (profiles/bert_fold_ln_ab.json)."""
+        c = self.cfg
+        fused = self.fuse_qkv_attn and ops.qkv_attention_supported(c.seq_len, c.heads, c.hidden // c.heads, c.hidden)
+        return compute_streams == 1 and not fused
+
     def refresh_folded_weights(self):
         """Recompute the LayerNorm-folded weights (call after changing weights)."""
         self._folded = None
@@ -141,6 +159,15 @@ class BertForSequenceClassification:
         return tuple((t.data_ptr(), t._version) for L in self.layers
                      for t in (L["w_qkv"], L["b_qkv"], L["w_i"], L["b_i"], L["ln1_g"], L["ln1_b"],
                                L["ln2_g"], L["ln2_b"]))
+
+    def _packed_qkv(self):
+        """Head-major QKV weights for ops.qkv_attention, rebuilt when a source
+        tensor is swapped or modified in place."""
+        key = tuple((t.data_ptr(), t._version) for L in self.layers for t in (L["w_qkv"], L["b_qkv"]))
+        if self._packed is None or self._packed[0] != key:
+            H = self.cfg.heads
+            self._packed = (key, [ops.pack_qkv_heads(L["w_qkv"], L["b_qkv"], H) for L in self.layers])
+        return self._packed[1]
 
     def _folded_weights(self):
         key = self._fold_key()
@@ -169,9 +196,14 @@ class BertForSequenceClassification:
         lens = ops.seq_lens(ids, c.pad_token_id)
         h = ops.embed_ln(ids, self.word, self.pos, self.typ, self.emb_g, self.emb_b, c.eps)
         n = len(self.layers)
+        fuse = self.fuse_qkv_attn and ops.qkv_attention_supported(S, H, D // H, D)
+        packed = self._packed_qkv() if fuse else None
         for i, L in enumerate(self.layers):
-            qkv = ops.linear(h, L["w_qkv"], L["b_qkv"])
-            ctx = ops.attention(qkv, B, S, H, H, D // H, lens=lens)
+            if fuse:   # one kernel: projection tile of (sequence, head) -> attention in LDS
+                ctx = ops.qkv_attention(h.reshape(B * S, D), packed[i][0], packed[i][1], B, S, H, lens=lens)
+            else:
+                qkv = ops.linear(h, L["w_qkv"], L["b_qkv"])
+                ctx = ops.attention(qkv, B, S, H, H, D // H, lens=lens)
             if i == n - 1 and self.cls_only_last_layer:
                 # Only the [CLS] row of the last layer reaches the pooler: its
                 # keys/values need every token, but the o-proj, LN and FFN after

@@ -495,6 +495,66 @@ def attention(qkv: torch.Tensor, B: int, S: int, H: int, Hkv: int, D: int, lens:
     return out
 
 
+NUM_QKV_ATTN_CFGS = 3   # qkv_attention.hip: 8 waves x 3 stages, 8 x 2, 4 x 2
+QKV_ATTN_MAX_S = 128
+
+
+def pack_qkv_heads(w: torch.Tensor, b: torch.Tensor, H: int) -> Tuple[torch.Tensor, torch.Tensor]:
+    """[q | k | v] projection rows (nn.Linear [3*H*D, K] layout) -> head-major
+    [H*3*D, K]: rows h*3D + [0,D) = q_h, [D,2D) = k_h, [2D,3D) = v_h (and the
+    bias likewise) -- the operand layout of ``qkv_attention``."""
+    N, K = w.shape
+    _check(N % (3 * H) == 0 and b.numel() == N, "pack_qkv_heads: rows must be 3*H*D")
+    D = N // (3 * H)
+    wp = w.view(3, H, D, K).transpose(0, 1).reshape(N, K).contiguous()
+    bp = b.view(3, H, D).transpose(0, 1).reshape(N).contiguous()
+    return wp, bp
+
+
+def qkv_attention_supported(S: int, H: int, D: int, K: int) -> bool:
+    return 1 <= S <= QKV_ATTN_MAX_S and D == 64 and K % 8 == 0
+
+
+def qkv_attention(x: torch.Tensor, w_packed: torch.Tensor, b_packed: torch.Tensor, B: int, S: int, H: int,
+                  lens: Optional[torch.Tensor] = None, scale: Optional[float] = None,
+                  out: Optional[torch.Tensor] = None, cfg: int = -1) -> torch.Tensor:
+    """Fused QKV projection + bidirectional attention (qkv_attention.hip):
+    ctx [B*S, H*64] = MHA(x @ W^T + b) for S <= 128, head dim 64, with the
+    projection weight in ``pack_qkv_heads`` layout.  The [B*S, 3*H*64] QKV
+    activation is never materialised."""
+    _check(x.is_cuda and x.dtype in (torch.bfloat16, torch.float16) and x.dim() == 2 and x.stride(1) == 1,
+           "qkv_attention: x must be a 2-D [B*S, K] (row-strided) bf16/f16 view")
+    _check(w_packed.dtype == x.dtype and w_packed.is_contiguous() and b_packed.dtype == x.dtype
+           and b_packed.is_contiguous(), "qkv_attention: weight / bias dtype and layout")
+    N, K = w_packed.shape
+    _check(x.shape == (B * S, K), f"qkv_attention: x must be [B*S, K] = [{B * S}, {K}], got {tuple(x.shape)}")
+    _check(N == H * 192 and b_packed.numel() == N, "qkv_attention: packed weight must be [H*3*64, K]")
+    _check(qkv_attention_supported(S, H, 64, K), "qkv_attention: S <= 128, head dim 64, K % 8 == 0")
+    _check(x.stride(0) % 8 == 0 and _aligned(x) and _aligned(w_packed) and _aligned(b_packed, 8),
+           "qkv_attention: alignment")
+    if lens is not None:
+        _check(lens.dtype == torch.int32 and lens.numel() == B and lens.is_cuda, "qkv_attention: lens must be int32 [B]")
+    if out is None:
+        out = torch.empty(B * S, H * 64, device=x.device, dtype=x.dtype)
+    _check(out.is_contiguous() and out.shape == (B * S, H * 64) and _aligned(out), "qkv_attention: bad out")
+    scale = 1.0 / 8.0 if scale is None else scale
+    args = (DTYPE_CODE[x.dtype], x.data_ptr(), x.stride(0), w_packed.data_ptr(), b_packed.data_ptr(), B, S, H, K,
+            _ptr(lens), out.data_ptr(), H * 64, float(scale))
+    fn = _ops().qkv_attn_fwd
+    if cfg < 0:
+        key = ("qkv_attn", x.dtype, B, S, H, K, x.stride(0))
+        cfg = _tuned_cfg(key, lambda c: fn(*args, c, _stream()), range(NUM_QKV_ATTN_CFGS))
+    fn(*args, int(cfg), _stream())
+    return out
+
+
+def qkv_attention_ref(x, w, b, B, S, H, lens=None, scale=None):
+    """Unfused fp32 reference with the UNPACKED [q | k | v] weight; the projection
+    is rounded to x's dtype like the two-kernel path."""
+    qkv = F.linear(x.float(), w.float(), b.float()).to(x.dtype)
+    return attention_ref(qkv, B, S, H, H, w.shape[0] // (3 * H), lens=lens, scale=scale)
+
+
 def attention_ref(qkv, B, S, H, Hkv, D, lens=None, causal=False, scale=None, q_off=0, k_off=None, v_off=None):
     k_off = H * D if k_off is None else k_off
     v_off = (H + Hkv) * D if v_off is None else v_off

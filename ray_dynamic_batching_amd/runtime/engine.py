@@ -105,7 +105,8 @@ class EngineRunner:
                 # when batches overlap on several compute streams, where the
                 # LayerNorm kernels already hide under the other stream's GEMMs
                 # (profiles/bert_fold_ln_ab.json)
-                m.fold_ln = self.compute_streams == 1
+                m.fold_ln = m.auto_fold_ln(self.compute_streams) if hasattr(m, "auto_fold_ln") \
+                    else self.compute_streams == 1
                 if os.environ.get("RDB_FOLD_LN") in ("0", "1"):      # A/B override
                     m.fold_ln = os.environ["RDB_FOLD_LN"] == "1"
             if hasattr(m, "refresh_folded_weights"):

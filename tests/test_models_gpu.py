@@ -22,6 +22,35 @@ def test_bert_hip_matches_torch():
     assert torch.allclose(y, ref, atol=5e-2, rtol=5e-2), (y - ref).abs().max()
 
 
+def test_bert_fused_qkv_attention_matches_unfused_and_torch():
+    """LayerNorm-kernel forward with the fused projection+attention kernel ==
+    the two-kernel path == eager torch; an in-place weight update re-packs."""
+    from ray_dynamic_batching_amd.models.bert import BertConfig, BertForSequenceClassification
+
+    m = BertForSequenceClassification(BertConfig(layers=3), device="cuda", backend="hip", seed=6)
+    m.fold_ln = False
+    ids = m.example_input(8, seed=7)
+    ids[2, 70:] = 0
+    m.fuse_qkv_attn = True
+    y = m(ids)
+    m.fuse_qkv_attn = False
+    y2 = m(ids)
+    m.backend = "torch"
+    ref = m(ids)
+    assert torch.allclose(y, y2, atol=3e-2, rtol=3e-2), (y - y2).abs().max()
+    assert torch.allclose(y, ref, atol=5e-2, rtol=5e-2), (y - ref).abs().max()
+    # weights changed in place after a forward: the packed copy must follow
+    m.backend = "hip"
+    m.fuse_qkv_attn = True
+    for L in m.layers:
+        L["w_qkv"].mul_(1.5)
+        L["b_qkv"].add_(0.05)
+    y = m(ids)
+    m.backend = "torch"
+    ref = m(ids)
+    assert torch.allclose(y, ref, atol=5e-2, rtol=5e-2), (y - ref).abs().max()
+
+
 @pytest.mark.parametrize("cls_only", [True, False])
 def test_bert_folded_layernorm_matches_unfolded(cls_only):
     """The deferred-LayerNorm forward (ops.linear_ln) == the LayerNorm-kernel

@@ -135,6 +135,43 @@ def test_attention_spike_rescale():
     _close(ops.attention(qkv, B, S, H, H, D), ops.attention_ref(qkv, B, S, H, H, D), 2e-2, 2e-2)
 
 
+@pytest.mark.parametrize("B,S,H,K", [(4, 128, 12, 768), (3, 100, 4, 256), (2, 64, 2, 136), (1, 1, 1, 64)])
+@pytest.mark.parametrize("cfg", [0, 1, 2])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_qkv_attention(B, S, H, K, cfg, dtype):
+    """Fused projection + attention (qkv_attention.hip) == GEMM -> attention in fp32,
+    with padding lengths, every block-shape config, S < 128 (the 128-row tile
+    reaches into the next sequence / past the last row) and K not a multiple of 64."""
+    ops = _ops()
+    torch.manual_seed(11)
+    x = torch.randn(B * S, K, device="cuda", dtype=dtype)
+    w = torch.randn(3 * H * 64, K, device="cuda", dtype=dtype) * (K ** -0.5)
+    b = torch.randn(3 * H * 64, device="cuda", dtype=dtype) * 0.1
+    lens = torch.randint(1, S + 1, (B,), device="cuda", dtype=torch.int32)
+    lens[0] = S
+    wp, bp = ops.pack_qkv_heads(w, b, H)
+    for ln in (None, lens):
+        y = ops.qkv_attention(x, wp, bp, B, S, H, lens=ln, cfg=cfg)
+        ref = ops.qkv_attention_ref(x, w, b, B, S, H, lens=ln)
+        _close(y, ref, 2e-2, 2e-2)
+
+
+def test_qkv_attention_matches_two_kernel_path():
+    """The fused kernel against OUR unfused kernels (ops.linear -> ops.attention)
+    at the BERT-base shape, row-strided input included."""
+    ops = _ops()
+    torch.manual_seed(12)
+    B, S, H, D = 8, 128, 12, 768
+    big = torch.randn(B * S, D + 64, device="cuda", dtype=torch.bfloat16)
+    x = big[:, :D]                                      # row stride D + 64
+    w = torch.randn(3 * D, D, device="cuda", dtype=torch.bfloat16) * 0.03
+    b = torch.randn(3 * D, device="cuda", dtype=torch.bfloat16) * 0.1
+    wp, bp = ops.pack_qkv_heads(w, b, H)
+    y = ops.qkv_attention(x, wp, bp, B, S, H)
+    two = ops.attention(ops.linear(x, w, b), B, S, H, H, 64)
+    _close(y, two, 2e-2, 2e-2)
+
+
 def test_softmax_topk():
     ops = _ops()
     torch.manual_seed(6)
