@@ -187,8 +187,35 @@ class BertForSequenceClassification:
             self._folded = f
         return self._folded
 
+    def _deferred_weights(self):
+        """Per layer, for _forward_hip_fused_deferred: the packed QKV weight with
+        the previous layer's LN2 folded in (layer 0: plain) and FFN-up with LN1
+        folded in; rebuilt when a source tensor is swapped or modified."""
+        key = tuple((t.data_ptr(), t._version) for L in self.layers
+                    for t in (L["w_qkv"], L["b_qkv"], L["w_i"], L["b_i"], L["ln1_g"], L["ln1_b"],
+                              L["ln2_g"], L["ln2_b"]))
+        if getattr(self, "_deferred", None) is None or self._deferred[0] != key:
+            H = self.cfg.heads
+            out = []
+            for i, L in enumerate(self.layers):
+                d = {}
+                if i == 0:
+                    d["wq"], d["bq"] = ops.pack_qkv_heads(L["w_qkv"], L["b_qkv"], H)
+                else:
+                    P = self.layers[i - 1]
+                    w2, cs, bf = ops.fold_ln_weights(L["w_qkv"], L["b_qkv"], P["ln2_g"], P["ln2_b"])
+                    d["wq"], d["bfq"] = ops.pack_qkv_heads(w2, bf, H)
+                    d["csq"] = ops.pack_qkv_vec(cs, H)
+                d["w_i"], d["cs_i"], d["b_i"] = ops.fold_ln_weights(L["w_i"], L["b_i"], L["ln1_g"], L["ln1_b"])
+                out.append(d)
+            self._deferred = (key, out)
+        return self._deferred[1]
+
     def _forward_hip(self, ids: torch.Tensor) -> torch.Tensor:
-        if self.fold_ln and self.dtype == torch.bfloat16 and self.cfg.hidden % 4 == 0:
+        c = self.cfg
+        if self.fold_ln and self.dtype == torch.bfloat16 and c.hidden % 4 == 0:
+            if self.fuse_qkv_attn and ops.qkv_attention_supported(ids.shape[1], c.heads, c.hidden // c.heads, c.hidden):
+                return self._forward_hip_fused_deferred(ids)
             return self._forward_hip_folded(ids)
         c = self.cfg
         B, S = ids.shape
@@ -217,6 +244,54 @@ class BertForSequenceClassification:
             h = ops.layer_norm(o, L["ln2_g"], L["ln2_b"], c.eps)
         cls = h if self.cls_only_last_layer else h.view(B, S, D)[:, 0, :]
         pooled = ops.linear(cls, self.w_pool, self.b_pool, act="tanh")
+        return ops.linear(pooled, self.w_cls, self.b_cls, out_dtype=torch.float32)
+
+    def _forward_hip_fused_deferred(self, ids: torch.Tensor) -> torch.Tensor:
+        """Four kernels per layer and no LayerNorm kernel inside the stack:
+        fused QKV+attention reading the RAW residual stream with LN2 folded into
+        its weights (row statistics computed in its own main loop, published by
+        head 0), o-proj normalising that residual on load, FFN-up with LN1 folded
+        in (statistics again computed in-loop, published by the first N tile),
+        FFN-down normalising its residual on load.  No statistics pass, no atomics."""
+        c = self.cfg
+        B, S = ids.shape
+        D, H, eps = c.hidden, c.heads, c.eps
+        Wd = self._deferred_weights()
+        lens = ops.seq_lens(ids, c.pad_token_id)
+        M = B * S
+        n = len(self.layers)
+        stats = torch.empty(n, 2, M, 2, device=ids.device, dtype=torch.float32)   # (x rows, a rows) per layer
+        x = ops.embed_ln(ids, self.word, self.pos, self.typ, self.emb_g, self.emb_b, eps).reshape(M, D)
+        xg = xb = None             # x is raw (pre-LN2 of the previous layer) iff xg is not None
+        h = None
+        for i, L in enumerate(self.layers):
+            st_x, st_a = stats[i, 0], stats[i, 1]
+            d = Wd[i]
+            if xg is None:
+                ctx = ops.qkv_attention(x, d["wq"], d["bq"], B, S, H, lens=lens)
+            else:
+                ctx = ops.qkv_attention(x, d["wq"], None, B, S, H, lens=lens, lna=(d["csq"], d["bfq"], eps),
+                                        stats_out=st_x)
+            if i == n - 1 and self.cls_only_last_layer:
+                xc = x.view(B, S, D)[:, 0, :]
+                hc = xc if xg is None else ops.layer_norm(xc, xg, xb, eps)
+                a = ops.linear(ctx.view(B, S, D)[:, 0, :], L["w_o"], L["b_o"], residual=hc)
+                h1 = ops.layer_norm(a, L["ln1_g"], L["ln1_b"], eps)
+                inter = ops.linear(h1, L["w_i"], L["b_i"], act="gelu")
+                o = ops.linear(inter, L["w_out"], L["b_out"], residual=h1)
+                h = ops.layer_norm(o, L["ln2_g"], L["ln2_b"], eps)
+                break
+            if xg is None:
+                a = ops.linear(ctx, L["w_o"], L["b_o"], residual=x)
+            else:
+                a = ops.linear_ln(ctx, L["w_o"], L["b_o"], residual=x, lnr=(st_x, xg, xb, D, eps))
+            inter = ops.linear_ln(a, d["w_i"], act="gelu", lna=(None, d["cs_i"], d["b_i"], D, eps), out_stats=st_a)
+            o = ops.linear_ln(inter, L["w_out"], L["b_out"], residual=a, lnr=(st_a, L["ln1_g"], L["ln1_b"], D, eps))
+            x, xg, xb = o, L["ln2_g"], L["ln2_b"]
+        if h is None:
+            h = ops.layer_norm(x, xg, xb, eps) if xg is not None else x
+            h = h.view(B, S, D)[:, 0, :]
+        pooled = ops.linear(h, self.w_pool, self.b_pool, act="tanh")
         return ops.linear(pooled, self.w_cls, self.b_cls, out_dtype=torch.float32)
 
     def _forward_hip_folded(self, ids: torch.Tensor) -> torch.Tensor:

@@ -242,7 +242,7 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
     return out
 
 
-LN_LNA, LN_LNR, LN_STATS = 1, 2, 4
+LN_LNA, LN_LNR, LN_STATS, LN_SELF = 1, 2, 4, 8
 
 
 def _stats_ld(st: torch.Tensor, M: int, what: str) -> int:
@@ -260,7 +260,10 @@ def linear_ln(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = N
     * ``lna=(stats, colsum, bias_f32, D, eps)``: x holds RAW rows whose LayerNorm
       is folded into w (w = W * gamma, colsum = w.float().sum(1), bias_f32 =
       b + W @ beta); ``stats`` [M, 2] f32 = per-row (sum, sum of squares).
-      y = act(LN(x) @ W.T + b); ``bias`` must be None.
+      y = act(LN(x) @ W.T + b); ``bias`` must be None.  ``stats=None``: the
+      GEMM computes x's row statistics itself in its main loop (no producer
+      pass) and, if ``out_stats`` is given, STORES them there (for a later
+      ``lnr`` of the same rows) -- ``out_stats`` needs no zeroing in this mode.
     * ``lnr=(stats, gamma, beta, D, eps)``: ``residual`` holds raw rows and is
       added as LayerNorm(residual) (normalised on load).
     * ``out_stats`` [M, 2] f32: += per-row (sum, sum of squares) of the stored y
@@ -273,9 +276,15 @@ def linear_ln(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = N
     M, lda = x.shape[0], x.stride(0)
     _check(K % 8 == 0 and lda % 8 == 0 and N % 4 == 0 and _aligned(x) and _aligned(w), "linear_ln: alignment")
     _check(act != "swiglu", "linear_ln: no swiglu")
-    mode = (LN_LNA if lna is not None else 0) | (LN_LNR if lnr is not None else 0) | \
-        (LN_STATS if out_stats is not None else 0)
-    _check(mode in (LN_LNA, LN_STATS, LN_LNR | LN_STATS), "linear_ln: modes are lna, out_stats, or lnr + out_stats")
+    self_stats = lna is not None and lna[0] is None
+    if self_stats:
+        mode = LN_LNA | LN_SELF
+        _check(lnr is None, "linear_ln: lna with in-kernel statistics takes no lnr")
+    else:
+        mode = (LN_LNA if lna is not None else 0) | (LN_LNR if lnr is not None else 0) | \
+            (LN_STATS if out_stats is not None else 0)
+    _check(mode in (LN_LNA, LN_STATS, LN_LNR | LN_STATS, LN_LNR, LN_LNA | LN_SELF),
+           "linear_ln: modes are lna, out_stats, lnr, lnr + out_stats, or lna with in-kernel statistics")
     if out is None:
         out = torch.empty(M, N, device=x.device, dtype=x.dtype)
     _check(out.is_contiguous() and out.shape == (M, N), "linear_ln: bad out")
@@ -293,7 +302,7 @@ def linear_ln(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = N
     eps = 0.0
     if lna is not None:
         a_st, a_cs, a_b, d, eps = lna
-        a_ld = _stats_ld(a_st, M, "lna")
+        a_ld = 0 if a_st is None else _stats_ld(a_st, M, "lna")
         _check(a_cs.dtype == torch.float32 and a_cs.numel() == N and a_cs.is_contiguous()
                and a_b.dtype == torch.float32 and a_b.numel() == N and a_b.is_contiguous(), "linear_ln: bad lna vectors")
         a_inv = 1.0 / d
@@ -315,7 +324,7 @@ def linear_ln(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = N
         key = ("gemm_ln", x.dtype, M, N, K, lda, act, mode)
         tuned = key in _TUNE
         tile_cfg = _tuned_cfg(key, lambda c: fn(*args, _stream(), c), range(NUM_LN_TILE_CFGS))
-        if not tuned and out_stats is not None and not torch.cuda.is_current_stream_capturing():
+        if not tuned and mode & LN_STATS and not torch.cuda.is_current_stream_capturing():
             out_stats.zero_()        # the tuning launches accumulated into it
     fn(*args, _stream(), int(tile_cfg))
     return out
@@ -511,40 +520,68 @@ def pack_qkv_heads(w: torch.Tensor, b: torch.Tensor, H: int) -> Tuple[torch.Tens
     return wp, bp
 
 
+def pack_qkv_vec(v: torch.Tensor, H: int) -> torch.Tensor:
+    """A per-output-row vector of the [q | k | v] projection (bias, folded
+    colsum / bias) in ``pack_qkv_heads`` order."""
+    N = v.numel()
+    _check(N % (3 * H) == 0, "pack_qkv_vec: length must be 3*H*D")
+    return v.view(3, H, N // (3 * H)).transpose(0, 1).reshape(N).contiguous()
+
+
 def qkv_attention_supported(S: int, H: int, D: int, K: int) -> bool:
     return 1 <= S <= QKV_ATTN_MAX_S and D == 64 and K % 8 == 0
 
 
-def qkv_attention(x: torch.Tensor, w_packed: torch.Tensor, b_packed: torch.Tensor, B: int, S: int, H: int,
+def qkv_attention(x: torch.Tensor, w_packed: torch.Tensor, b_packed: Optional[torch.Tensor], B: int, S: int, H: int,
                   lens: Optional[torch.Tensor] = None, scale: Optional[float] = None,
-                  out: Optional[torch.Tensor] = None, cfg: int = -1) -> torch.Tensor:
+                  out: Optional[torch.Tensor] = None, cfg: int = -1, lna: Optional[tuple] = None,
+                  stats_out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Fused QKV projection + bidirectional attention (qkv_attention.hip):
     ctx [B*S, H*64] = MHA(x @ W^T + b) for S <= 128, head dim 64, with the
     projection weight in ``pack_qkv_heads`` layout.  The [B*S, 3*H*64] QKV
-    activation is never materialised."""
+    activation is never materialised.
+
+    ``lna=(colsum, bias_f32, eps)`` (packed order, f32): x holds RAW rows whose
+    LayerNorm is folded into ``w_packed`` (``fold_ln_weights`` then packing);
+    the kernel computes each row's statistics itself and, with ``stats_out``
+    [B*S, 2] f32, stores (sum, sum of squares) for a later ``linear_ln(lnr=...)``.
+    ``b_packed`` must then be None."""
     _check(x.is_cuda and x.dtype in (torch.bfloat16, torch.float16) and x.dim() == 2 and x.stride(1) == 1,
            "qkv_attention: x must be a 2-D [B*S, K] (row-strided) bf16/f16 view")
-    _check(w_packed.dtype == x.dtype and w_packed.is_contiguous() and b_packed.dtype == x.dtype
-           and b_packed.is_contiguous(), "qkv_attention: weight / bias dtype and layout")
     N, K = w_packed.shape
+    _check(w_packed.dtype == x.dtype and w_packed.is_contiguous(), "qkv_attention: weight dtype and layout")
+    cs = bf = None
+    eps = 0.0
+    if lna is not None:
+        cs, bf, eps = lna
+        _check(b_packed is None, "qkv_attention: the folded form takes its bias from lna")
+        _check(all(v.dtype == torch.float32 and v.is_contiguous() and v.numel() == N and _aligned(v) for v in (cs, bf)),
+               "qkv_attention: lna colsum / bias must be contiguous f32 [H*192]")
+        if stats_out is not None:
+            _check(stats_out.dtype == torch.float32 and stats_out.is_contiguous() and stats_out.shape == (B * S, 2),
+                   "qkv_attention: stats_out must be contiguous f32 [B*S, 2]")
+    else:
+        _check(b_packed is not None and b_packed.dtype == x.dtype and b_packed.is_contiguous()
+               and b_packed.numel() == N and _aligned(b_packed, 8), "qkv_attention: bias dtype / layout")
+        _check(stats_out is None, "qkv_attention: stats_out needs lna")
     _check(x.shape == (B * S, K), f"qkv_attention: x must be [B*S, K] = [{B * S}, {K}], got {tuple(x.shape)}")
-    _check(N == H * 192 and b_packed.numel() == N, "qkv_attention: packed weight must be [H*3*64, K]")
+    _check(N == H * 192, "qkv_attention: packed weight must be [H*3*64, K]")
     _check(qkv_attention_supported(S, H, 64, K), "qkv_attention: S <= 128, head dim 64, K % 8 == 0")
-    _check(x.stride(0) % 8 == 0 and _aligned(x) and _aligned(w_packed) and _aligned(b_packed, 8),
-           "qkv_attention: alignment")
+    _check(x.stride(0) % 8 == 0 and _aligned(x) and _aligned(w_packed), "qkv_attention: alignment")
     if lens is not None:
         _check(lens.dtype == torch.int32 and lens.numel() == B and lens.is_cuda, "qkv_attention: lens must be int32 [B]")
     if out is None:
         out = torch.empty(B * S, H * 64, device=x.device, dtype=x.dtype)
     _check(out.is_contiguous() and out.shape == (B * S, H * 64) and _aligned(out), "qkv_attention: bad out")
     scale = 1.0 / 8.0 if scale is None else scale
-    args = (DTYPE_CODE[x.dtype], x.data_ptr(), x.stride(0), w_packed.data_ptr(), b_packed.data_ptr(), B, S, H, K,
+    args = (DTYPE_CODE[x.dtype], x.data_ptr(), x.stride(0), w_packed.data_ptr(), _ptr(b_packed), B, S, H, K,
             _ptr(lens), out.data_ptr(), H * 64, float(scale))
+    extra = (_ptr(cs), _ptr(bf), _ptr(stats_out), float(eps))
     fn = _ops().qkv_attn_fwd
     if cfg < 0:
-        key = ("qkv_attn", x.dtype, B, S, H, K, x.stride(0))
-        cfg = _tuned_cfg(key, lambda c: fn(*args, c, _stream()), range(NUM_QKV_ATTN_CFGS))
-    fn(*args, int(cfg), _stream())
+        key = ("qkv_attn", x.dtype, B, S, H, K, x.stride(0), lna is not None)
+        cfg = _tuned_cfg(key, lambda c: fn(*args, c, _stream(), *extra), range(NUM_QKV_ATTN_CFGS))
+    fn(*args, int(cfg), _stream(), *extra)
     return out
 
 

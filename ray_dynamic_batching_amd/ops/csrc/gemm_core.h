@@ -186,7 +186,12 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, char* lds, uint3
 // and a residual operand that is a normalised row is normalised on load (LNR):
 //     R'[m, n] = (R[m, n] - mean_R[m]) * rstd_R[m] * g[n] + be[n].
 // No LayerNorm kernel runs and the normalised rows are never materialised.
-constexpr int EPI_LNA = 1, EPI_LNR = 2, EPI_STATS = 4;
+// EPI_SELF (with LNA): the GEMM computes A's row statistics itself from the
+// A fragments it already holds for the MFMAs (every block streams whole rows
+// of A through the main loop) -- no producer-side statistics pass, no atomics.
+// Blocks of the first N tile also store them to o_stats (plain stores, one
+// writer per row) for a later LNR consumer of the same rows.
+constexpr int EPI_LNA = 1, EPI_LNR = 2, EPI_STATS = 4, EPI_SELF = 8;
 struct LnEpi {
   const float* a_stats;   // LNA: (sum, sumsq) of A's rows, row stride a_ld floats
   const float* a_colsum;  // LNA: colsum(W') [N]
@@ -198,6 +203,26 @@ struct LnEpi {
   int a_ld, r_ld, o_ld;
   float a_inv_d, r_inv_d, eps;
 };
+
+// (sum, sum of squares) of the 8 elements of an MFMA fragment, accumulated with
+// the packed dot instructions (v_dot2_f32_{bf16,f16}: 2 elements per VALU op)
+template <typename T, typename F8>
+__device__ __forceinline__ void frag_stats(const F8& f, float& s1, float& s2) {
+  typedef T t2 __attribute__((ext_vector_type(2)));
+  const T one = (T)1.0f;
+  const t2 ones = {one, one};
+#pragma unroll
+  for (int e = 0; e < 8; e += 2) {
+    const t2 p = {f[e], f[e + 1]};
+    if constexpr (std::is_same<T, bf16>::value) {
+      s1 = __builtin_amdgcn_fdot2_f32_bf16(p, ones, s1, false);
+      s2 = __builtin_amdgcn_fdot2_f32_bf16(p, p, s2, false);
+    } else {
+      s1 = __builtin_amdgcn_fdot2(p, ones, s1, false);
+      s2 = __builtin_amdgcn_fdot2(p, p, s2, false);
+    }
+  }
+}
 
 __device__ __forceinline__ void ln_row_stats(float2 v, float inv_d, float eps, float& mu, float& rstd) {
   mu = v.x * inv_d;
@@ -332,6 +357,8 @@ mfma_gemm_kernel(typename LoaderT<T, 1>::Params ap, const T* __restrict__ W, int
                  OutT* __restrict__ C, int ldc, const T* __restrict__ bias,
                  const T* __restrict__ R, int ldr, int M, int N, int K, float alpha, int act, LnEpi ln) {
   constexpr bool LNA = (EPI & EPI_LNA) != 0, LNR = (EPI & EPI_LNR) != 0, OST = (EPI & EPI_STATS) != 0;
+  constexpr bool SELF = (EPI & EPI_SELF) != 0;
+  static_assert(!SELF || (LNA && !OST), "SELF computes LNA's statistics; it writes o_stats itself");
   static_assert(!LNA || !HAS_BIAS, "LNA takes its (folded) bias from ln.a_bias");
   static_assert(!LNR || HAS_RES, "LNR normalises the residual operand");
   constexpr int BK = 64;
@@ -398,7 +425,12 @@ mfma_gemm_kernel(typename LoaderT<T, 1>::Params ap, const T* __restrict__ W, int
     for (int j = 0; j < TM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int fr = lane & 15, fg = lane >> 4;
-  auto compute = [&](int buf) {
+  // SELF: per-lane partial (sum, sum of squares) of A rows wm*WM + j*16 + fr over
+  // this lane's k slice; the 4 lanes of a row are combined after the loop
+  float st1[SELF ? TM : 1], st2[SELF ? TM : 1];
+#pragma unroll
+  for (int j = 0; j < (SELF ? TM : 1); ++j) st1[j] = st2[j] = 0.f;
+  auto compute = [&](int buf, int k0) {
     const char* sa = smem + buf * kStage;
     const char* sw = sa + BM * BK * 2;
 #pragma unroll
@@ -411,6 +443,12 @@ mfma_gemm_kernel(typename LoaderT<T, 1>::Params ap, const T* __restrict__ W, int
 #pragma unroll
       for (int j = 0; j < TM; ++j)
         af[j] = *reinterpret_cast<const frag*>(sa + swz_off(wm * WM + j * 16 + fr, chunk));
+      if constexpr (SELF) {
+        // k >= K reads as zero (DMA bounds check): contributes nothing to either sum
+#pragma unroll
+        for (int j = 0; j < TM; ++j) frag_stats<T>(af[j], st1[j], st2[j]);
+        (void)k0;
+      }
 #pragma unroll
       for (int i = 0; i < TN; ++i)
 #pragma unroll
@@ -424,12 +462,12 @@ mfma_gemm_kernel(typename LoaderT<T, 1>::Params ap, const T* __restrict__ W, int
   // deferred-LN row statistics are fetched before the main loop: their latency
   // hides under it instead of opening the epilogue
   float2 ast[LNA ? TM : 1], rst[LNR ? TM : 1];
-  if constexpr (LNA || LNR) {
+  if constexpr ((LNA && !SELF) || LNR) {
 #pragma unroll
     for (int j = 0; j < TM; ++j) {
       const int m = m0 + wm * WM + j * 16 + fr;
       const size_t ms = (size_t)(m < M ? m : M - 1);
-      if constexpr (LNA) ast[j] = *reinterpret_cast<const float2*>(ln.a_stats + ms * ln.a_ld);
+      if constexpr (LNA && !SELF) ast[j] = *reinterpret_cast<const float2*>(ln.a_stats + ms * ln.a_ld);
       if constexpr (LNR) rst[j] = *reinterpret_cast<const float2*>(ln.r_stats + ms * ln.r_ld);
     }
   }
@@ -443,7 +481,7 @@ mfma_gemm_kernel(typename LoaderT<T, 1>::Params ap, const T* __restrict__ W, int
     __syncthreads();
     for (int kt = 0; kt < nk; ++kt) {
       if (kt + 1 < nk) stage((kt + 1) & 1, (kt + 1) * BK);
-      compute(kt & 1);
+      compute(kt & 1, kt * BK);
       __syncthreads();
     }
   } else {
@@ -468,10 +506,24 @@ mfma_gemm_kernel(typename LoaderT<T, 1>::Params ap, const T* __restrict__ W, int
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
       if (kt + 2 < nk) stage(buf == 0 ? 2 : buf - 1, (kt + 2) * BK);
-      compute(buf);
+      compute(buf, kt * BK);
       buf = buf == 2 ? 0 : buf + 1;
     }
     __syncthreads();
+  }
+  if constexpr (SELF) {
+#pragma unroll
+    for (int j = 0; j < TM; ++j) {
+      float a = st1[j], q = st2[j];
+      a += __shfl_xor(a, 16, 64);
+      q += __shfl_xor(q, 16, 64);
+      a += __shfl_xor(a, 32, 64);
+      q += __shfl_xor(q, 32, 64);
+      ast[j] = float2{a, q};
+      const int m = m0 + wm * WM + j * 16 + fr;
+      if (ln.o_stats != nullptr && tile_n == 0 && wn == 0 && fg == 0 && m < M)
+        *reinterpret_cast<float2*>(ln.o_stats + (size_t)m * ln.o_ld) = ast[j];
+    }
   }
 
   // ---- LDS-staged coalesced epilogue (plain modes; LN / SwiGLU keep the direct one) ----

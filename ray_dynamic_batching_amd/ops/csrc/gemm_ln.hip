@@ -5,6 +5,10 @@
 //   mode LNA          y = act(rstd_A[m] (A W'^T - mean_A[m] colsum[n]) + bias'[n])   (W' = W * gamma)
 //   mode STATS        y = A W^T + bias + R,                 stats[m] += (sum y, sum y^2)
 //   mode LNR | STATS  y = A W^T + bias + LN(R) (normalised on load), stats[m] += ...
+//   mode LNR          y = A W^T + bias + LN(R)
+//   mode LNA | SELF   as LNA, but A's row statistics are computed by this GEMM
+//                     from the A tiles of its own main loop; the first N-tile's
+//                     blocks store them to o_stats (for a later LNR of A)
 //
 // Used by models/bert.py (fold_ln): QKV and FFN-up take LNA, o-proj and
 // FFN-down take (LNR |) STATS.  Reference behaviour being preserved: the
@@ -59,8 +63,18 @@ void gemm_tn_ln(uintptr_t A, int lda, uintptr_t W, int ldw, uintptr_t C, int ldc
       launch_mfma_gemm_t<bf16, bf16, DenseLoader, true, true, EPI_LNR | EPI_STATS>(p, w, ldw, c, ldc, b, r, ldr, M,
                                                                                    N, K, alpha, act, s, cfg, ln);
       break;
+    case EPI_LNR:
+      need(bias && R && r_stats && r_g && r_b, "gemm_tn_ln: LNR needs bias, R, r_*");
+      launch_mfma_gemm_t<bf16, bf16, DenseLoader, true, true, EPI_LNR>(p, w, ldw, c, ldc, b, r, ldr, M, N, K, alpha,
+                                                                       act, s, cfg, ln);
+      break;
+    case EPI_LNA | EPI_SELF:
+      need(a_colsum && a_bias && !bias && !R, "gemm_tn_ln: LNA|SELF needs a_colsum/a_bias, no bias/R");
+      launch_mfma_gemm_t<bf16, bf16, DenseLoader, false, false, EPI_LNA | EPI_SELF>(p, w, ldw, c, ldc, b, r, ldr, M, N,
+                                                                                    K, alpha, act, s, cfg, ln);
+      break;
     default:
-      throw std::invalid_argument("gemm_tn_ln: mode must be LNA (1), STATS (4) or LNR|STATS (6)");
+      throw std::invalid_argument("gemm_tn_ln: mode must be LNA (1), STATS (4), LNR|STATS (6), LNR (2) or LNA|SELF (9)");
   }
   RDB_HIP_CHECK(hipGetLastError());
 }

@@ -23,15 +23,30 @@
 //
 // Grid: B * H blocks, XCD-remapped so the H heads of one sequence (which share
 // its 128 x hidden A panel) run on one XCD's L2.
+//
+// LNA = true: X holds RAW rows whose LayerNorm is folded into the weight
+// (Wp = W * gamma, colsum = rowsum(Wp), bias_f = b + W beta; gemm_core.h
+// "deferred-LayerNorm"): the block computes each token's (sum, sum of squares)
+// from the A fragments of its own main loop (frag_stats) and corrects
+//   P = rstd * (X Wp^T - mean * colsum) + bias_f;
+// head 0's block stores the statistics to stats_out for the o-projection's
+// LayerNorm-on-load of the same rows (the residual).  No LayerNorm kernel runs.
 #include "gemm_core.h"
 #include <stdexcept>
 
 namespace rdb {
 
-template <typename T, int NW, int STAGES>
+struct QkvLn {
+  const float* colsum;   // [H*192], packed order
+  const float* bias_f;   // [H*192]
+  float* stats_out;      // [B*S, 2] (sum, sum of squares) of X's rows, row stride 2; may be null
+  float inv_d, eps;
+};
+
+template <typename T, int NW, int STAGES, bool LNA>
 __global__ void __launch_bounds__(64 * NW, NW == 8 && STAGES == 3 ? 1 : 2)
 qkv_attn_kernel(DenseParams ap, const T* __restrict__ W, const T* __restrict__ bias, int S, int H,
-                const int* __restrict__ lens, T* __restrict__ out, int ld_out, float scale_log2e) {
+                const int* __restrict__ lens, T* __restrict__ out, int ld_out, float scale_log2e, QkvLn ln) {
   constexpr int BM = 128, BN = 192, BK = 64, D = 64;
   constexpr int WGM = NW == 8 ? 4 : 2, WGN = 2;
   constexpr int NT = 64 * NW;
@@ -88,6 +103,9 @@ qkv_attn_kernel(DenseParams ap, const T* __restrict__ W, const T* __restrict__ b
   for (int i = 0; i < TN; ++i)
 #pragma unroll
     for (int j = 0; j < TM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float st1[LNA ? TM : 1], st2[LNA ? TM : 1];
+#pragma unroll
+  for (int j = 0; j < (LNA ? TM : 1); ++j) st1[j] = st2[j] = 0.f;
   auto compute = [&](int buf) {
     const char* sa = smem + buf * kStage;
     const char* sw = sa + BM * BK * 2;
@@ -99,6 +117,10 @@ qkv_attn_kernel(DenseParams ap, const T* __restrict__ W, const T* __restrict__ b
       for (int i = 0; i < TN; ++i) wf[i] = *reinterpret_cast<const frag*>(sw + swz_off(wn * WN + i * 16 + fr, chunk));
 #pragma unroll
       for (int j = 0; j < TM; ++j) af[j] = *reinterpret_cast<const frag*>(sa + swz_off(wm * WM + j * 16 + fr, chunk));
+      if constexpr (LNA) {
+#pragma unroll
+        for (int j = 0; j < TM; ++j) frag_stats<T>(af[j], st1[j], st2[j]);   // k >= K reads as 0
+      }
 #pragma unroll
       for (int i = 0; i < TN; ++i)
 #pragma unroll
@@ -139,6 +161,22 @@ qkv_attn_kernel(DenseParams ap, const T* __restrict__ W, const T* __restrict__ b
     __syncthreads();
   }
   kv_len = kv_len < S ? (kv_len < 1 ? 1 : kv_len) : S;
+  // LNA: per-row (mean, rstd) of this lane's rows; head 0 publishes the sums
+  float mu[LNA ? TM : 1], rs[LNA ? TM : 1];
+  if constexpr (LNA) {
+#pragma unroll
+    for (int j = 0; j < TM; ++j) {
+      float a = st1[j], q = st2[j];
+      a += __shfl_xor(a, 16, 64);
+      q += __shfl_xor(q, 16, 64);
+      a += __shfl_xor(a, 32, 64);
+      q += __shfl_xor(q, 32, 64);
+      ln_row_stats(float2{a, q}, ln.inv_d, ln.eps, mu[j], rs[j]);
+      const int tok = wm * WM + j * 16 + fr;
+      if (ln.stats_out != nullptr && h == 0 && wn == 0 && fg == 0 && tok < S && m0 + tok < ap.M)
+        *reinterpret_cast<float2*>(ln.stats_out + (size_t)(m0 + tok) * 2) = float2{a, q};
+    }
+  }
 
   // ---- 2. + bias, round to T, park Q / K / V^T in LDS ----
   // lane holds P[token = wm*WM + j*16 + fr][col = wn*WN + i*16 + fg*4 .. +3];
@@ -150,14 +188,22 @@ qkv_attn_kernel(DenseParams ap, const T* __restrict__ W, const T* __restrict__ b
   for (int i = 0; i < TN; ++i) {
     const int c0 = wn * WN + i * 16;                  // wave-uniform
     const int c = c0 + fg * 4;
-    const u32x2 braw = *reinterpret_cast<const u32x2*>(bias + n0 + c);
-    const T* be = reinterpret_cast<const T*>(&braw);
+    f32x4 bv, cs;
+    if constexpr (LNA) {
+      bv = *reinterpret_cast<const f32x4*>(ln.bias_f + n0 + c);
+      cs = *reinterpret_cast<const f32x4*>(ln.colsum + n0 + c);
+    } else {
+      const u32x2 braw = *reinterpret_cast<const u32x2*>(bias + n0 + c);
+      const T* be = reinterpret_cast<const T*>(&braw);
+      bv = f32x4{(float)be[0], (float)be[1], (float)be[2], (float)be[3]};
+    }
 #pragma unroll
     for (int j = 0; j < TM; ++j) {
       const int tok = wm * WM + j * 16 + fr;
-      const f32x4 v = acc[i][j];
-      const frag4 y = {(T)(v[0] + (float)be[0]), (T)(v[1] + (float)be[1]), (T)(v[2] + (float)be[2]),
-                       (T)(v[3] + (float)be[3])};
+      f32x4 v = acc[i][j];
+      if constexpr (LNA) v = (v - mu[j] * cs) * rs[j];
+      v += bv;
+      const frag4 y = {(T)v[0], (T)v[1], (T)v[2], (T)v[3]};
       if (c0 < 128) {        // Q or K: row-major [tok][d], 16-B chunks XOR-swizzled
         const int d = c0 < 64 ? c : c - 64;
         *reinterpret_cast<frag4*>((c0 < 64 ? Qs : Ks) + swz_off(tok, d >> 3) + (d & 7) * 2) = y;
@@ -265,43 +311,56 @@ qkv_attn_kernel(DenseParams ap, const T* __restrict__ W, const T* __restrict__ b
 // cfg: 0 = 8 waves / 3 stages (1 block per CU), 1 = 8 waves / 2 stages, 2 = 4 waves / 2 stages
 constexpr int kNumQkvAttnCfgs = 3;
 
-template <typename T>
+template <typename T, bool LNA>
 static void launch_qkv_attn(int cfg, const DenseParams& p, const T* W, const T* bias, int B, int S, int H,
-                            const int* lens, T* out, int ld_out, float sl2e, hipStream_t s) {
+                            const int* lens, T* out, int ld_out, float sl2e, const QkvLn& ln, hipStream_t s) {
   const dim3 grid(B * H);
   switch (cfg) {
     case 0:
-      hipLaunchKernelGGL((qkv_attn_kernel<T, 8, 3>), grid, dim3(512), 0, s, p, W, bias, S, H, lens, out, ld_out, sl2e);
+      hipLaunchKernelGGL((qkv_attn_kernel<T, 8, 3, LNA>), grid, dim3(512), 0, s, p, W, bias, S, H, lens, out, ld_out,
+                         sl2e, ln);
       break;
     case 1:
-      hipLaunchKernelGGL((qkv_attn_kernel<T, 8, 2>), grid, dim3(512), 0, s, p, W, bias, S, H, lens, out, ld_out, sl2e);
+      hipLaunchKernelGGL((qkv_attn_kernel<T, 8, 2, LNA>), grid, dim3(512), 0, s, p, W, bias, S, H, lens, out, ld_out,
+                         sl2e, ln);
       break;
     default:
-      hipLaunchKernelGGL((qkv_attn_kernel<T, 4, 2>), grid, dim3(256), 0, s, p, W, bias, S, H, lens, out, ld_out, sl2e);
+      hipLaunchKernelGGL((qkv_attn_kernel<T, 4, 2, LNA>), grid, dim3(256), 0, s, p, W, bias, S, H, lens, out, ld_out,
+                         sl2e, ln);
       break;
   }
 }
 
 // X [B*S, hidden] (row stride ldx), Wp [H*192, hidden] head-major packed, bp [H*192],
 // out [B*S, H*64] (row stride ld_out).  dtype 0 = bf16, 1 = f16.
+// colsum != 0 selects the LayerNorm-folded form: bp is unused, colsum / bias_f
+// are f32 [H*192] (packed order), stats_out (optional) f32 [B*S, 2].
 void qkv_attn_fwd(int dtype, uintptr_t X, int ldx, uintptr_t Wp, uintptr_t bp, int B, int S, int H, int hidden,
-                  uintptr_t lens, uintptr_t out, int ld_out, float scale, int cfg, uintptr_t stream) {
+                  uintptr_t lens, uintptr_t out, int ld_out, float scale, int cfg, uintptr_t stream,
+                  uintptr_t colsum, uintptr_t bias_f, uintptr_t stats_out, float eps) {
   if (S < 1 || S > 128) throw std::invalid_argument("qkv_attn: 1 <= S <= 128");
   if (hidden % 8 || ldx % 8 || ld_out % 4) throw std::invalid_argument("qkv_attn: hidden / ldx % 8, ld_out % 4");
-  if ((X | Wp | out) & 15 || bp & 7) throw std::invalid_argument("qkv_attn: alignment");
+  const bool lna = colsum != 0;
+  if ((X | Wp | out) & 15 || (!lna && (bp & 7)) || (lna && ((colsum | bias_f) & 15 || !bias_f)) || stats_out & 7)
+    throw std::invalid_argument("qkv_attn: alignment / folded-LayerNorm operands");
   if (cfg < 0 || cfg >= kNumQkvAttnCfgs) cfg = 1;
   if (B <= 0 || H <= 0) return;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const DenseParams p{reinterpret_cast<const void*>(X), ldx, B * S, hidden};
   const float sl2e = scale * 1.4426950408889634f;
-  if (dtype == 0)
-    launch_qkv_attn<bf16>(cfg, p, reinterpret_cast<const bf16*>(Wp), reinterpret_cast<const bf16*>(bp), B, S, H,
-                          reinterpret_cast<const int*>(lens), reinterpret_cast<bf16*>(out), ld_out, sl2e, s);
-  else if (dtype == 1)
-    launch_qkv_attn<f16>(cfg, p, reinterpret_cast<const f16*>(Wp), reinterpret_cast<const f16*>(bp), B, S, H,
-                         reinterpret_cast<const int*>(lens), reinterpret_cast<f16*>(out), ld_out, sl2e, s);
-  else
+  const QkvLn ln{reinterpret_cast<const float*>(colsum), reinterpret_cast<const float*>(bias_f),
+                 reinterpret_cast<float*>(stats_out), 1.0f / hidden, eps};
+#define RDB_QA(T, L)                                                                                            \
+  launch_qkv_attn<T, L>(cfg, p, reinterpret_cast<const T*>(Wp), reinterpret_cast<const T*>(bp), B, S, H,        \
+                        reinterpret_cast<const int*>(lens), reinterpret_cast<T*>(out), ld_out, sl2e, ln, s)
+  if (dtype == 0) {
+    if (lna) RDB_QA(bf16, true); else RDB_QA(bf16, false);
+  } else if (dtype == 1) {
+    if (lna) RDB_QA(f16, true); else RDB_QA(f16, false);
+  } else {
     throw std::invalid_argument("qkv_attn: dtype must be bf16 or f16");
+  }
+#undef RDB_QA
   RDB_HIP_CHECK(hipGetLastError());
 }
 

@@ -52,12 +52,16 @@ def test_bert_fused_qkv_attention_matches_unfused_and_torch():
 
 
 @pytest.mark.parametrize("cls_only", [True, False])
-def test_bert_folded_layernorm_matches_unfolded(cls_only):
-    """The deferred-LayerNorm forward (ops.linear_ln) == the LayerNorm-kernel
-    forward and the eager torch model, with non-trivial LN gamma/beta."""
+@pytest.mark.parametrize("fused", [True, False])
+def test_bert_folded_layernorm_matches_unfolded(cls_only, fused):
+    """The deferred-LayerNorm forwards (fused: qkv_attention + in-kernel row
+    statistics, 4 kernels per layer; unfused: STATS-epilogue chain) == the
+    LayerNorm-kernel forward and the eager torch model, with non-trivial LN
+    gamma/beta."""
     from ray_dynamic_batching_amd.models.bert import BertConfig, BertForSequenceClassification
 
     m = BertForSequenceClassification(BertConfig(layers=4), device="cuda", backend="hip", seed=2)
+    m.fuse_qkv_attn = fused
     g = torch.Generator(device="cpu").manual_seed(5)
     for L in m.layers:
         for k in ("ln1_g", "ln2_g"):

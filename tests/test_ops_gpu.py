@@ -433,6 +433,60 @@ def test_deferred_ln_large_row_mean(offset):
     _close(y, ops.linear_ln_ref(x, w, b, ln_x=(g, be)), 3e-2, 3e-2)
 
 
+@pytest.mark.parametrize("cfg", list(range(19)))
+def test_linear_ln_self_stats_and_lnr_only_all_tiles(cfg):
+    """LNA with in-kernel row statistics (no producer pass) on every tile: the
+    output == LayerNorm-then-GEMM, the published (sum, sumsq) == a torch
+    reduction of A; then LNR alone consumes them as the residual's LayerNorm.
+    K = 776 leaves a partial last K tile (zero-filled, must not bias the sums)."""
+    ops = _ops()
+    torch.manual_seed(40 + cfg)
+    M, N, K = 520, 768, 776
+    x = (torch.randn(M, K, device="cuda") * 1.5 + 0.4).to(torch.bfloat16)
+    w = (torch.randn(N, K, device="cuda") * K ** -0.5).to(torch.bfloat16)
+    b = (torch.randn(N, device="cuda") * 0.1).to(torch.bfloat16)
+    g = (1 + 0.2 * torch.randn(K, device="cuda")).to(torch.bfloat16)
+    be = (0.1 * torch.randn(K, device="cuda")).to(torch.bfloat16)
+    w2, cs, b2 = ops.fold_ln_weights(w, b, g, be)
+    st = torch.full((M, 2), float("nan"), device="cuda")
+    y = ops.linear_ln(x, w2, act="gelu", lna=(None, cs, b2, K, 1e-12), out_stats=st, tile_cfg=cfg)
+    _close(y, ops.linear_ln_ref(x, w, b, act="gelu", ln_x=(g, be)), 3e-2, 3e-2)
+    ref = _ln_stats(x)
+    assert torch.allclose(st, ref, rtol=1e-4, atol=1e-2), (st - ref).abs().max()
+    # LNR only: y2 = h @ w3.T + b3 + LN(x)
+    h = torch.randn(M, 384, device="cuda").to(torch.bfloat16)
+    w3 = (torch.randn(K, 384, device="cuda") * 384 ** -0.5).to(torch.bfloat16)
+    b3 = (torch.randn(K, device="cuda") * 0.1).to(torch.bfloat16)
+    y2 = ops.linear_ln(h, w3, b3, residual=x, lnr=(st, g, be, K, 1e-12), tile_cfg=cfg)
+    _close(y2, ops.linear_ln_ref(h, w3, b3, residual=x, ln_res=(g, be)), 3e-2, 3e-2)
+
+
+@pytest.mark.parametrize("cfg", [0, 1, 2])
+def test_qkv_attention_folded_layernorm(cfg):
+    """Fused projection+attention on RAW rows with the LayerNorm folded into the
+    packed weight == LayerNorm -> unfused reference; the statistics it
+    publishes (head 0) == a torch reduction; S < 128 so the 128-row tile
+    reaches into the next sequence (whose rows it must not publish)."""
+    ops = _ops()
+    torch.manual_seed(50 + cfg)
+    B, S, H, K = 5, 100, 4, 256
+    x = (torch.randn(B * S, K, device="cuda") * 1.3 - 0.2).to(torch.bfloat16)
+    w = (torch.randn(3 * H * 64, K, device="cuda") * K ** -0.5).to(torch.bfloat16)
+    b = (torch.randn(3 * H * 64, device="cuda") * 0.1).to(torch.bfloat16)
+    g = (1 + 0.2 * torch.randn(K, device="cuda")).to(torch.bfloat16)
+    be = (0.1 * torch.randn(K, device="cuda")).to(torch.bfloat16)
+    lens = torch.randint(1, S + 1, (B,), device="cuda", dtype=torch.int32)
+    w2, cs, bf = ops.fold_ln_weights(w, b, g, be)
+    wp, bfp = ops.pack_qkv_heads(w2, bf, H)
+    csp = ops.pack_qkv_vec(cs, H)
+    st = torch.full((B * S, 2), float("nan"), device="cuda")
+    y = ops.qkv_attention(x, wp, None, B, S, H, lens=lens, cfg=cfg, lna=(csp, bfp, 1e-12), stats_out=st)
+    xn = ops.layer_norm_ref(x, g, be, 1e-12)
+    _close(y, ops.qkv_attention_ref(xn, w, b, B, S, H, lens=lens), 3e-2, 3e-2)
+    ref = _ln_stats(x)
+    assert torch.allclose(st, ref, rtol=1e-4, atol=1e-2), (st - ref).abs().max()
+
+
 def test_layer_norm_row_strided_view_and_embed_zeroes_stats():
     ops = _ops()
     torch.manual_seed(1)
