@@ -75,6 +75,13 @@ class BertForSequenceClassification:
         # activation is never materialised; RDB_BERT_FUSED_ATTN=0 runs the
         # two-kernel path (GEMM -> ops.attention)
         self.fuse_qkv_attn = os.environ.get("RDB_BERT_FUSED_ATTN", "1") != "0"
+        # RDB_BERT_LNOUT=1: o-proj / FFN-down with the residual add AND the
+        # LayerNorm in the GEMM epilogue (ops.linear_residual_ln, row-panel
+        # statistics through a workspace + arrival counter): no LayerNorm kernel
+        # in the layer stack, but the panel wait (~2 memory round trips on the
+        # critical path) costs more than the LayerNorm kernel it removes
+        # (+11 us vs -5 us per GEMM, profiles/ab_r2.json) -- off by default
+        self.fuse_residual_ln = os.environ.get("RDB_BERT_LNOUT", "0") == "1"
         env = os.environ.get("RDB_BERT_FOLD_LN", "")
         self.fold_ln_auto = env == ""
         self.fold_ln = env == "1" or (env == "" and self.auto_fold_ln(1))
@@ -221,8 +228,11 @@ class BertForSequenceClassification:
         B, S = ids.shape
         D, H = c.hidden, c.heads
         lens = ops.seq_lens(ids, c.pad_token_id)
-        h = ops.embed_ln(ids, self.word, self.pos, self.typ, self.emb_g, self.emb_b, c.eps)
         n = len(self.layers)
+        lnout = self.fuse_residual_ln and self.dtype == torch.bfloat16 and D % 8 == 0
+        # row-panel LayerNorm workspaces, 2 per LNOUT GEMM: zeroed by the embedding kernel
+        ws = torch.empty(4 * n, B * S, 2, device=ids.device, dtype=torch.float32) if lnout else None
+        h = ops.embed_ln(ids, self.word, self.pos, self.typ, self.emb_g, self.emb_b, c.eps, zero_stats=ws)
         fuse = self.fuse_qkv_attn and ops.qkv_attention_supported(S, H, D // H, D)
         packed = self._packed_qkv() if fuse else None
         for i, L in enumerate(self.layers):
@@ -237,6 +247,14 @@ class BertForSequenceClassification:
                 # attention are row-wise, so they run on the B CLS rows (strided
                 # views, no copy) instead of B*S -- the same logits, ~1/12 fewer FLOPs.
                 ctx, h = ctx.view(B, S, D)[:, 0, :], h.view(B, S, D)[:, 0, :]
+            elif lnout:
+                h2 = h.reshape(B * S, D)
+                h1 = ops.linear_residual_ln(ctx, L["w_o"], L["b_o"], h2, L["ln1_g"], L["ln1_b"], c.eps,
+                                            ws[4 * i], ws[4 * i + 1].view(torch.int32))
+                inter = ops.linear(h1, L["w_i"], L["b_i"], act="gelu")
+                h = ops.linear_residual_ln(inter, L["w_out"], L["b_out"], h1, L["ln2_g"], L["ln2_b"], c.eps,
+                                           ws[4 * i + 2], ws[4 * i + 3].view(torch.int32))
+                continue
             a = ops.linear(ctx, L["w_o"], L["b_o"], residual=h)
             h1 = ops.layer_norm(a, L["ln1_g"], L["ln1_b"], c.eps)
             inter = ops.linear(h1, L["w_i"], L["b_i"], act="gelu")

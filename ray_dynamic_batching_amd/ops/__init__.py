@@ -330,6 +330,81 @@ def linear_ln(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = N
     return out
 
 
+LN_OUT = 16
+_LNOUT_ERR: Dict[int, torch.Tensor] = {}
+
+
+def _lnout_err(dev: torch.device) -> torch.Tensor:
+    i = dev.index if dev.index is not None else torch.cuda.current_device()
+    if i not in _LNOUT_ERR:
+        _LNOUT_ERR[i] = torch.zeros(1, device=dev, dtype=torch.int32)
+    return _LNOUT_ERR[i]
+
+
+def ln_out_error(device=None, reset: bool = True) -> bool:
+    """True if a ``linear_residual_ln`` row-panel wait timed out on ``device``
+    since the last reset (its output is then wrong; the kernel never hangs)."""
+    dev = torch.device("cuda", torch.cuda.current_device() if device is None else device)
+    e = _lnout_err(dev)
+    bad = bool(e.item())
+    if reset and bad:
+        e.zero_()
+    return bad
+
+
+def linear_residual_ln(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, residual: torch.Tensor,
+                       gamma: torch.Tensor, beta: torch.Tensor, eps: float, stats_ws: torch.Tensor,
+                       panel_ws: torch.Tensor, out: Optional[torch.Tensor] = None, tile_cfg: int = -1) -> torch.Tensor:
+    """y = LayerNorm(x @ w.T + bias + residual) * gamma + beta in ONE GEMM (bf16;
+    gemm_core.h EPI_LNOUT): the blocks of a row panel reduce the row statistics
+    through ``stats_ws`` (f32 [M, 2]) and ``panel_ws`` (int32, >= M entries),
+    which must be ZERO at launch (one use per zeroing: models/bert.py zeroes a
+    forward's workspaces in its embedding kernel).  The post-LN transformer's
+    o-proj -> LN1 and FFN-down -> LN2 without a LayerNorm kernel or the pre-LN
+    activation round trip."""
+    _check(x.is_cuda and x.dtype == torch.bfloat16 and w.dtype == x.dtype, "linear_residual_ln: bf16 on the GPU")
+    _check(w.dim() == 2 and w.is_contiguous(), "linear_residual_ln: w must be a contiguous [N, K] matrix")
+    N, K = w.shape
+    _check(x.dim() == 2 and x.stride(1) == 1 and x.shape[1] == K, "linear_residual_ln: x must be a 2-D [M, K] view")
+    M, lda = x.shape[0], x.stride(0)
+    _check(K % 8 == 0 and lda % 8 == 0 and N % 8 == 0 and _aligned(x) and _aligned(w), "linear_residual_ln: alignment")
+    _check(bias.is_contiguous() and bias.numel() == N and bias.dtype == x.dtype, "linear_residual_ln: bad bias")
+    _check(residual.dim() == 2 and residual.shape == (M, N) and residual.stride(1) == 1 and residual.stride(0) % 8 == 0
+           and residual.dtype == x.dtype and _aligned(residual), "linear_residual_ln: bad residual")
+    for v in (gamma, beta):
+        _check(v.is_contiguous() and v.numel() == N and v.dtype == x.dtype and _aligned(v), "linear_residual_ln: gamma/beta")
+    _check(stats_ws.dtype == torch.float32 and stats_ws.is_contiguous() and stats_ws.numel() >= 2 * M
+           and _aligned(stats_ws, 8), "linear_residual_ln: stats_ws must be contiguous f32 [M, 2]")
+    _check(panel_ws.dtype == torch.int32 and panel_ws.is_contiguous() and panel_ws.numel() >= M,
+           "linear_residual_ln: panel_ws must be contiguous int32 with >= M entries")
+    if out is None:
+        out = torch.empty(M, N, device=x.device, dtype=x.dtype)
+    _check(out.is_contiguous() and out.shape == (M, N) and _aligned(out), "linear_residual_ln: bad out")
+    err = _lnout_err(x.device)
+    fn = _ops().gemm_tn_ln
+
+    def launch(c):
+        fn(x.data_ptr(), lda, w.data_ptr(), K, out.data_ptr(), N, bias.data_ptr(), residual.data_ptr(),
+           residual.stride(0), M, N, K, 1.0, 0, LN_OUT, 0, 0, 0, 0, 0, 0, gamma.data_ptr(), beta.data_ptr(),
+           stats_ws.data_ptr(), 2, 0.0, 1.0 / N, float(eps), _stream(), int(c), panel=panel_ws.data_ptr(),
+           err=err.data_ptr())
+
+    if tile_cfg < 0:
+        key = ("gemm_lnout", M, N, K, lda)
+        tuned = key in _TUNE
+        tile_cfg = _tuned_cfg(key, launch, range(NUM_LN_TILE_CFGS))
+        if not tuned and not torch.cuda.is_current_stream_capturing():
+            stats_ws.zero_()         # the tuning launches used (and left) the workspaces
+            panel_ws.zero_()
+    launch(tile_cfg)
+    return out
+
+
+def linear_residual_ln_ref(x, w, bias, residual, gamma, beta, eps=1e-12):
+    y = x.float() @ w.float().t() + bias.float() + residual.float()
+    return F.layer_norm(y, (y.shape[-1],), gamma.float(), beta.float(), eps).to(x.dtype)
+
+
 def fold_ln_weights(w: torch.Tensor, b: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor):
     """(w', colsum, bias_f32) for ``linear_ln(lna=...)``: LN(x) @ w.T + b ==
     rstd * (x @ w'.T - mean * colsum) + bias_f32 with w' = w * gamma."""

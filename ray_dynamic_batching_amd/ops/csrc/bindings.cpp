@@ -17,7 +17,8 @@ void gemm_tn(int in_dtype, int out_dtype, uintptr_t A, int lda, uintptr_t W, int
 void gemm_tn_ln(uintptr_t A, int lda, uintptr_t W, int ldw, uintptr_t C, int ldc, uintptr_t bias, uintptr_t R,
                 int ldr, int M, int N, int K, float alpha, int act, int mode, uintptr_t a_stats, int a_ld,
                 uintptr_t a_colsum, uintptr_t a_bias, uintptr_t r_stats, int r_ld, uintptr_t r_g, uintptr_t r_b,
-                uintptr_t o_stats, int o_ld, float a_inv_d, float r_inv_d, float eps, uintptr_t stream, int cfg);
+                uintptr_t o_stats, int o_ld, float a_inv_d, float r_inv_d, float eps, uintptr_t stream, int cfg,
+                uintptr_t panel, uintptr_t err);
 void norm_fwd(int dtype, int mode, uintptr_t x, uintptr_t res, uintptr_t res_out, uintptr_t gamma,
               uintptr_t beta, uintptr_t y, int rows, int D, int ldx, float eps, uintptr_t stream);
 void embed_ln_fwd(int dtype, uintptr_t ids, uintptr_t types, uintptr_t word, uintptr_t pos,
@@ -69,7 +70,12 @@ static void hip_check(hipError_t e, const char* what) {
 PYBIND11_MODULE(_rdb_ops, m) {
   m.doc() = "ray_dynamic_batching_amd gfx950 kernels (MFMA GEMM/conv, norm, attention, ...)";
   m.def("gemm_tn", &rdb::gemm_tn, py::call_guard<py::gil_scoped_release>());
-  m.def("gemm_tn_ln", &rdb::gemm_tn_ln, py::call_guard<py::gil_scoped_release>());
+  m.def("gemm_tn_ln", &rdb::gemm_tn_ln, py::arg("A"), py::arg("lda"), py::arg("W"), py::arg("ldw"), py::arg("C"),
+        py::arg("ldc"), py::arg("bias"), py::arg("R"), py::arg("ldr"), py::arg("M"), py::arg("N"), py::arg("K"),
+        py::arg("alpha"), py::arg("act"), py::arg("mode"), py::arg("a_stats"), py::arg("a_ld"), py::arg("a_colsum"),
+        py::arg("a_bias"), py::arg("r_stats"), py::arg("r_ld"), py::arg("r_g"), py::arg("r_b"), py::arg("o_stats"),
+        py::arg("o_ld"), py::arg("a_inv_d"), py::arg("r_inv_d"), py::arg("eps"), py::arg("stream"), py::arg("cfg"),
+        py::arg("panel") = 0, py::arg("err") = 0, py::call_guard<py::gil_scoped_release>());
   m.def("norm_fwd", &rdb::norm_fwd, py::call_guard<py::gil_scoped_release>());
   m.def("embed_ln_fwd", &rdb::embed_ln_fwd, py::call_guard<py::gil_scoped_release>());
   m.def("attn_fwd", &rdb::attn_fwd, py::call_guard<py::gil_scoped_release>());

@@ -191,7 +191,11 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, char* lds, uint3
 // of A through the main loop) -- no producer-side statistics pass, no atomics.
 // Blocks of the first N tile also store them to o_stats (plain stores, one
 // writer per row) for a later LNR consumer of the same rows.
-constexpr int EPI_LNA = 1, EPI_LNR = 2, EPI_STATS = 4, EPI_SELF = 8;
+//
+// EPI_LNOUT: y = LayerNorm(A W^T + bias + R) written directly -- the GEMM's
+// row panel (the tiles_n blocks sharing BM rows) reduces each row's statistics
+// through a zeroed workspace and a per-panel arrival counter (staged_ln_epilogue).
+constexpr int EPI_LNA = 1, EPI_LNR = 2, EPI_STATS = 4, EPI_SELF = 8, EPI_LNOUT = 16;
 struct LnEpi {
   const float* a_stats;   // LNA: (sum, sumsq) of A's rows, row stride a_ld floats
   const float* a_colsum;  // LNA: colsum(W') [N]
@@ -200,8 +204,11 @@ struct LnEpi {
   const void* r_g;        // LNR: gamma, beta [N] (element type T)
   const void* r_b;
   float* o_stats;         // STATS: += (sum, sumsq) of the stored rows, row stride o_ld floats
+                          // LNOUT: zeroed [M, 2] workspace (row stride 2)
   int a_ld, r_ld, o_ld;
   float a_inv_d, r_inv_d, eps;
+  int* panel;             // LNOUT: zeroed arrival counters, one per row panel (tiles_m)
+  int* err;               // LNOUT: set to 1 if a panel wait timed out (never hangs)
 };
 
 // (sum, sum of squares) of the 8 elements of an MFMA fragment, accumulated with
@@ -331,6 +338,146 @@ __device__ __forceinline__ void staged_epilogue(char* smem, const f32x4 (&acc)[T
   }
 }
 
+// ---- GEMM + residual + LayerNorm epilogue (EPI_LNOUT) ---------------------------
+// y[m, :] = LN(alpha * acc + bias + R)[m, :] * gamma + beta for post-LN
+// transformers (BERT's o-proj -> LN1, FFN-down -> LN2): no LayerNorm kernel and
+// no pre-LN activation round trip.  A row's N columns are spread over the
+// tiles_n blocks of its row panel, so:
+//   1. the tile (+ bias + residual) is parked in LDS as f32 (staged layout),
+//      each row's partial (sum, sum of squares) accumulated with LDS atomics;
+//   2. one thread per row adds them to the zeroed workspace (system-scope float
+//      atomics: performed past the per-XCD L2s, so a panel may straddle XCDs),
+//      then thread 0 arrives on the panel's
+//      counter and waits (bounded: ~20 ms, then ln.err = 1 -- a wrong result,
+//      never a hang) until all tiles_n blocks arrived;
+//   3. the block reads the full statistics and writes normalised rows, 16 B
+//      per lane.
+// Deadlock freedom: blocks are dispatched in blockIdx order and xcd_remap keeps
+// a panel's tiles_n consecutive tiles on one XCD, so an incomplete panel only
+// waits on blocks behind the dispatched prefix, which are dispatched as soon as
+// complete panels (or other kernels) free their slots -- as long as an XCD has
+// more block slots than tiles_n (host-checked).  The workspace must be zeroed
+// before every launch (models/bert.py: the embedding kernel does it).
+template <int BM, int BN, int SMEM_BYTES>
+struct LnOutFit {
+  typedef StagedEpi<BM, BN, SMEM_BYTES> E;
+  static constexpr bool ok = E::RC == BM && BM * E::ROWB + BM * 8 <= SMEM_BYTES;
+};
+
+template <typename T, typename OutT, int BM, int BN, int SMEM_BYTES, int NT, int TM, int TN, int BIAS_LDS = -1>
+__device__ __forceinline__ void staged_ln_epilogue(char* smem, const f32x4 (&acc)[TN][TM], int row_base, int col_base,
+                                                   int m0, int n0, int M, int N, OutT* __restrict__ C, int ldc,
+                                                   const T* __restrict__ bias, const T* __restrict__ R, int ldr,
+                                                   float alpha, const LnEpi& ln, int tile_m, int tiles_n) {
+  typedef StagedEpi<BM, BN, SMEM_BYTES> E;
+  if constexpr (!LnOutFit<BM, BN, SMEM_BYTES>::ok) {
+    __builtin_trap();   // host-side ln_out_tile_ok() never launches this
+  } else {
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int fr = lane & 15, fg = lane >> 4;
+    float2* racc = reinterpret_cast<float2*>(smem + BM * E::ROWB);
+    // phase 1: alpha * acc + bias -> LDS (f32)
+#pragma unroll
+    for (int i = 0; i < TN; ++i) {
+      const int nt = col_base + i * 16 + fg * 4;
+      f32x4 bv;
+      if constexpr (BIAS_LDS >= 0) {
+        bv = *reinterpret_cast<const f32x4*>(smem + BIAS_LDS + nt * 4);
+      } else {
+        const __amdgpu_buffer_rsrc_t bsrc = make_rsrc(bias, (uint32_t)(N * sizeof(T)));
+        const u32x2 raw = bload8(bsrc, (uint32_t)((n0 + nt) * sizeof(T)));
+        const T* e = reinterpret_cast<const T*>(&raw);
+        bv = f32x4{(float)e[0], (float)e[1], (float)e[2], (float)e[3]};
+      }
+#pragma unroll
+      for (int j = 0; j < TM; ++j)
+        *reinterpret_cast<f32x4*>(smem + (row_base + j * 16 + fr) * E::ROWB + nt * 4) = acc[i][j] * alpha + bv;
+    }
+    for (int r = tid; r < BM; r += NT) racc[r] = float2{0.f, 0.f};
+    __syncthreads();
+    // phase 2a: + residual (16-B loads), x back to LDS, row partial sums (LDS atomics)
+#pragma unroll 4
+    for (int idx = tid; idx < BM * E::NV; idx += NT) {
+      const int r = idx / E::NV, vcol = idx - r * E::NV;
+      const int m = m0 + r, n = n0 + vcol * 8;
+      if (m < M && n < N) {
+        const u32x4 rraw = *reinterpret_cast<const u32x4*>(R + (size_t)m * ldr + n);
+        f32x4* p = reinterpret_cast<f32x4*>(smem + r * E::ROWB + vcol * 32);
+        f32x4 a = p[0], b = p[1];
+        const T* e = reinterpret_cast<const T*>(&rraw);
+        a += f32x4{(float)e[0], (float)e[1], (float)e[2], (float)e[3]};
+        b += f32x4{(float)e[4], (float)e[5], (float)e[6], (float)e[7]};
+        p[0] = a;
+        p[1] = b;
+        const float s = (a[0] + a[1]) + (a[2] + a[3]) + (b[0] + b[1]) + (b[2] + b[3]);
+        const float q = a[0] * a[0] + a[1] * a[1] + a[2] * a[2] + a[3] * a[3] + b[0] * b[0] + b[1] * b[1] +
+                        b[2] * b[2] + b[3] * b[3];
+        atomicAdd(&racc[r].x, s);
+        atomicAdd(&racc[r].y, q);
+      }
+    }
+    __syncthreads();
+    for (int r = tid; r < BM; r += NT) {
+      const int m = m0 + r;
+      if (m < M) {
+        __hip_atomic_fetch_add(ln.o_stats + (size_t)m * 2, racc[r].x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_fetch_add(ln.o_stats + (size_t)m * 2 + 1, racc[r].y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+    }
+    // Ordering without L2-wide fences (a release / acquire here is a whole-L2
+    // writeback / invalidate per block): every thread waits for ITS atomics to
+    // be acknowledged (gfx9 counts no-return atomics in vmcnt), the barrier
+    // joins them, then one relaxed arrival; readers poll and read with
+    // system-scope loads, which are served past the non-coherent L2s.
+    __builtin_amdgcn_s_waitcnt(0x70 | 0xF00);   // vmcnt(0)
+    __syncthreads();
+    if (tid == 0) {
+      int* cnt = ln.panel + tile_m;
+      __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();        // 100 MHz
+      while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < tiles_n) {
+        if (__builtin_amdgcn_s_memrealtime() - t0 > 2000000ull) {   // 20 ms
+          if (ln.err) __hip_atomic_store(ln.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+      }
+    }
+    __syncthreads();
+    for (int r = tid; r < BM; r += NT) {
+      const int m = m0 + r < M ? m0 + r : M - 1;
+      const float sm = __hip_atomic_load(ln.o_stats + (size_t)m * 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      const float sq = __hip_atomic_load(ln.o_stats + (size_t)m * 2 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      float mu, rstd;
+      ln_row_stats(float2{sm, sq}, ln.r_inv_d, ln.eps, mu, rstd);
+      racc[r] = float2{mu, rstd};
+    }
+    __syncthreads();
+    // phase 2b: normalise, gamma / beta, 16-B stores of whole lines
+    const T* g = static_cast<const T*>(ln.r_g);
+    const T* be = static_cast<const T*>(ln.r_b);
+#pragma unroll 4
+    for (int idx = tid; idx < BM * E::NV; idx += NT) {
+      const int r = idx / E::NV, vcol = idx - r * E::NV;
+      const int m = m0 + r, n = n0 + vcol * 8;
+      if (m < M && n < N) {
+        const u32x4 graw = *reinterpret_cast<const u32x4*>(g + n);
+        const u32x4 braw = *reinterpret_cast<const u32x4*>(be + n);
+        const T* ge = reinterpret_cast<const T*>(&graw);
+        const T* bb = reinterpret_cast<const T*>(&braw);
+        const f32x4 a = *reinterpret_cast<const f32x4*>(smem + r * E::ROWB + vcol * 32);
+        const f32x4 b = *reinterpret_cast<const f32x4*>(smem + r * E::ROWB + vcol * 32 + 16);
+        const float2 st = racc[r];
+        const float x[8] = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+        OutT o[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) o[q] = (OutT)((x[q] - st.x) * st.y * (float)ge[q] + (float)bb[q]);
+        *reinterpret_cast<u32x4*>(C + (size_t)m * ldc + n) = *reinterpret_cast<const u32x4*>(o);
+      }
+    }
+  }
+}
+
 template <typename T, typename OutT, bool HAS_RES>
 __device__ __forceinline__ bool staged_epilogue_ok(int N, const OutT* C, int ldc, const T* bias, const T* R, int ldr) {
   if constexpr (sizeof(OutT) != 2) return false;
@@ -358,7 +505,9 @@ mfma_gemm_kernel(typename LoaderT<T, 1>::Params ap, const T* __restrict__ W, int
                  const T* __restrict__ R, int ldr, int M, int N, int K, float alpha, int act, LnEpi ln) {
   constexpr bool LNA = (EPI & EPI_LNA) != 0, LNR = (EPI & EPI_LNR) != 0, OST = (EPI & EPI_STATS) != 0;
   constexpr bool SELF = (EPI & EPI_SELF) != 0;
+  constexpr bool LNOUT = (EPI & EPI_LNOUT) != 0;
   static_assert(!SELF || (LNA && !OST), "SELF computes LNA's statistics; it writes o_stats itself");
+  static_assert(!LNOUT || (EPI == EPI_LNOUT && HAS_BIAS && HAS_RES), "LNOUT: bias + residual, no other LN mode");
   static_assert(!LNA || !HAS_BIAS, "LNA takes its (folded) bias from ln.a_bias");
   static_assert(!LNR || HAS_RES, "LNR normalises the residual operand");
   constexpr int BK = 64;
@@ -526,6 +675,12 @@ mfma_gemm_kernel(typename LoaderT<T, 1>::Params ap, const T* __restrict__ W, int
     }
   }
 
+  if constexpr (LNOUT && sizeof(OutT) == 2) {
+    // host-checked: N % 8, ldc % 8, 16-B aligned C / R, ldr % 8, no activation
+    staged_ln_epilogue<T, OutT, BM, BN, kStages * kStage, NT, TM, TN>(smem, acc, wm * WM, wn * WN, m0, n0, M, N, C,
+                                                                     ldc, bias, R, ldr, alpha, ln, tile_m, tiles_n);
+    return;
+  }
   // ---- LDS-staged coalesced epilogue (plain modes; LN / SwiGLU keep the direct one) ----
   if constexpr (EPI == 0 && sizeof(OutT) == 2) {
     if (act != ACT_SWIGLU && staged_epilogue_ok<T, OutT, HAS_RES>(N, C, ldc, bias, R, ldr)) {
@@ -731,6 +886,18 @@ inline int tile_blocks_per_cu(int cfg) {
   const int lds = 2 * (kTileBM[cfg] + bnp) * 64 * 2;
   return std::min(8 / kTileNW[cfg], 163840 / lds);
 }
+// Whether tile cfg (0..18) can run the GEMM + residual + LayerNorm epilogue:
+// the whole f32 tile plus per-row accumulators must fit the staging LDS
+// (mirrors mfma_gemm_kernel's kStages / kStage and LnOutFit).
+inline bool ln_out_tile_ok(int cfg) {
+  if (cfg < 0 || cfg >= 19) return false;
+  const int nw = kTileNW[cfg], bm = kTileBM[cfg], bn = kTileBN[cfg];
+  const int wch = (bn + 8 * nw - 1) / (8 * nw);
+  const int stage = (bm + wch * 8 * nw) * 64 * 2;
+  const int stages = (3 * stage <= (nw == 4 ? 80 : 160) * 1024) ? 3 : 2;
+  return bm * (bn * 4 + 16) + bm * 8 <= stages * stage;
+}
+
 // Heuristic: minimise (rounds of blocks over 256 CUs) x (tile work / tile efficiency).
 constexpr int kNumTiles4 = 13;  // tiles 0..12 are 4-wave (every loader); 13.. are 8-wave (dense only)
 inline int pick_tile_cfg(int M, int N, bool dense) {

@@ -6,6 +6,9 @@
 //   mode STATS        y = A W^T + bias + R,                 stats[m] += (sum y, sum y^2)
 //   mode LNR | STATS  y = A W^T + bias + LN(R) (normalised on load), stats[m] += ...
 //   mode LNR          y = A W^T + bias + LN(R)
+//   mode LNOUT        y = LN(A W^T + bias + R) (gamma r_g, beta r_b): the row
+//                     panel reduces statistics through o_stats (zeroed [M, 2])
+//                     and the panel counters (zeroed int [tiles_m])
 //   mode LNA | SELF   as LNA, but A's row statistics are computed by this GEMM
 //                     from the A tiles of its own main loop; the first N-tile's
 //                     blocks store them to o_stats (for a later LNR of A)
@@ -21,7 +24,8 @@ namespace rdb {
 void gemm_tn_ln(uintptr_t A, int lda, uintptr_t W, int ldw, uintptr_t C, int ldc, uintptr_t bias, uintptr_t R,
                 int ldr, int M, int N, int K, float alpha, int act, int mode, uintptr_t a_stats, int a_ld,
                 uintptr_t a_colsum, uintptr_t a_bias, uintptr_t r_stats, int r_ld, uintptr_t r_g, uintptr_t r_b,
-                uintptr_t o_stats, int o_ld, float a_inv_d, float r_inv_d, float eps, uintptr_t stream, int cfg) {
+                uintptr_t o_stats, int o_ld, float a_inv_d, float r_inv_d, float eps, uintptr_t stream, int cfg,
+                uintptr_t panel, uintptr_t err) {
   if (K % 8 != 0 || lda % 8 != 0 || ldw % 8 != 0) throw std::invalid_argument("gemm_tn_ln: K/lda/ldw % 8");
   if ((A | W) & 15) throw std::invalid_argument("gemm_tn_ln: A/W must be 16-byte aligned");
   if (N % 4 != 0 || ldc % 4 != 0) throw std::invalid_argument("gemm_tn_ln: N and ldc must be multiples of 4");
@@ -38,6 +42,8 @@ void gemm_tn_ln(uintptr_t A, int lda, uintptr_t W, int ldw, uintptr_t C, int ldc
   ln.o_stats = reinterpret_cast<float*>(o_stats);
   ln.a_ld = a_ld; ln.r_ld = r_ld; ln.o_ld = o_ld;
   ln.a_inv_d = a_inv_d; ln.r_inv_d = r_inv_d; ln.eps = eps;
+  ln.panel = reinterpret_cast<int*>(panel);
+  ln.err = reinterpret_cast<int*>(err);
   DenseParams p{reinterpret_cast<const void*>(A), lda, M, K};
   auto w = reinterpret_cast<const bf16*>(W);
   auto b = reinterpret_cast<const bf16*>(bias);
@@ -68,13 +74,35 @@ void gemm_tn_ln(uintptr_t A, int lda, uintptr_t W, int ldw, uintptr_t C, int ldc
       launch_mfma_gemm_t<bf16, bf16, DenseLoader, true, true, EPI_LNR>(p, w, ldw, c, ldc, b, r, ldr, M, N, K, alpha,
                                                                        act, s, cfg, ln);
       break;
+    case EPI_LNOUT: {
+      need(bias && R && r_g && r_b && o_stats && panel && act == ACT_NONE,
+           "gemm_tn_ln: LNOUT needs bias, R, r_g/r_b, o_stats, panel workspaces and no activation");
+      need(N % 8 == 0 && ldc % 8 == 0 && ldr % 8 == 0 && ((C | R | r_g | r_b) & 15) == 0,
+           "gemm_tn_ln: LNOUT needs N, ldc, ldr % 8 and 16-byte aligned C, R, gamma, beta");
+      if (!ln_out_tile_ok(cfg)) cfg = -1;
+      if (cfg >= 0) {   // every block of a row panel must be able to be resident at once
+        const long tiles = (long)((M + kTileBM[cfg] - 1) / kTileBM[cfg]) * ((N + kTileBN[cfg] - 1) / kTileBN[cfg]);
+        if (tiles > 256L * tile_blocks_per_cu(cfg)) cfg = -1;
+      }
+      if (cfg < 0) {
+        for (int t = 0; t < 19 && cfg < 0; ++t) {
+          const long tiles = (long)((M + kTileBM[t] - 1) / kTileBM[t]) * ((N + kTileBN[t] - 1) / kTileBN[t]);
+          if (ln_out_tile_ok(t) && tiles <= 256L * tile_blocks_per_cu(t)) cfg = t;
+        }
+        need(cfg >= 0, "gemm_tn_ln: LNOUT: no tile keeps every row panel resident at this M, N");
+      }
+      launch_mfma_gemm_t<bf16, bf16, DenseLoader, true, true, EPI_LNOUT>(p, w, ldw, c, ldc, b, r, ldr, M, N, K, alpha,
+                                                                         act, s, cfg, ln);
+      break;
+    }
     case EPI_LNA | EPI_SELF:
       need(a_colsum && a_bias && !bias && !R, "gemm_tn_ln: LNA|SELF needs a_colsum/a_bias, no bias/R");
       launch_mfma_gemm_t<bf16, bf16, DenseLoader, false, false, EPI_LNA | EPI_SELF>(p, w, ldw, c, ldc, b, r, ldr, M, N,
                                                                                     K, alpha, act, s, cfg, ln);
       break;
     default:
-      throw std::invalid_argument("gemm_tn_ln: mode must be LNA (1), STATS (4), LNR|STATS (6), LNR (2) or LNA|SELF (9)");
+      throw std::invalid_argument(
+          "gemm_tn_ln: mode must be LNA (1), STATS (4), LNR|STATS (6), LNR (2), LNA|SELF (9) or LNOUT (16)");
   }
   RDB_HIP_CHECK(hipGetLastError());
 }

@@ -52,6 +52,48 @@ def test_bert_fused_qkv_attention_matches_unfused_and_torch():
 
 
 @pytest.mark.parametrize("cls_only", [True, False])
+def test_bert_gemm_residual_layernorm_matches_layernorm_kernels(cls_only):
+    """o-proj / FFN-down with residual + LayerNorm in the GEMM epilogue (no
+    LayerNorm kernels) == GEMM -> LayerNorm kernel == eager torch, under a
+    hipGraph replayed several times (the workspaces are re-zeroed per replay by
+    the embedding kernel)."""
+    from ray_dynamic_batching_amd import ops
+    from ray_dynamic_batching_amd.models.bert import BertConfig, BertForSequenceClassification
+
+    m = BertForSequenceClassification(BertConfig(layers=4), device="cuda", backend="hip", seed=8)
+    g = torch.Generator(device="cpu").manual_seed(9)
+    for L in m.layers:
+        for k in ("ln1_g", "ln2_g"):
+            L[k].copy_(1 + 0.2 * torch.randn(L[k].shape, generator=g))
+        for k in ("ln1_b", "ln2_b"):
+            L[k].copy_(0.1 * torch.randn(L[k].shape, generator=g))
+    m.fold_ln = False
+    m.cls_only_last_layer = cls_only
+    ids = m.example_input(16, seed=10)
+    ids[4, 50:] = 0
+    m.fuse_residual_ln = True
+    y = m(ids)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    gr = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(gr, stream=s):
+            yg = m(ids)
+    torch.cuda.synchronize()
+    for _ in range(3):
+        gr.replay()
+        torch.cuda.synchronize()
+        assert torch.allclose(yg, y, atol=1e-2, rtol=1e-2), (yg - y).abs().max()
+    assert not ops.ln_out_error()
+    m.fuse_residual_ln = False
+    y2 = m(ids)
+    m.backend = "torch"
+    ref = m(ids)
+    assert torch.allclose(y, y2, atol=3e-2, rtol=3e-2), (y - y2).abs().max()
+    assert torch.allclose(y, ref, atol=5e-2, rtol=5e-2), (y - ref).abs().max()
+
+
+@pytest.mark.parametrize("cls_only", [True, False])
 @pytest.mark.parametrize("fused", [True, False])
 def test_bert_folded_layernorm_matches_unfolded(cls_only, fused):
     """The deferred-LayerNorm forwards (fused: qkv_attention + in-kernel row

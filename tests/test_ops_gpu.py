@@ -487,6 +487,35 @@ def test_qkv_attention_folded_layernorm(cfg):
     assert torch.allclose(st, ref, rtol=1e-4, atol=1e-2), (st - ref).abs().max()
 
 
+@pytest.mark.parametrize("cfg", list(range(19)))
+@pytest.mark.parametrize("M", [4096, 520])
+def test_linear_residual_ln_all_tiles(cfg, M):
+    """GEMM + bias + residual + LayerNorm in one kernel (row-panel statistics):
+    every tile (those that cannot hold the f32 tile are remapped on the host),
+    M = 520 leaves a partial last row panel and makes panels straddle XCDs
+    (xcd_remap: 9 tiles per XCD with 8 tiles per panel at 64x96).  Repeated
+    launches on re-zeroed workspaces agree (up to the f32 atomic order)."""
+    ops = _ops()
+    torch.manual_seed(60 + cfg)
+    N, K = 768, 768
+    x = torch.randn(M, K, device="cuda").to(torch.bfloat16)
+    w = (torch.randn(N, K, device="cuda") * K ** -0.5).to(torch.bfloat16)
+    b = (torch.randn(N, device="cuda") * 0.1).to(torch.bfloat16)
+    r = (torch.randn(M, N, device="cuda") * 2 + 0.5).to(torch.bfloat16)
+    g = (1 + 0.2 * torch.randn(N, device="cuda")).to(torch.bfloat16)
+    be = (0.1 * torch.randn(N, device="cuda")).to(torch.bfloat16)
+    ref = ops.linear_residual_ln_ref(x, w, b, r, g, be)
+    outs = []
+    for _ in range(2):
+        st = torch.zeros(M, 2, device="cuda")
+        pn = torch.zeros(M, device="cuda", dtype=torch.int32)
+        outs.append(ops.linear_residual_ln(x, w, b, r, g, be, 1e-12, st, pn, tile_cfg=cfg))
+    torch.cuda.synchronize()
+    assert not ops.ln_out_error()
+    _close(outs[0], ref, 3e-2, 3e-2)
+    _close(outs[1], outs[0], 1e-2, 1e-2)
+
+
 def test_layer_norm_row_strided_view_and_embed_zeroes_stats():
     ops = _ops()
     torch.manual_seed(1)
