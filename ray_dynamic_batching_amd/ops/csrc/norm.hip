@@ -5,6 +5,7 @@
 // registers between the statistics pass and the output pass, so each element
 // is read from HBM exactly once.
 #include "common.h"
+#include <cstdlib>
 #include <stdexcept>
 
 namespace rdb {
@@ -100,6 +101,91 @@ norm_kernel(const T* __restrict__ x, const T* __restrict__ res, T* __restrict__ 
       }
       if (c < D) st4(yr + c, o);
     }
+  }
+}
+
+// Half-wave-per-row form for rows of 256 * NV16 elements with 16-B aligned
+// operands (the transformer hidden sizes: 768 = 3 x 256, 1024, 4096): 32 lanes
+// own a row, each lane NV16 16-B vectors (8 elements), so every load / store
+// instruction moves 512 B of ONE row and a wave keeps two rows in flight; the
+// row reductions stay inside the half wave (xor 1..16: DPP / swizzle, no
+// cross-half ds_bpermute).  Two passes (mean, then centered variance) over the
+// register-resident row.  Measured against norm_kernel: bench/launch_floor.py.
+template <typename T>
+__device__ __forceinline__ void load8(const T* p, float* o) {
+  const u32x4 raw = *reinterpret_cast<const u32x4*>(p);
+  const T* e = reinterpret_cast<const T*>(&raw);
+#pragma unroll
+  for (int q = 0; q < 8; ++q) o[q] = (float)e[q];
+}
+template <typename T>
+__device__ __forceinline__ void st8(T* p, const float* o) {
+  T v[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) v[q] = (T)o[q];
+  *reinterpret_cast<u32x4*>(p) = *reinterpret_cast<const u32x4*>(v);
+}
+__device__ __forceinline__ float half_sum(float v) {
+#pragma unroll
+  for (int o = 16; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+template <typename T, int MODE, int NV16>
+__global__ void __launch_bounds__(256)
+norm16_kernel(const T* __restrict__ x, const T* __restrict__ res, T* __restrict__ res_out,
+              const T* __restrict__ gamma, const T* __restrict__ beta, T* __restrict__ y, int rows, int ldx,
+              float eps) {
+  constexpr int D = 256 * NV16;
+  const int hl = threadIdx.x & 31;
+  const int row = blockIdx.x * 8 + (threadIdx.x >> 5);
+  if (row >= rows) return;
+  const T* xr = x + (size_t)row * ldx;
+  float v[NV16][8];
+#pragma unroll
+  for (int i = 0; i < NV16; ++i) load8(xr + i * 256 + hl * 8, v[i]);
+  if (res != nullptr) {
+#pragma unroll
+    for (int i = 0; i < NV16; ++i) {
+      float r[8];
+      load8(res + (size_t)row * D + i * 256 + hl * 8, r);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) v[i][q] += r[q];
+      if (res_out != nullptr) st8(res_out + (size_t)row * D + i * 256 + hl * 8, v[i]);
+    }
+  }
+  float mean = 0.f, rstd;
+  if constexpr (MODE == 0) {
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < NV16; ++i)
+#pragma unroll
+      for (int q = 0; q < 8; ++q) s += v[i][q];
+    mean = half_sum(s) * (1.0f / D);
+    float qs = 0.f;
+#pragma unroll
+    for (int i = 0; i < NV16; ++i)
+#pragma unroll
+      for (int q = 0; q < 8; ++q) { const float d = v[i][q] - mean; qs += d * d; }
+    rstd = rsqrtf(half_sum(qs) * (1.0f / D) + eps);
+  } else {
+    float qs = 0.f;
+#pragma unroll
+    for (int i = 0; i < NV16; ++i)
+#pragma unroll
+      for (int q = 0; q < 8; ++q) qs += v[i][q] * v[i][q];
+    rstd = rsqrtf(half_sum(qs) * (1.0f / D) + eps);
+  }
+  T* yr = y + (size_t)row * D;
+#pragma unroll
+  for (int i = 0; i < NV16; ++i) {
+    const int c = i * 256 + hl * 8;
+    float g[8], b[8], o[8];
+    load8(gamma + c, g);
+    if constexpr (MODE == 0) load8(beta + c, b);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) o[q] = MODE == 0 ? (v[i][q] - mean) * rstd * g[q] + b[q] : v[i][q] * rstd * g[q];
+    st8(yr + c, o);
   }
 }
 
@@ -211,12 +297,42 @@ static void launch_embed(dim3 grid, hipStream_t s, uintptr_t ids, uintptr_t type
 #undef RDB_CASE
 }
 
+template <typename T, int MODE>
+static bool launch_norm16(hipStream_t s, uintptr_t x, uintptr_t res, uintptr_t res_out, uintptr_t gamma,
+                          uintptr_t beta, uintptr_t y, int rows, int D, int ldx, float eps) {
+  const dim3 grid((rows + 7) / 8), blk(256);
+#define RDB_N16(NV)                                                                                         \
+  if (D == 256 * NV) {                                                                                      \
+    hipLaunchKernelGGL((norm16_kernel<T, MODE, NV>), grid, blk, 0, s, (const T*)x, (const T*)res, (T*)res_out, \
+                       (const T*)gamma, (const T*)beta, (T*)y, rows, ldx, eps);                              \
+    return true;                                                                                            \
+  }
+  RDB_N16(1) RDB_N16(2) RDB_N16(3) RDB_N16(4) RDB_N16(8) RDB_N16(16)
+#undef RDB_N16
+  return false;
+}
+
 void norm_fwd(int dtype, int mode, uintptr_t x, uintptr_t res, uintptr_t res_out, uintptr_t gamma,
               uintptr_t beta, uintptr_t y, int rows, int D, int ldx, float eps, uintptr_t stream) {
   if (D % 4 != 0 || D <= 0 || D > 8192) throw std::invalid_argument("norm: D must be a multiple of 4, <= 8192");
   if (ldx < D || ldx % 4 != 0 || (ldx != D && res != 0)) throw std::invalid_argument("norm: bad x row stride");
   if (rows <= 0) return;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  // 16-B half-wave form when every operand allows it (RDB_NORM16=0 forces the 8-B form)
+  static const bool n16_env = [] { const char* e = getenv("RDB_NORM16"); return !(e && e[0] == '0'); }();
+  const bool a16 = ((x | res | res_out | gamma | beta | y) & 15) == 0 && ldx % 8 == 0 && D % 256 == 0;
+  if (n16_env && a16) {
+    bool ok;
+    if (dtype == 0) ok = mode == 0 ? launch_norm16<bf16, 0>(s, x, res, res_out, gamma, beta, y, rows, D, ldx, eps)
+                                   : launch_norm16<bf16, 1>(s, x, res, res_out, gamma, beta, y, rows, D, ldx, eps);
+    else if (dtype == 1) ok = mode == 0 ? launch_norm16<f16, 0>(s, x, res, res_out, gamma, beta, y, rows, D, ldx, eps)
+                                        : launch_norm16<f16, 1>(s, x, res, res_out, gamma, beta, y, rows, D, ldx, eps);
+    else ok = false;
+    if (ok) {
+      RDB_HIP_CHECK(hipGetLastError());
+      return;
+    }
+  }
   dim3 grid((rows + 3) / 4);
   if (dtype == 0) {
     if (mode == 0) launch_norm<bf16, 0>(grid, s, x, res, res_out, gamma, beta, y, rows, D, ldx, eps);

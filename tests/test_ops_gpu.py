@@ -75,7 +75,7 @@ def test_linear_strided_rows():
     _close(ops.linear(cls, w, act="tanh"), ops.linear_ref(cls.contiguous(), w, act="tanh"), 2e-2, 2e-2)
 
 
-@pytest.mark.parametrize("D", [768, 1024, 4096])
+@pytest.mark.parametrize("D", [768, 1024, 4096, 320])
 def test_norms(D):
     ops = _ops()
     torch.manual_seed(3)
