@@ -43,12 +43,12 @@ struct QkvLn {
   float inv_d, eps;
 };
 
-template <typename T, int NW, int STAGES, bool LNA>
+template <typename T, int NW, int STAGES, bool LNA, int WGM_ = (NW == 8 ? 4 : 2)>
 __global__ void __launch_bounds__(64 * NW, NW == 8 && STAGES == 3 ? 1 : 2)
 qkv_attn_kernel(DenseParams ap, const T* __restrict__ W, const T* __restrict__ bias, int S, int H,
                 const int* __restrict__ lens, T* __restrict__ out, int ld_out, float scale_log2e, QkvLn ln) {
   constexpr int BM = 128, BN = 192, BK = 64, D = 64;
-  constexpr int WGM = NW == 8 ? 4 : 2, WGN = 2;
+  constexpr int WGM = WGM_, WGN = NW / WGM_;
   constexpr int NT = 64 * NW;
   constexpr int WM = BM / WGM, WN = BN / WGN;       // 32|64 x 96
   constexpr int TM = WM / 16, TN = WN / 16;
@@ -308,8 +308,9 @@ qkv_attn_kernel(DenseParams ap, const T* __restrict__ W, const T* __restrict__ b
   }
 }
 
-// cfg: 0 = 8 waves / 3 stages (1 block per CU), 1 = 8 waves / 2 stages, 2 = 4 waves / 2 stages
-constexpr int kNumQkvAttnCfgs = 3;
+// cfg: 0 = 8 waves (4x2) / 3 stages (1 block per CU), 1 = 8 waves (4x2) / 2 stages, 2 = 4 waves / 2 stages,
+//      3 = 8 waves (2x4: 64x48 wave tiles, fewer LDS fragment reads per MFMA) / 2 stages
+constexpr int kNumQkvAttnCfgs = 4;
 
 template <typename T, bool LNA>
 static void launch_qkv_attn(int cfg, const DenseParams& p, const T* W, const T* bias, int B, int S, int H,
@@ -323,6 +324,10 @@ static void launch_qkv_attn(int cfg, const DenseParams& p, const T* W, const T* 
     case 1:
       hipLaunchKernelGGL((qkv_attn_kernel<T, 8, 2, LNA>), grid, dim3(512), 0, s, p, W, bias, S, H, lens, out, ld_out,
                          sl2e, ln);
+      break;
+    case 3:
+      hipLaunchKernelGGL((qkv_attn_kernel<T, 8, 2, LNA, 2>), grid, dim3(512), 0, s, p, W, bias, S, H, lens, out,
+                         ld_out, sl2e, ln);
       break;
     default:
       hipLaunchKernelGGL((qkv_attn_kernel<T, 4, 2, LNA>), grid, dim3(256), 0, s, p, W, bias, S, H, lens, out, ld_out,
