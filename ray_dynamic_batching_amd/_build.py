@@ -96,19 +96,30 @@ def hipcc() -> str:
     return p
 
 
-def build_ops(force: bool = False, jobs: int | None = None, verbose: bool = False) -> Path:
-    target = ops_target()
+def variant_target(name: str) -> Path:
+    """Where ``build_ops(variant=name)`` puts an A/B build of the kernels
+    (loaded instead of the default one when ``RDB_OPS_SO`` points at it)."""
+    return PKG / "_variants" / name / f"_rdb_ops{EXT}"
+
+
+def build_ops(force: bool = False, jobs: int | None = None, verbose: bool = False, variant: str = "",
+              defines: tuple = ()) -> Path:
+    """Build _rdb_ops; ``variant`` + ``defines`` (e.g. ("RDB_GEMM_GROUPED",)) build
+    an A/B copy under ``_variants/<variant>/`` from separate objects."""
+    target = variant_target(variant) if variant else ops_target()
+    bdir = BUILD / ("variant-" + variant) if variant else BUILD
     srcs = _ops_sources()
     if not force and not _stale(target, _deps(srcs, [OPS_SRC, RT_SRC])):
         return target
-    BUILD.mkdir(parents=True, exist_ok=True)
+    bdir.mkdir(parents=True, exist_ok=True)
+    target.parent.mkdir(parents=True, exist_ok=True)
     cc = hipcc()
     common = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wno-unused-result",
-              f"-I{OPS_SRC}", f"-I{RT_SRC}"] + _pybind_includes()
+              f"-I{OPS_SRC}", f"-I{RT_SRC}"] + _pybind_includes() + [f"-D{d}" for d in defines]
     objs = []
     cmds = []
     for s in srcs:
-        o = BUILD / (s.name + ".o")
+        o = bdir / (s.name + ".o")
         objs.append(o)
         newest = max(p.stat().st_mtime for p in [s] + _local_includes(s))
         if not force and o.exists() and o.stat().st_mtime >= newest:
@@ -154,7 +165,12 @@ def main(argv=None) -> int:
     ap.add_argument("--force", action="store_true")
     ap.add_argument("--only", choices=["ops", "runtime"])
     ap.add_argument("-v", "--verbose", action="store_true")
+    ap.add_argument("--variant", default="", help="A/B build name (kernels only), with -D defines")
+    ap.add_argument("-D", dest="defines", action="append", default=[])
     a = ap.parse_args(argv)
+    if a.variant:
+        print("built", build_ops(a.force, verbose=a.verbose, variant=a.variant, defines=tuple(a.defines)))
+        return 0
     if a.only in (None, "runtime"):
         print("built", build_runtime(a.force))
     if a.only in (None, "ops"):

@@ -537,6 +537,10 @@ mfma_gemm_kernel(typename LoaderT<T, 1>::Params ap, const T* __restrict__ W, int
   const int tiles_m = (M + BM - 1) / BM;
   const int nwg = tiles_m * tiles_n;
   const int t = xcd_remap(blockIdx.x, nwg);
+  // row-major tile order: an XCD gets whole row panels.  A grouped (GM x N/GM
+  // block per XCD) order lowers the per-XCD operand bytes on paper but measured
+  // -5 % req/s (profiles/ab_r2.json): the row panels of consecutive kernels
+  // then land on the XCD whose L2 holds the producer's rows.
   const int tile_m = t / tiles_n, tile_n = t - tile_m * tiles_n;
   const int m0 = tile_m * BM, n0 = tile_n * BN;
 

@@ -7,7 +7,9 @@ fallback to eager PyTorch on the GPU path.
 from __future__ import annotations
 
 import importlib
+import importlib.util
 import os
+import sys
 import threading
 
 _lock = threading.Lock()
@@ -50,6 +52,14 @@ def load_ops():
             import torch  # noqa: F401  (shares its HIP runtime)
             from .. import _build
 
+            alt = os.environ.get("RDB_OPS_SO", "")
+            if alt:
+                # A/B runs: a variant build (python -m ray_dynamic_batching_amd._build --variant X -D ...)
+                spec = importlib.util.spec_from_file_location("ray_dynamic_batching_amd._rdb_ops", alt)
+                _ops = importlib.util.module_from_spec(spec)
+                spec.loader.exec_module(_ops)
+                sys.modules["ray_dynamic_batching_amd._rdb_ops"] = _ops
+                return _ops
             if os.environ.get("RDB_NO_AUTOBUILD") != "1":
                 _build.build_ops()
             _ops = importlib.import_module("ray_dynamic_batching_amd._rdb_ops")

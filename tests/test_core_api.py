@@ -1,0 +1,206 @@
+"""Ray-core-compatible API (ray_dynamic_batching_amd.core): actors as pinned
+processes (and in local mode), ordering, errors, named actors across drivers,
+tasks, put/get/wait, util.queue.Queue semantics, and the fork's structure --
+GPU worker actors draining per-model RayQueues (293-project/src/scheduler.py)."""
+import os
+import subprocess
+import sys
+import textwrap
+import time
+import uuid
+
+import cloudpickle
+import pytest
+
+import ray_dynamic_batching_amd.core as ray
+from ray_dynamic_batching_amd.core.util.queue import Empty, Full, Queue
+
+cloudpickle.register_pickle_by_value(sys.modules[__name__])
+
+
+@pytest.fixture(params=["process", "local"])
+def rt(request):
+    ray.init(num_gpus=2, local_mode=request.param == "local", namespace="t" + uuid.uuid4().hex[:8])
+    yield request.param
+    ray.shutdown()
+
+
+class Counter:
+    def __init__(self, start=0):
+        self.n = start
+
+    def incr(self, k=1):
+        self.n += k
+        return self.n
+
+    def gpus(self):
+        import ray_dynamic_batching_amd.core as r
+
+        return r.get_gpu_ids(), os.environ.get("HIP_VISIBLE_DEVICES")
+
+    def boom(self):
+        raise ValueError("bad input")
+
+    async def aget(self):
+        return self.n
+
+
+def test_actor_calls_ordering_errors_and_gpu_pinning(rt):
+    C = ray.remote(num_gpus=1)(Counter)
+    a, b = C.remote(10), C.options(name="second").remote()
+    refs = [a.incr.remote() for _ in range(50)]
+    assert ray.get(refs) == list(range(11, 61))                      # per-caller FIFO
+    assert ray.get(a.aget.remote()) == 60                            # async method
+    ga, gb = ray.get(a.gpus.remote()), ray.get(b.gpus.remote())
+    assert sorted([ga[0], gb[0]]) == [[0], [1]]                       # whole GPUs, first-fit
+    if rt == "process":
+        assert ga[1] == str(ga[0][0])                                # HIP_VISIBLE_DEVICES pinned
+    assert ray.available_resources()["GPU"] == 0.0
+    with pytest.raises(ray.RayTaskError) as e:
+        ray.get(a.boom.remote())
+    assert isinstance(e.value.cause, ValueError) and "bad input" in str(e.value)
+    # no GPU left: creation waits, then fails; killing an actor frees its GPU
+    os.environ["RDB_CORE_PENDING_TIMEOUT_S"] = "0.3"
+    try:
+        with pytest.raises(ray.RayError):
+            C.remote()
+        ray.kill(b)
+        c = C.remote(5)
+        assert ray.get(c.incr.remote()) == 6
+    finally:
+        del os.environ["RDB_CORE_PENDING_TIMEOUT_S"]
+    # fractional GPUs co-locate best-fit on the freed... fully used -> none left
+    assert ray.available_resources()["GPU"] == 0.0
+
+
+def test_tasks_put_get_wait(rt):
+    @ray.remote
+    def add(x, y):
+        time.sleep(0.01 * y)
+        return x + y
+
+    r = ray.put(40)
+    refs = [add.remote(r, i) for i in range(5)]                      # ObjectRef args resolved
+    ready, rest = ray.wait(refs, num_returns=2, timeout=5)
+    assert len(ready) == 2 and len(rest) == 3
+    assert ray.get(refs) == [40, 41, 42, 43, 44]
+    with pytest.raises(ray.GetTimeoutError):
+        ray.get(add.remote(0, 100), timeout=0.05)
+
+
+def test_queue_semantics(rt):
+    q = Queue(maxsize=2)
+    assert q.empty() and not q.full()
+    q.put(1)
+    q.put_nowait(2)
+    assert q.full() and q.qsize() == 2
+    with pytest.raises(Full):
+        q.put_nowait(3)
+    with pytest.raises(Full):
+        q.put(3, timeout=0.05)
+    assert q.get() == 1 and q.get_nowait() == 2
+    with pytest.raises(Empty):
+        q.get(timeout=0.05)
+    with pytest.raises(Empty):
+        q.get_nowait()
+    q.put_nowait_batch([7, 8])
+    with pytest.raises(Full):
+        q.put_nowait_batch([9])
+    with pytest.raises(Empty):
+        q.get_nowait_batch(3)
+    assert q.get_nowait_batch(2) == [7, 8]
+    q.shutdown()
+
+
+class GPUWorker:
+    """The fork's worker shape: pinned to one GPU, drains its model queues."""
+
+    def __init__(self, name):
+        self.name = name
+
+    def execute(self, queues, n):
+        import ray_dynamic_batching_amd.core as r
+
+        # nested refs stay refs (Ray semantics): the worker gets them, as the fork's executor does
+        queues = {m: r.get(q) if isinstance(q, r.ObjectRef) else q for m, q in queues.items()}
+        out = []
+        while True:       # drain until every model queue is empty (n: batch size cap)
+            took = 0
+            for model, q in queues.items():
+                try:
+                    got = q.get_nowait_batch(min(q.qsize(), n))
+                except Empty:          # another worker emptied it meanwhile
+                    got = []
+                out.extend((model, x) for x in got)
+                took += len(got)
+            if not took and all(q.empty() for q in queues.values()):
+                return self.name, r.get_gpu_ids(), out
+
+
+def test_fork_structure_workers_drain_model_queues(rt):
+    queues = {"resnet": Queue(maxsize=64), "vit": Queue(maxsize=64)}
+    W = ray.remote(num_gpus=1)(GPUWorker)
+    workers = [W.options(name=f"gpu{i}").remote(f"gpu{i}") for i in range(2)]
+    qrefs = {m: ray.put(q) for m, q in queues.items()}                # ray.put(queue) as the fork does
+    for i in range(10):
+        queues["resnet"].put(i)
+        queues["vit"].put(100 + i)
+    futs = [w.execute.remote(qrefs, 4) for w in workers]
+    res = ray.get(futs, timeout=60)
+    got = sorted(x for _, _, out in res for _, x in out)
+    assert got == sorted(list(range(10)) + [100 + i for i in range(10)])
+    assert sorted(g[0] for _, g, _ in res) == [0, 1]
+    acts = ray.state.actors()
+    assert {a["Name"] for a in acts.values()} >= {"gpu0", "gpu1"}
+    assert all(a["State"] == "ALIVE" for a in acts.values())
+
+
+def test_named_actor_from_another_driver():
+    ns = "x" + uuid.uuid4().hex[:8]
+    ray.init(num_gpus=0, namespace=ns)
+    try:
+        h = ray.remote(Counter).options(name="tracker", lifetime="detached").remote(3)
+        assert ray.get(h.incr.remote()) == 4
+        with pytest.raises(ValueError):
+            ray.remote(Counter).options(name="tracker").remote()
+        code = textwrap.dedent(f"""
+            import ray_dynamic_batching_amd.core as ray
+            ray.init(address="auto", namespace="{ns}")
+            h = ray.get_actor("tracker")
+            print(ray.get(h.incr.remote(10)))
+            ray.shutdown()
+        """)
+        out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120,
+                             env=dict(os.environ, PYTHONPATH=os.getcwd()))
+        assert out.returncode == 0, out.stderr
+        assert out.stdout.strip().splitlines()[-1] == "14"
+        assert ray.get(h.incr.remote()) == 15
+        ray.kill(h)
+        with pytest.raises(ValueError):
+            ray.get_actor("tracker")
+    finally:
+        ray.shutdown()
+
+
+def test_actor_death_fails_pending_calls():
+    ray.init(num_gpus=0, namespace="d" + uuid.uuid4().hex[:8])
+    try:
+        class Slow:
+            def sleep(self, s):
+                time.sleep(s)
+                return s
+
+            def pid(self):
+                return os.getpid()
+
+        h = ray.remote(Slow).remote()
+        pid = ray.get(h.pid.remote())
+        ref = h.sleep.remote(30)
+        time.sleep(0.2)
+        os.kill(pid, 9)
+        with pytest.raises(ray.RayActorError):
+            ray.get(ref, timeout=30)
+        with pytest.raises(ray.RayActorError):
+            ray.get(h.pid.remote(), timeout=30)
+    finally:
+        ray.shutdown()
