@@ -12,7 +12,8 @@ as ray``:
 * ``init`` / ``is_initialized`` / ``shutdown`` / ``remote`` (functions and
   classes, ``.options(...)``) / ``get`` / ``put`` / ``wait`` / ``kill`` /
   ``get_actor`` / ``get_gpu_ids`` / ``cluster_resources`` /
-  ``available_resources``; ``state.actors()``; ``util.queue.Queue``.
+  ``available_resources``; ``state.actors()``; ``util.queue.Queue``; ``data``
+  (offline batch inference: ``map_batches`` on GPU actor pools).
 * An actor is ONE process (spawned, not forked: a GPU runtime must never be
   forked) pinned to the GPUs the node's slot allocator gave it
   (``runtime/resources.py``: whole GPUs first-fit, fractional best-fit, the
@@ -49,7 +50,7 @@ from typing import Any, Dict, List, Optional, Sequence, Tuple
 
 __all__ = ["init", "is_initialized", "shutdown", "remote", "get", "put", "wait", "kill", "get_actor",
            "get_gpu_ids", "cluster_resources", "available_resources", "ObjectRef", "ActorHandle",
-           "RayError", "RayTaskError", "RayActorError", "GetTimeoutError", "state", "util"]
+           "RayError", "RayTaskError", "RayActorError", "GetTimeoutError", "state", "util", "data"]
 
 
 class RayError(Exception):
@@ -672,4 +673,4 @@ def remote(*args, **options):
     return wrap
 
 
-from . import state, util  # noqa: E402  (submodules use the names above)
+from . import data, state, util  # noqa: E402  (submodules use the names above)

@@ -151,6 +151,13 @@ class EngineRunner:
                     s.graphs[bi][slot] = g
                     s.outputs[bi][slot] = y
                     self.engine.set_graph(s.sid, bi, slot, g.raw_cuda_graph_exec(), y.data_ptr())
+            # first launch of a graph exec uploads it (kernel-arg buffers, AQL
+            # packet templates); do that here for every (bucket, slot) so no
+            # served batch pays it
+            for row in s.graphs:
+                for g in row:
+                    g.replay()
+            torch.cuda.synchronize()
             # latency estimates per bucket (used for stale-request dropping)
             for bi, b in enumerate(buckets):
                 g = s.graphs[bi][0]
