@@ -50,7 +50,7 @@ from typing import Any, Dict, List, Optional, Sequence, Tuple
 
 __all__ = ["init", "is_initialized", "shutdown", "remote", "get", "put", "wait", "kill", "get_actor",
            "get_gpu_ids", "cluster_resources", "available_resources", "ObjectRef", "ActorHandle",
-           "RayError", "RayTaskError", "RayActorError", "GetTimeoutError", "state", "util", "data"]
+           "RayError", "RayTaskError", "RayActorError", "GetTimeoutError", "state", "util", "data", "dag"]
 
 
 class RayError(Exception):
@@ -673,4 +673,4 @@ def remote(*args, **options):
     return wrap
 
 
-from . import data, state, util  # noqa: E402  (submodules use the names above)
+from . import dag, data, state, util  # noqa: E402  (submodules use the names above)
