@@ -94,7 +94,10 @@ def main():
         dist.init_process_group("gloo")
     elif world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        # RCCL default group, created lazily: DP replicas issue no device
+        # collectives (requests are routed, not reduced), so no communicator is
+        # built and no RCCL proxy thread competes with the replica engine
+        dist.init_process_group("nccl")
     else:
         torch.cuda.set_device(0)
 
