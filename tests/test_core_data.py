@@ -97,3 +97,47 @@ def test_actor_pool_map_batches_on_gpus(rt):
     # UDF errors surface in the consumer
     with pytest.raises(ray.RayTaskError):
         rd.range(8).map_batches(Boom, batch_size=4, compute=rd.ActorPoolStrategy(size=1)).take_all()
+
+
+class BertPredictor:
+    """A GPU pool actor: random-init BERT (seeded) on the HIP kernels, loaded once."""
+
+    def __init__(self, layers):
+        import torch
+
+        from ray_dynamic_batching_amd.models.bert import BertConfig, BertForSequenceClassification
+
+        self.torch = torch
+        self.m = BertForSequenceClassification(BertConfig(layers=layers), device="cuda:0", backend="hip", seed=7)
+
+    def __call__(self, batch):
+        torch = self.torch
+        ids = torch.as_tensor(np.stack(batch["ids"]), dtype=torch.int32, device="cuda:0")
+        with torch.no_grad():
+            logits = self.m(ids).float().cpu().numpy()
+        return {"row": batch["row"], "logits": logits}
+
+
+@pytest.mark.gpu
+def test_map_batches_bert_on_gpu_actor_pool():
+    """Offline batch inference of BERT (HIP kernels) through a GPU-pinned pool
+    actor process == the same seeded model run in this process."""
+    import torch
+
+    from ray_dynamic_batching_amd.models.bert import BertConfig, BertForSequenceClassification
+
+    m = BertForSequenceClassification(BertConfig(layers=2), device="cuda:0", backend="hip", seed=7)
+    ids = m.example_input(40, seed=3).cpu().numpy()
+    ray.init(num_gpus=1, namespace="dg" + uuid.uuid4().hex[:8])
+    try:
+        ds = rd.from_items([{"row": i, "ids": ids[i]} for i in range(40)])
+        out = ds.map_batches(BertPredictor, batch_size=16, num_gpus=1, fn_constructor_args=(2,),
+                             compute=rd.ActorPoolStrategy(size=1)).take_all()
+    finally:
+        ray.shutdown()
+    assert [r["row"] for r in out] == list(range(40))
+    got = np.stack([r["logits"] for r in out])
+    with torch.no_grad():
+        ref = torch.cat([m(torch.as_tensor(ids[i:i + 16], device="cuda:0")).float().cpu()
+                         for i in range(0, 40, 16)]).numpy()
+    assert np.abs(got - ref).max() < 2e-2
