@@ -19,16 +19,25 @@ class Factory:
         return self.fn(device=device, **self.kw)
 
 
-def _bert(device, layers=12, seq_len=128, backend="hip"):
+def _bert(device, layers=12, seq_len=128, backend="hip", checkpoint=None):
     from .bert import BertConfig, BertForSequenceClassification
 
+    if checkpoint:
+        from .weights import bert_from_hf
+
+        return bert_from_hf(checkpoint, seq_len=seq_len, device=device, backend=backend)
     return BertForSequenceClassification(BertConfig(layers=layers, seq_len=seq_len), device=device, backend=backend)
 
 
-def _resnet(device, backend="hip"):
+def _resnet(device, backend="hip", checkpoint=None):
     from .resnet import ResNet50
 
-    return ResNet50(device=device, backend=backend)
+    m = ResNet50(device=device, backend=backend)
+    if checkpoint:
+        from .weights import load_resnet50
+
+        load_resnet50(m, checkpoint)
+    return m
 
 
 def _vit(device, backend="hip"):
@@ -43,13 +52,22 @@ def _mlp(device, **kw):
     return MLP(device=device, **kw)
 
 
-def bert_base(layers: int = 12, seq_len: int = 128, backend: str = "hip") -> Factory:
-    return Factory(_bert, ((seq_len,), torch.int32, (2,), torch.float32), layers=layers, seq_len=seq_len,
-                   backend=backend)
+def bert_base(layers: int = 12, seq_len: int = 128, backend: str = "hip", checkpoint: str = None) -> Factory:
+    """``checkpoint``: a Hugging Face BERT sequence-classification directory or
+    file (models/weights.py); its config sets the shape and the label count."""
+    labels = 2
+    if checkpoint:
+        from .weights import _bert_config, read_config
+
+        labels = _bert_config(read_config(checkpoint), seq_len).num_labels
+    return Factory(_bert, ((seq_len,), torch.int32, (labels,), torch.float32), layers=layers, seq_len=seq_len,
+                   backend=backend, checkpoint=checkpoint)
 
 
-def resnet50(backend: str = "hip") -> Factory:
-    return Factory(_resnet, ((224, 224, 3), torch.uint8, (10,), torch.float32), backend=backend)
+def resnet50(backend: str = "hip", checkpoint: str = None) -> Factory:
+    """``checkpoint``: torchvision resnet50 weights (safetensors / .pth, BN folded at load)."""
+    return Factory(_resnet, ((224, 224, 3), torch.uint8, (10,), torch.float32), backend=backend,
+                   checkpoint=checkpoint)
 
 
 def vit_b16(backend: str = "hip") -> Factory:

@@ -71,6 +71,55 @@ class ResNet50:
         self.fc_w = (torch.randn(num_classes, 2048, generator=g) * 0.01).to(self.device, dtype).contiguous()
         self.fc_b = torch.zeros(num_classes, device=self.device, dtype=dtype)
 
+    @torch.no_grad()
+    def load_torchvision_state_dict(self, sd, strict: bool = True, eps: float = 1e-5) -> "ResNet50":
+        """Load torchvision ``resnet50`` weights (the reference's registry model,
+        ``scheduler.py:43``): BatchNorm eval statistics are folded into each
+        conv -- W' = W * g / sqrt(var + eps), b' = beta - mean * g / sqrt(var + eps)
+        -- and the weights are laid out NHWC ([Cout, kh, kw, Cin]) for the
+        implicit-GEMM kernels (stem Cin padded 3 -> 8)."""
+        used = set()
+
+        def t(name):
+            used.add(name)
+            return sd[name].float()
+
+        def fold(conv, bn):
+            w = t(conv + ".weight")
+            scale = t(bn + ".weight") / torch.sqrt(t(bn + ".running_var") + eps)
+            b = t(bn + ".bias") - t(bn + ".running_mean") * scale
+            used.add(bn + ".num_batches_tracked")
+            return (w * scale[:, None, None, None]).permute(0, 2, 3, 1), b
+
+        def put(dst, src):
+            if tuple(dst.shape) != tuple(src.shape):
+                raise ValueError(f"shape {tuple(src.shape)} does not fit {tuple(dst.shape)}")
+            dst.copy_(src.to(dst.device, dst.dtype))
+
+        w, b = fold("conv1", "bn1")
+        self.stem_w.zero_()
+        put(self.stem_w[..., :3], w)
+        put(self.stem_b, b)
+        bi = 0
+        for si, (_, n, _) in enumerate(STAGES):
+            for i in range(n):
+                blk, p = self.blocks[bi], f"layer{si + 1}.{i}."
+                for j in (1, 2, 3):
+                    w, b = fold(p + f"conv{j}", p + f"bn{j}")
+                    put(blk[f"w{j}"], w)
+                    put(blk[f"b{j}"], b)
+                if "wd" in blk:
+                    w, b = fold(p + "downsample.0", p + "downsample.1")
+                    put(blk["wd"], w)
+                    put(blk["bd"], b)
+                bi += 1
+        put(self.fc_w, t("fc.weight"))
+        put(self.fc_b, t("fc.bias"))
+        left = sorted(k for k in sd if k not in used)
+        if strict and left:
+            raise ValueError(f"unused checkpoint keys: {left[:8]}")
+        return self
+
     # -- serving contract
     @property
     def input_shape(self):

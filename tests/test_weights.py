@@ -1,0 +1,280 @@
+"""Checkpoint loading (models/weights.py): Hugging Face BERT and Llama
+checkpoints (built from a config with random init by ``transformers`` -- no
+download) and torchvision-format ResNet-50 weights (a torchvision-compatible
+nn reference defined here, since torchvision is not installed) load into this
+framework's models, whose outputs then match the independent implementations.
+CPU tests run the eager backends in fp32; the GPU tests run the HIP kernels."""
+import math
+
+import pytest
+import torch
+import torch.nn as nn
+
+from ray_dynamic_batching_amd.models import weights as W
+
+transformers = pytest.importorskip("transformers")
+
+
+# ---------------------------------------------------------------------------
+# fixtures: reference models
+# ---------------------------------------------------------------------------
+def _hf_bert(tmp_path, num_labels=3, hidden=128):
+    cfg = transformers.BertConfig(vocab_size=1000, hidden_size=hidden, num_hidden_layers=2,
+                                  num_attention_heads=hidden // 64 if hidden >= 256 else 4,
+                                  intermediate_size=2 * hidden, max_position_embeddings=64, num_labels=num_labels)
+    torch.manual_seed(0)
+    m = transformers.BertForSequenceClassification(cfg).eval()
+    with torch.no_grad():                      # non-trivial LayerNorm affine params
+        for n, p in m.named_parameters():
+            if "LayerNorm" in n:
+                p.add_(torch.randn_like(p) * 0.1)
+    m.save_pretrained(tmp_path / "bert")
+    return m
+
+
+def _bert_ids(n=5, S=32, vocab=1000):
+    g = torch.Generator().manual_seed(1)
+    ids = torch.randint(1, vocab, (n, S), generator=g)
+    ids[:, 0] = 101
+    ids[1, 20:] = 0                            # padded sequences
+    ids[3, 5:] = 0
+    return ids
+
+
+def _hf_llama(tmp_path, tied=False, scaling=True):
+    cfg = transformers.LlamaConfig(
+        vocab_size=512, hidden_size=256, num_hidden_layers=2, num_attention_heads=4, num_key_value_heads=2,
+        head_dim=64, intermediate_size=512, max_position_embeddings=128, rope_theta=10000.0, rms_norm_eps=1e-5,
+        tie_word_embeddings=tied,
+        rope_scaling=({"rope_type": "llama3", "factor": 8.0, "low_freq_factor": 1.0, "high_freq_factor": 4.0,
+                       "original_max_position_embeddings": 32} if scaling else None))
+    torch.manual_seed(2)
+    m = transformers.LlamaForCausalLM(cfg).eval()
+    with torch.no_grad():
+        for n, p in m.named_parameters():
+            if "norm" in n:
+                p.add_(torch.randn_like(p) * 0.1)
+    m.save_pretrained(tmp_path / "llama")
+    return m
+
+
+class _Bottleneck(nn.Module):
+    def __init__(self, cin, width, stride, down):
+        super().__init__()
+        self.conv1, self.bn1 = nn.Conv2d(cin, width, 1, bias=False), nn.BatchNorm2d(width)
+        self.conv2, self.bn2 = nn.Conv2d(width, width, 3, stride, 1, bias=False), nn.BatchNorm2d(width)
+        self.conv3, self.bn3 = nn.Conv2d(width, width * 4, 1, bias=False), nn.BatchNorm2d(width * 4)
+        self.downsample = nn.Sequential(nn.Conv2d(cin, width * 4, 1, stride, bias=False),
+                                        nn.BatchNorm2d(width * 4)) if down else None
+
+    def forward(self, x):
+        h = torch.relu(self.bn1(self.conv1(x)))
+        h = torch.relu(self.bn2(self.conv2(h)))
+        h = self.bn3(self.conv3(h))
+        return torch.relu(h + (self.downsample(x) if self.downsample is not None else x))
+
+
+class _TVResNet50(nn.Module):
+    """torchvision.models.resnet50's module names and structure (v1.5: stride on the 3x3)."""
+
+    def __init__(self, num_classes=1000):
+        super().__init__()
+        self.conv1, self.bn1 = nn.Conv2d(3, 64, 7, 2, 3, bias=False), nn.BatchNorm2d(64)
+        cin = 64
+        for si, (width, n, stride) in enumerate([(64, 3, 1), (128, 4, 2), (256, 6, 2), (512, 3, 2)]):
+            blocks = []
+            for i in range(n):
+                s = stride if i == 0 else 1
+                blocks.append(_Bottleneck(cin, width, s, s != 1 or cin != width * 4))
+                cin = width * 4
+            setattr(self, f"layer{si + 1}", nn.Sequential(*blocks))
+        self.fc = nn.Linear(2048, num_classes)
+
+    def forward(self, x):
+        x = nn.functional.max_pool2d(torch.relu(self.bn1(self.conv1(x))), 3, 2, 1)
+        for i in range(1, 5):
+            x = getattr(self, f"layer{i}")(x)
+        return self.fc(x.mean(dim=(2, 3)))
+
+
+def _tv_resnet():
+    torch.manual_seed(3)
+    m = _TVResNet50()
+    with torch.no_grad():
+        for mod in m.modules():
+            if isinstance(mod, nn.BatchNorm2d):
+                mod.running_mean.normal_(0, 0.05)
+                mod.running_var.uniform_(0.8, 1.2)
+                mod.weight.uniform_(0.3, 0.7)
+                mod.bias.normal_(0, 0.05)
+    return m.eval()
+
+
+def _normalize(img):
+    mean = torch.tensor([0.485, 0.456, 0.406])
+    std = torch.tensor([0.229, 0.224, 0.225])
+    return ((img.float() / 255.0 - mean) / std).permute(0, 3, 1, 2)
+
+
+# ---------------------------------------------------------------------------
+# CPU: eager backends, fp32
+# ---------------------------------------------------------------------------
+def test_bert_hf_checkpoint_matches_transformers(tmp_path):
+    ref = _hf_bert(tmp_path)
+    ids = _bert_ids()
+    with torch.no_grad():
+        want = ref(input_ids=ids, attention_mask=(ids != 0).long()).logits
+    m = W.bert_from_hf(tmp_path / "bert", seq_len=32, device="cpu", dtype=torch.float32, backend="torch")
+    assert m.cfg.num_labels == 3 and m.cfg.hidden == 128
+    got = m(ids.to(torch.int32))
+    assert torch.allclose(got, want, atol=1e-4, rtol=1e-4), (got - want).abs().max()
+    # a state dict in memory, old gamma/beta LayerNorm names, strictness
+    sd = {k.replace("LayerNorm.weight", "LayerNorm.gamma").replace("LayerNorm.bias", "LayerNorm.beta"): v
+          for k, v in ref.state_dict().items()}
+    m2 = W.load_bert_hf(type(m)(m.cfg, device="cpu", dtype=torch.float32, backend="torch"), sd)
+    assert torch.allclose(m2(ids.to(torch.int32)), want, atol=1e-4, rtol=1e-4)
+    with pytest.raises(ValueError, match="unused"):
+        W.load_bert_hf(m2, dict(sd, extra_head=torch.zeros(1)))
+    with pytest.raises(ValueError, match="shape"):
+        W.bert_from_hf(tmp_path / "bert", config=dict(ref.config.to_dict(), hidden_size=64, intermediate_size=128),
+                       seq_len=32, device="cpu", dtype=torch.float32, backend="torch")
+
+
+@pytest.mark.parametrize("tied,scaling", [(False, True), (True, False)])
+def test_llama_hf_checkpoint_matches_transformers(tmp_path, tied, scaling):
+    ref = _hf_llama(tmp_path, tied=tied, scaling=scaling)
+    g = torch.Generator().manual_seed(4)
+    ids = torch.randint(1, 512, (3, 48), generator=g)
+    with torch.no_grad():
+        logits = ref(input_ids=ids).logits[:, -1].float()
+    m = W.llama_from_hf(tmp_path / "llama", seq_len=48, device="cpu", dtype=torch.float32, backend="torch")
+    out = m(ids.to(torch.int32))
+    assert torch.equal(out[:, 0].long(), logits.argmax(-1))
+    assert torch.allclose(out[:, 1].contiguous().view(torch.float32), logits.max(-1).values, atol=1e-4, rtol=1e-4)
+
+
+def test_llama_hf_tp_shards_tile_the_full_model(tmp_path):
+    _hf_llama(tmp_path)
+    full = W.llama_from_hf(tmp_path / "llama", seq_len=16, device="cpu", dtype=torch.float32, backend="torch")
+    ranks = [W.llama_from_hf(tmp_path / "llama", seq_len=16, tp_rank=r, tp_size=2, device="cpu",
+                             dtype=torch.float32, backend="torch") for r in range(2)]
+    Dh, Hl, Hkvl = 64, 2, 1
+    for i, L in enumerate(full.layers):
+        q = torch.cat([r.layers[i]["w_qkv"][:Hl * Dh] for r in ranks])
+        k = torch.cat([r.layers[i]["w_qkv"][Hl * Dh:(Hl + Hkvl) * Dh] for r in ranks])
+        assert torch.equal(q, L["w_qkv"][:2 * Hl * Dh]) and torch.equal(k, L["w_qkv"][4 * Dh:6 * Dh])
+        assert torch.equal(torch.cat([r.layers[i]["w_o"] for r in ranks], 1), L["w_o"])
+        assert torch.equal(torch.cat([r.layers[i]["w_down"] for r in ranks], 1), L["w_down"])
+    assert torch.equal(torch.cat([r.lm_head for r in ranks]), full.lm_head)
+
+
+def test_llama3_rope_scaling_matches_transformers():
+    from ray_dynamic_batching_amd.models.llama import LlamaConfig
+
+    rs = {"rope_type": "llama3", "factor": 8.0, "low_freq_factor": 1.0, "high_freq_factor": 4.0,
+          "original_max_position_embeddings": 32}
+    hf_cfg = transformers.LlamaConfig(hidden_size=256, num_attention_heads=4, head_dim=64, rope_theta=10000.0,
+                                      max_position_embeddings=128, rope_scaling=rs)
+    from transformers.modeling_rope_utils import ROPE_INIT_FUNCTIONS
+
+    inv, _ = ROPE_INIT_FUNCTIONS["llama3"](hf_cfg, "cpu")
+    cos, _ = W.llama_rope_tables(LlamaConfig(head_dim=64, rope_theta=10000.0, max_position=128), rs)
+    want = torch.outer(torch.arange(128, dtype=torch.float64), inv.double()).cos().float()
+    assert torch.allclose(cos, want, atol=1e-5)
+
+
+def test_resnet50_torchvision_weights_fold_bn():
+    from ray_dynamic_batching_amd.models.resnet import ResNet50
+
+    ref = _tv_resnet()
+    img = torch.randint(0, 256, (2, 64, 64, 3), dtype=torch.uint8)
+    with torch.no_grad():
+        want = ref(_normalize(img))
+    m = ResNet50(device="cpu", backend="torch", image_size=64)
+    W.load_resnet50(m, ref.state_dict())
+    got = m.logits(img)
+    assert torch.allclose(got, want, atol=2e-3 * want.abs().max().item(), rtol=1e-3), (got - want).abs().max()
+    with pytest.raises(KeyError):
+        W.load_resnet50(m, {k: v for k, v in ref.state_dict().items() if k != "fc.bias"})
+
+
+def test_checkpoint_files(tmp_path):
+    from safetensors.torch import save_file
+
+    sd = {"a": torch.arange(4.0), "b": torch.ones(2, 2)}
+    save_file(sd, str(tmp_path / "m.safetensors"))
+    torch.save(sd, tmp_path / "m.pt")
+    for p in ("m.safetensors", "m.pt"):
+        got = W.load_state_dict(tmp_path / p)
+        assert set(got) == {"a", "b"} and torch.equal(got["a"], sd["a"])
+    (tmp_path / "shards").mkdir()
+    save_file({"a": sd["a"]}, str(tmp_path / "shards" / "s1.safetensors"))
+    save_file({"b": sd["b"]}, str(tmp_path / "shards" / "s2.safetensors"))
+    import json
+
+    (tmp_path / "shards" / "model.safetensors.index.json").write_text(
+        json.dumps({"weight_map": {"a": "s1.safetensors", "b": "s2.safetensors"}}))
+    assert set(W.load_state_dict(tmp_path / "shards")) == {"a", "b"}
+    with pytest.raises(ValueError):
+        W.load_state_dict(tmp_path / "m.pkl")
+
+
+# ---------------------------------------------------------------------------
+# GPU: the HIP kernels on loaded weights
+# ---------------------------------------------------------------------------
+@pytest.mark.gpu
+def test_bert_hf_checkpoint_on_hip_kernels(tmp_path):
+    ref = _hf_bert(tmp_path, hidden=256)           # the kernels take hidden = 256 k, head dim 64
+    ids = _bert_ids()
+    with torch.no_grad():
+        want = ref(input_ids=ids, attention_mask=(ids != 0).long()).logits
+    m = W.bert_from_hf(tmp_path / "bert", seq_len=32, device="cuda", backend="hip")
+    got = m(ids.to(torch.int32).cuda()).cpu()
+    assert torch.allclose(got, want, atol=5e-2, rtol=5e-2), (got - want).abs().max()
+
+
+@pytest.mark.gpu
+def test_llama_hf_checkpoint_on_hip_kernels(tmp_path):
+    ref = _hf_llama(tmp_path)
+    g = torch.Generator().manual_seed(4)
+    ids = torch.randint(1, 512, (3, 64), generator=g)
+    with torch.no_grad():
+        logits = ref(input_ids=ids).logits[:, -1].float()
+    m = W.llama_from_hf(tmp_path / "llama", seq_len=64, device="cuda", backend="hip")
+    out = m(ids.to(torch.int32).cuda()).cpu()
+    top = logits.max(-1).values
+    assert torch.allclose(out[:, 1].contiguous().view(torch.float32), top, atol=5e-2, rtol=5e-2)
+    picked = logits[torch.arange(3), out[:, 0].long()]
+    assert torch.all(top - picked < 5e-2)          # the chosen token is a (near-)argmax in fp32
+
+
+@pytest.mark.gpu
+def test_resnet50_torchvision_weights_on_hip_kernels():
+    from ray_dynamic_batching_amd.models.resnet import ResNet50
+
+    ref = _tv_resnet()
+    img = torch.randint(0, 256, (4, 224, 224, 3), dtype=torch.uint8)
+    with torch.no_grad():
+        want = ref(_normalize(img))
+    m = ResNet50(device="cuda", backend="hip")
+    W.load_resnet50(m, ref.state_dict())
+    got = m.logits(img.cuda()).cpu()
+    scale = want.abs().max().item()
+    assert (got - want).abs().max().item() < 3e-2 * scale + 1e-2
+
+
+def test_factories_take_checkpoints(tmp_path):
+    from ray_dynamic_batching_amd.models import factories
+
+    ref = _hf_bert(tmp_path, num_labels=5)
+    f = factories.bert_base(seq_len=32, backend="torch", checkpoint=str(tmp_path / "bert"))
+    assert f.io_spec[2] == (5,)
+    m = f(device="cpu")
+    ids = _bert_ids()
+    with torch.no_grad():
+        want = ref(input_ids=ids, attention_mask=(ids != 0).long()).logits
+    assert torch.allclose(m(ids.to(torch.int32)).float(), want, atol=3e-2, rtol=3e-2)   # bf16 weights
+    tv = _tv_resnet()
+    torch.save(tv.state_dict(), tmp_path / "rn50.pth")
+    r = factories.resnet50(backend="torch", checkpoint=str(tmp_path / "rn50.pth"))(device="cpu")
+    assert torch.equal(r.fc_b.float(), tv.fc.bias.detach().to(r.fc_b.dtype).float())
