@@ -104,6 +104,9 @@ class ViT:
         p, i = (ops.softmax_topk if self.backend == "hip" else ops.softmax_topk_ref)(logits, self.topk)
         return torch.cat([p, i.float()], dim=1).contiguous()
 
+    def logits(self, img):
+        return self._logits_hip(img) if self.backend == "hip" else self._logits_torch(img)
+
     def _tokens(self, patches):  # patches [B, n, D]
         B = patches.shape[0]
         return (torch.cat([self.cls.expand(B, 1, -1), patches], dim=1) + self.pos).contiguous()

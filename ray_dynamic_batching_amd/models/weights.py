@@ -19,6 +19,11 @@ such models ship in and maps them onto this framework's kernel-layout models:
   interleaved for the SwiGLU epilogue --, its o/down columns and its vocab
   slice of the LM head); ``tie_word_embeddings`` and the ``llama3`` RoPE
   frequency scaling of Llama-3.x configs are honoured;
+* ViT: Hugging Face ``ViTForImageClassification`` keys or torchvision
+  ``vit_b_16`` keys -> ``models.vit.ViT``; a checkpoint trained on another
+  input normalisation (HF ViT: mean = std = 0.5) is re-expressed in this
+  model's ImageNet-normalised input space by folding the difference into the
+  patch-embedding weights and bias (exact: the patch conv has no padding);
 * ResNet-50: torchvision ``resnet50`` keys -> ``models.resnet.ResNet50`` with
   every BatchNorm folded into its convolution at load (see ``load_resnet50``).
 
@@ -40,7 +45,7 @@ StateDict = Dict[str, torch.Tensor]
 Source = Union[str, os.PathLike, Mapping[str, torch.Tensor]]
 
 __all__ = ["load_state_dict", "read_config", "load_bert_hf", "bert_from_hf", "load_llama_hf", "llama_from_hf",
-           "llama_rope_tables", "load_resnet50"]
+           "llama_rope_tables", "load_resnet50", "load_vit", "vit_from_hf"]
 
 
 # ---------------------------------------------------------------------------
@@ -308,3 +313,99 @@ def load_resnet50(model, src: Source, strict: bool = True):
     """torchvision ``resnet50`` state dict -> ``ResNet50``: each conv's
     BatchNorm (eval statistics) is folded into the conv weight and a bias."""
     return model.load_torchvision_state_dict(load_state_dict(src), strict=strict)
+
+
+# ---------------------------------------------------------------------------
+# ViT (Hugging Face or torchvision keys)
+# ---------------------------------------------------------------------------
+_IMAGENET_MEAN = (0.485, 0.456, 0.406)
+_IMAGENET_STD = (0.229, 0.224, 0.225)
+
+
+def _vit_config(hf: dict):
+    from .vit import ViTConfig
+
+    n = hf.get("num_labels") or len(hf.get("id2label", {})) or 1000
+    return ViTConfig(image=hf.get("image_size", 224), patch=hf.get("patch_size", 16), hidden=hf.get("hidden_size", 768),
+                     layers=hf.get("num_hidden_layers", 12), heads=hf.get("num_attention_heads", 12),
+                     mlp=hf.get("intermediate_size", 3072), classes=n, eps=hf.get("layer_norm_eps", 1e-12))
+
+
+def load_vit(model, src: Source, image_mean=None, image_std=None, strict: bool = True):
+    """HF ``ViTForImageClassification`` (default normalisation 0.5 / 0.5) or
+    torchvision ``vit_b_16`` (ImageNet normalisation) weights -> ``ViT``."""
+    sd = load_state_dict(src)
+    tv = "conv_proj.weight" in sd
+    if image_mean is None:
+        image_mean = _IMAGENET_MEAN if tv else (0.5, 0.5, 0.5)
+    if image_std is None:
+        image_std = _IMAGENET_STD if tv else (0.5, 0.5, 0.5)
+    k = _Keys(_strip(sd, ("vit.",)))
+    c = model.cfg
+    if tv:
+        pw, pb = k.get("conv_proj.weight"), k.get("conv_proj.bias")
+        cls, pos = k.get("class_token"), k.get("encoder.pos_embedding")
+    else:
+        pw, pb = k.get("embeddings.patch_embeddings.projection.weight"), k.get("embeddings.patch_embeddings.projection.bias")
+        cls, pos = k.get("embeddings.cls_token"), k.get("embeddings.position_embeddings")
+    # the model sees x_ours = (u - m_in) / s_in; the checkpoint expects
+    # x_ck = (u - m_ck) / s_ck = x_ours * s_in / s_ck + (m_in - m_ck) / s_ck
+    m_in, s_in = torch.tensor(_IMAGENET_MEAN), torch.tensor(_IMAGENET_STD)
+    m_ck, s_ck = torch.tensor(image_mean, dtype=torch.float32), torch.tensor(image_std, dtype=torch.float32)
+    pw = pw.float()
+    w_eff = pw * (s_in / s_ck)[None, :, None, None]
+    b_eff = pb.float() + (pw * ((m_in - m_ck) / s_ck)[None, :, None, None]).sum(dim=(1, 2, 3))
+    with torch.no_grad():
+        model.patch_w.zero_()
+    _copy(model.patch_w[..., :3], w_eff.permute(0, 2, 3, 1), "patch_embed")
+    _copy(model.patch_b, b_eff, "patch_embed")
+    _copy(model.cls, cls, "cls_token")
+    _copy(model.pos, pos, "position_embeddings")
+    for i, L in enumerate(model.layers):
+        if tv:
+            p = f"encoder.layers.encoder_layer_{i}."
+            names = dict(ln1=p + "ln_1", qkv_w=[p + "self_attention.in_proj_weight"],
+                         qkv_b=[p + "self_attention.in_proj_bias"], o=p + "self_attention.out_proj", ln2=p + "ln_2",
+                         fc1=p + "mlp.0", fc2=p + "mlp.3")
+        elif f"layers.{i}.attention.q_proj.weight" in k.sd:      # transformers 5 in-memory names
+            p = f"layers.{i}."
+            names = dict(ln1=p + "layernorm_before",
+                         qkv_w=[p + f"attention.{n}_proj.weight" for n in "qkv"],
+                         qkv_b=[p + f"attention.{n}_proj.bias" for n in "qkv"],
+                         o=p + "attention.o_proj", ln2=p + "layernorm_after", fc1=p + "mlp.fc1", fc2=p + "mlp.fc2")
+        else:                                                     # checkpoint-file names
+            p = f"encoder.layer.{i}."
+            names = dict(ln1=p + "layernorm_before",
+                         qkv_w=[p + f"attention.attention.{n}.weight" for n in ("query", "key", "value")],
+                         qkv_b=[p + f"attention.attention.{n}.bias" for n in ("query", "key", "value")],
+                         o=p + "attention.output.dense", ln2=p + "layernorm_after", fc1=p + "intermediate.dense",
+                         fc2=p + "output.dense")
+        _copy(L["ln1_g"], k.get(names["ln1"] + ".weight"), p + "ln1")
+        _copy(L["ln1_b"], k.get(names["ln1"] + ".bias"), p + "ln1")
+        _copy(L["w_qkv"], torch.cat([k.get(n) for n in names["qkv_w"]]), p + "qkv")
+        _copy(L["b_qkv"], torch.cat([k.get(n) for n in names["qkv_b"]]), p + "qkv")
+        _copy(L["w_o"], k.get(names["o"] + ".weight"), p + "o")
+        _copy(L["b_o"], k.get(names["o"] + ".bias"), p + "o")
+        _copy(L["ln2_g"], k.get(names["ln2"] + ".weight"), p + "ln2")
+        _copy(L["ln2_b"], k.get(names["ln2"] + ".bias"), p + "ln2")
+        _copy(L["w1"], k.get(names["fc1"] + ".weight"), p + "fc1")
+        _copy(L["b1"], k.get(names["fc1"] + ".bias"), p + "fc1")
+        _copy(L["w2"], k.get(names["fc2"] + ".weight"), p + "fc2")
+        _copy(L["b2"], k.get(names["fc2"] + ".bias"), p + "fc2")
+    ln, head = ("encoder.ln", "heads.head") if tv else ("layernorm", "classifier")
+    _copy(model.ln_g, k.get(ln + ".weight"), "final_ln")
+    _copy(model.ln_b, k.get(ln + ".bias"), "final_ln")
+    _copy(model.head_w, k.get(head + ".weight"), "head")
+    _copy(model.head_b, k.get(head + ".bias"), "head")
+    left = k.unused(ignore=("pooler",))
+    if strict and left:
+        raise ValueError(f"unused checkpoint keys: {left[:8]}{' ...' if len(left) > 8 else ''}")
+    return model
+
+
+def vit_from_hf(src: Source, config: Optional[dict] = None, *, device="cuda", dtype=torch.float16,
+                backend: str = "hip", image_mean=None, image_std=None, strict: bool = True):
+    from .vit import ViT
+
+    m = ViT(_vit_config(read_config(src, config)), device=device, dtype=dtype, backend=backend)
+    return load_vit(m, src, image_mean=image_mean, image_std=image_std, strict=strict)

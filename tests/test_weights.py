@@ -278,3 +278,68 @@ def test_factories_take_checkpoints(tmp_path):
     torch.save(tv.state_dict(), tmp_path / "rn50.pth")
     r = factories.resnet50(backend="torch", checkpoint=str(tmp_path / "rn50.pth"))(device="cpu")
     assert torch.equal(r.fc_b.float(), tv.fc.bias.detach().to(r.fc_b.dtype).float())
+
+
+def _hf_vit(tmp_path, hidden=256):
+    cfg = transformers.ViTConfig(image_size=64, patch_size=16, hidden_size=hidden, num_hidden_layers=2,
+                                 num_attention_heads=hidden // 64, intermediate_size=2 * hidden, num_labels=10,
+                                 layer_norm_eps=1e-12)
+    torch.manual_seed(5)
+    m = transformers.ViTForImageClassification(cfg).eval()
+    with torch.no_grad():
+        for n, p in m.named_parameters():
+            if "layernorm" in n or "embeddings" in n:
+                p.add_(torch.randn_like(p) * 0.1)
+    m.save_pretrained(tmp_path / "vit")
+    return m
+
+
+def _hf_vit_input(img):
+    return ((img.float() / 255.0 - 0.5) / 0.5).permute(0, 3, 1, 2)    # HF ViT image processor
+
+
+def test_vit_hf_checkpoint_matches_transformers(tmp_path):
+    ref = _hf_vit(tmp_path)
+    img = torch.randint(0, 256, (3, 64, 64, 3), dtype=torch.uint8)
+    with torch.no_grad():
+        want = ref(pixel_values=_hf_vit_input(img)).logits
+    m = W.vit_from_hf(tmp_path / "vit", device="cpu", dtype=torch.float32, backend="torch")
+    got = m.logits(img)
+    assert torch.allclose(got, want, atol=1e-3, rtol=1e-3), (got - want).abs().max()
+    # in-memory (transformers 5 module names) state dict
+    m1 = W.load_vit(type(m)(m.cfg, device="cpu", dtype=torch.float32, backend="torch"), ref.state_dict())
+    assert torch.allclose(m1.logits(img), want, atol=1e-3, rtol=1e-3)
+    # the same weights under torchvision's vit_b_16 key names and ImageNet normalisation
+    sd = W.load_state_dict(tmp_path / "vit")                  # checkpoint-file names
+    tv = {"conv_proj.weight": sd["vit.embeddings.patch_embeddings.projection.weight"],
+          "conv_proj.bias": sd["vit.embeddings.patch_embeddings.projection.bias"],
+          "class_token": sd["vit.embeddings.cls_token"], "encoder.pos_embedding": sd["vit.embeddings.position_embeddings"],
+          "encoder.ln.weight": sd["vit.layernorm.weight"], "encoder.ln.bias": sd["vit.layernorm.bias"],
+          "heads.head.weight": sd["classifier.weight"], "heads.head.bias": sd["classifier.bias"]}
+    for i in range(2):
+        p, q = f"vit.encoder.layer.{i}.", f"encoder.layers.encoder_layer_{i}."
+        for a, b in (("layernorm_before", "ln_1"), ("layernorm_after", "ln_2"), ("attention.output.dense",
+                     "self_attention.out_proj"), ("intermediate.dense", "mlp.0"), ("output.dense", "mlp.3")):
+            for t in ("weight", "bias"):
+                tv[f"{q}{b}.{t}"] = sd[f"{p}{a}.{t}"]
+        for t in ("weight", "bias"):
+            tv[f"{q}self_attention.in_proj_{t}"] = torch.cat(
+                [sd[f"{p}attention.attention.{n}.{t}"] for n in ("query", "key", "value")])
+    m2 = W.load_vit(type(m)(m.cfg, device="cpu", dtype=torch.float32, backend="torch"), tv)
+    # torchvision checkpoints expect ImageNet normalisation = this model's input space
+    with torch.no_grad():
+        mean = torch.tensor([0.485, 0.456, 0.406])
+        std = torch.tensor([0.229, 0.224, 0.225])
+        want_tv = ref(pixel_values=((img.float() / 255.0 - mean) / std).permute(0, 3, 1, 2)).logits
+    assert torch.allclose(m2.logits(img), want_tv, atol=1e-3, rtol=1e-3)
+
+
+@pytest.mark.gpu
+def test_vit_hf_checkpoint_on_hip_kernels(tmp_path):
+    ref = _hf_vit(tmp_path)
+    img = torch.randint(0, 256, (3, 64, 64, 3), dtype=torch.uint8)
+    with torch.no_grad():
+        want = ref(pixel_values=_hf_vit_input(img)).logits
+    m = W.vit_from_hf(tmp_path / "vit", device="cuda", backend="hip")
+    got = m.logits(img.cuda()).cpu()
+    assert (got - want).abs().max().item() < 3e-2 * want.abs().max().item() + 1e-2
