@@ -71,6 +71,59 @@ class BNFolder:
         return self.dev(wp), self.dev(bp)
 
 
+class CheckpointFolder(BNFolder):
+    """``BNFolder`` whose convs / linears come from a checkpoint (torchvision
+    key names) instead of random init: each ``conv`` call takes the next
+    (conv key, BatchNorm key) pair of ``conv_names`` -- the model constructor's
+    call order -- folds the BatchNorm's eval statistics into (W, b) and lays W
+    out like ``BNFolder`` ([Cout, k, k, Cin], depthwise [C, k, k]); each
+    ``linear`` takes the next key of ``linear_names``.  Shapes are checked
+    against what the constructor asks for; ``finish()`` rejects unused keys."""
+
+    def __init__(self, sd, conv_names, linear_names, device, dtype, eps: float = 1e-5):
+        super().__init__(0, device, dtype)
+        self.sd, self.eps = sd, eps
+        self.conv_names, self.linear_names = list(conv_names), list(linear_names)
+        self.used = set()
+
+    def _t(self, name):
+        if name not in self.sd:
+            raise KeyError(f"checkpoint has no {name!r}")
+        self.used.add(name)
+        return self.sd[name].float()
+
+    def conv(self, cin: int, cout: int, k: int, gamma: float = 1.0, depthwise: bool = False, bn: bool = True):
+        if not self.conv_names:
+            raise ValueError("checkpoint folder: more convs requested than names given")
+        cname, bname = self.conv_names.pop(0)
+        w = self._t(cname + ".weight")
+        want = (cout, 1 if depthwise else cin, k, k)
+        if tuple(w.shape) != want:
+            raise ValueError(f"{cname}: checkpoint shape {tuple(w.shape)} != model shape {want}")
+        w = w[:, 0] if depthwise else w.permute(0, 2, 3, 1)
+        if bname:
+            scale = self._t(bname + ".weight") / torch.sqrt(self._t(bname + ".running_var") + self.eps)
+            b = self._t(bname + ".bias") - self._t(bname + ".running_mean") * scale
+            self.used.add(bname + ".num_batches_tracked")
+            w = w * scale.view(-1, *([1] * (w.dim() - 1)))
+        else:
+            b = self._t(cname + ".bias") if cname + ".bias" in self.sd else torch.zeros(cout)
+        return w.contiguous(), b
+
+    def linear(self, cin: int, cout: int, std: Optional[float] = None):
+        name = self.linear_names.pop(0)
+        w, b = self._t(name + ".weight"), self._t(name + ".bias")
+        if tuple(w.shape) != (cout, cin):
+            raise ValueError(f"{name}: checkpoint shape {tuple(w.shape)} != model shape {(cout, cin)}")
+        return w, b
+
+    def finish(self, strict: bool = True) -> None:
+        left = sorted(k for k in self.sd if k not in self.used)
+        if strict and (left or self.conv_names or self.linear_names):
+            raise ValueError(f"checkpoint / model mismatch: unused keys {left[:8]}, "
+                             f"unconsumed names {(self.conv_names + self.linear_names)[:4]}")
+
+
 class ImageClassifier:
     """Serving contract shared by the CNN / ViT servables."""
 

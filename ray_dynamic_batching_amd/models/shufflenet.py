@@ -20,7 +20,7 @@ import torch
 import torch.nn.functional as F
 
 from .. import ops
-from .cnn_common import BNFolder, ImageClassifier, conv_t, round8
+from .cnn_common import BNFolder, CheckpointFolder, ImageClassifier, conv_t, round8
 
 STAGE_OUT = [116, 232, 464]
 STAGE_REPEATS = [4, 8, 4]
@@ -29,16 +29,20 @@ STAGE_REPEATS = [4, 8, 4]
 class ShuffleNetV2(ImageClassifier):
     def __init__(self, device="cuda", dtype=torch.float16, backend: str = "hip", num_classes: int = 1000,
                  seed: int = 0, image_size: int = 224, topk: int = 5, width: List[int] = None,
-                 repeats: List[int] = None):
+                 repeats: List[int] = None, state_dict=None, strict: bool = True):
+        """``state_dict``: torchvision ``shufflenet_v2_x1_0`` weights (BN folded)."""
         self.device = torch.device(device)
         self.dtype = dtype
         self.backend = backend
         self.image_size = image_size
         self.topk = topk
         self.num_classes = num_classes
-        bf = BNFolder(seed, self.device, dtype)
         self.stage_out = list(width or STAGE_OUT)
         self.repeats = list(repeats or STAGE_REPEATS)
+        if state_dict is not None:
+            bf = CheckpointFolder(state_dict, *self.torchvision_names(self.repeats), self.device, dtype)
+        else:
+            bf = BNFolder(seed, self.device, dtype)
         w, b = bf.conv(3, 24, 3)
         self.stem = (bf.dev(w), bf.dev(b))                      # logical
         self.stem_p = bf.pad_conv(w, b, 24, 8)                  # physical (C 3 -> 8)
@@ -80,6 +84,24 @@ class ShuffleNetV2(ImageClassifier):
                     u[k] = (bf.dev(u[k][0]), bf.dev(u[k][1]))
         self.conv5_p = bf.pad_conv(*self.conv5, 1024, round8(cin))
         self.conv5 = (bf.dev(self.conv5[0]), bf.dev(self.conv5[1]))
+        if state_dict is not None:
+            bf.finish(strict)
+
+    @staticmethod
+    def torchvision_names(repeats):
+        """(conv, BN) key pairs in constructor call order + linear keys."""
+        convs = [("conv1.0", "conv1.1")]
+        for s, rep in enumerate(repeats):
+            for i in range(rep):
+                p = f"stage{s + 2}.{i}."
+                if i == 0:
+                    convs += [(p + "branch1.0", p + "branch1.1"), (p + "branch1.2", p + "branch1.3"),
+                              (p + "branch2.0", p + "branch2.1")]
+                else:
+                    convs.append((p + "branch2.0", p + "branch2.1"))
+                convs += [(p + "branch2.3", p + "branch2.4"), (p + "branch2.5", p + "branch2.6")]
+        convs.append(("conv5.0", "conv5.1"))
+        return convs, ["fc"]
 
     # -- HIP path: padded NHWC f16 -----------------------------------------
     def _logits_hip(self, img):

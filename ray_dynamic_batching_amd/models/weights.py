@@ -24,6 +24,8 @@ such models ship in and maps them onto this framework's kernel-layout models:
   input normalisation (HF ViT: mean = std = 0.5) is re-expressed in this
   model's ImageNet-normalised input space by folding the difference into the
   patch-embedding weights and bias (exact: the patch conv has no padding);
+* ShuffleNetV2 x1.0: torchvision ``shufflenet_v2_x1_0`` keys, BN folded and
+  channel-padded by ``cnn_common.CheckpointFolder`` in the constructor;
 * ResNet-50: torchvision ``resnet50`` keys -> ``models.resnet.ResNet50`` with
   every BatchNorm folded into its convolution at load (see ``load_resnet50``).
 
@@ -45,7 +47,7 @@ StateDict = Dict[str, torch.Tensor]
 Source = Union[str, os.PathLike, Mapping[str, torch.Tensor]]
 
 __all__ = ["load_state_dict", "read_config", "load_bert_hf", "bert_from_hf", "load_llama_hf", "llama_from_hf",
-           "llama_rope_tables", "load_resnet50", "load_vit", "vit_from_hf"]
+           "llama_rope_tables", "load_resnet50", "load_vit", "vit_from_hf", "shufflenet_v2_from_torchvision"]
 
 
 # ---------------------------------------------------------------------------
@@ -409,3 +411,13 @@ def vit_from_hf(src: Source, config: Optional[dict] = None, *, device="cuda", dt
 
     m = ViT(_vit_config(read_config(src, config)), device=device, dtype=dtype, backend=backend)
     return load_vit(m, src, image_mean=image_mean, image_std=image_std, strict=strict)
+
+
+def shufflenet_v2_from_torchvision(src: Source, *, device="cuda", dtype=torch.float16, backend: str = "hip",
+                                   strict: bool = True, **kw):
+    from .shufflenet import ShuffleNetV2
+
+    sd = load_state_dict(src)
+    classes = sd["fc.weight"].shape[0] if "fc.weight" in sd else 1000
+    return ShuffleNetV2(device=device, dtype=dtype, backend=backend, num_classes=classes, state_dict=sd,
+                        strict=strict, **kw)

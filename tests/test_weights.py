@@ -343,3 +343,85 @@ def test_vit_hf_checkpoint_on_hip_kernels(tmp_path):
     m = W.vit_from_hf(tmp_path / "vit", device="cuda", backend="hip")
     got = m.logits(img.cuda()).cpu()
     assert (got - want).abs().max().item() < 3e-2 * want.abs().max().item() + 1e-2
+
+
+class _TVInvertedResidual(nn.Module):
+    """torchvision.models.shufflenetv2.InvertedResidual (module names and math)."""
+
+    def __init__(self, inp, oup, stride):
+        super().__init__()
+        self.stride = stride
+        bf = oup // 2
+        if stride > 1:
+            self.branch1 = nn.Sequential(nn.Conv2d(inp, inp, 3, stride, 1, groups=inp, bias=False), nn.BatchNorm2d(inp),
+                                         nn.Conv2d(inp, bf, 1, bias=False), nn.BatchNorm2d(bf), nn.ReLU())
+        else:
+            self.branch1 = nn.Sequential()
+        self.branch2 = nn.Sequential(
+            nn.Conv2d(inp if stride > 1 else bf, bf, 1, bias=False), nn.BatchNorm2d(bf), nn.ReLU(),
+            nn.Conv2d(bf, bf, 3, stride, 1, groups=bf, bias=False), nn.BatchNorm2d(bf),
+            nn.Conv2d(bf, bf, 1, bias=False), nn.BatchNorm2d(bf), nn.ReLU())
+
+    def forward(self, x):
+        if self.stride == 1:
+            x1, x2 = x.chunk(2, dim=1)
+            out = torch.cat((x1, self.branch2(x2)), dim=1)
+        else:
+            out = torch.cat((self.branch1(x), self.branch2(x)), dim=1)
+        b, c, h, w = out.shape
+        return out.view(b, 2, c // 2, h, w).transpose(1, 2).reshape(b, c, h, w)
+
+
+class _TVShuffleNetV2(nn.Module):
+    def __init__(self, num_classes=1000):
+        super().__init__()
+        self.conv1 = nn.Sequential(nn.Conv2d(3, 24, 3, 2, 1, bias=False), nn.BatchNorm2d(24), nn.ReLU())
+        cin = 24
+        for s, (rep, cout) in enumerate(zip([4, 8, 4], [116, 232, 464])):
+            units = [_TVInvertedResidual(cin, cout, 2)] + [_TVInvertedResidual(cout, cout, 1) for _ in range(rep - 1)]
+            setattr(self, f"stage{s + 2}", nn.Sequential(*units))
+            cin = cout
+        self.conv5 = nn.Sequential(nn.Conv2d(cin, 1024, 1, bias=False), nn.BatchNorm2d(1024), nn.ReLU())
+        self.fc = nn.Linear(1024, num_classes)
+
+    def forward(self, x):
+        x = nn.functional.max_pool2d(self.conv1(x), 3, 2, 1)
+        x = self.conv5(self.stage4(self.stage3(self.stage2(x))))
+        return self.fc(x.mean([2, 3]))
+
+
+def _tv_shufflenet():
+    torch.manual_seed(6)
+    m = _TVShuffleNetV2()
+    with torch.no_grad():
+        for mod in m.modules():
+            if isinstance(mod, nn.BatchNorm2d):
+                mod.running_mean.normal_(0, 0.05)
+                mod.running_var.uniform_(0.8, 1.2)
+                mod.weight.uniform_(0.5, 1.0)
+                mod.bias.normal_(0, 0.05)
+    return m.eval()
+
+
+def test_shufflenet_torchvision_weights():
+    ref = _tv_shufflenet()
+    img = torch.randint(0, 256, (2, 64, 64, 3), dtype=torch.uint8)
+    with torch.no_grad():
+        want = ref(_normalize(img))
+    m = W.shufflenet_v2_from_torchvision(ref.state_dict(), device="cpu", backend="torch", image_size=64)
+    got = m.logits(img)
+    assert torch.allclose(got, want, atol=2e-3 * want.abs().max().item(), rtol=1e-3), (got - want).abs().max()
+    bad = dict(ref.state_dict(), extra=torch.zeros(1))
+    with pytest.raises(ValueError):
+        W.shufflenet_v2_from_torchvision(bad, device="cpu", backend="torch")
+
+
+@pytest.mark.gpu
+def test_shufflenet_torchvision_weights_on_hip_kernels():
+    ref = _tv_shufflenet()
+    img = torch.randint(0, 256, (4, 224, 224, 3), dtype=torch.uint8)
+    with torch.no_grad():
+        want = ref(_normalize(img))
+    m = W.shufflenet_v2_from_torchvision(ref.state_dict(), device="cuda", backend="hip")
+    got = m.logits(img.cuda()).cpu()
+    assert (got - want).abs().max().item() < 3e-2 * want.abs().max().item() + 1e-2
