@@ -113,6 +113,8 @@ class CheckpointFolder(BNFolder):
     def linear(self, cin: int, cout: int, std: Optional[float] = None):
         name = self.linear_names.pop(0)
         w, b = self._t(name + ".weight"), self._t(name + ".bias")
+        if w.dim() == 4 and w.shape[2:] == (1, 1):          # 1x1 conv used as FC (SE blocks)
+            w = w[:, :, 0, 0]
         if tuple(w.shape) != (cout, cin):
             raise ValueError(f"{name}: checkpoint shape {tuple(w.shape)} != model shape {(cout, cin)}")
         return w, b

@@ -20,7 +20,7 @@ import torch
 import torch.nn.functional as F
 
 from .. import ops
-from .cnn_common import BNFolder, ImageClassifier, conv_t
+from .cnn_common import BNFolder, CheckpointFolder, ImageClassifier, conv_t
 
 # (block, expand, stride, cin, cout, layers)
 CONFIG = [("fused", 1, 1, 24, 24, 2), ("fused", 4, 2, 24, 48, 4), ("fused", 4, 2, 48, 64, 4),
@@ -29,13 +29,18 @@ CONFIG = [("fused", 1, 1, 24, 24, 2), ("fused", 4, 2, 24, 48, 4), ("fused", 4, 2
 
 class EfficientNetV2S(ImageClassifier):
     def __init__(self, device="cuda", dtype=torch.float16, backend: str = "hip", num_classes: int = 1000,
-                 seed: int = 0, image_size: int = 384, topk: int = 5, config=None):
+                 seed: int = 0, image_size: int = 384, topk: int = 5, config=None, state_dict=None,
+                 strict: bool = True):
+        """``state_dict``: torchvision ``efficientnet_v2_s`` weights (BN eps 1e-3 folded)."""
         self.device = torch.device(device)
         self.dtype = dtype
         self.backend = backend
         self.image_size = image_size
         self.topk = topk
-        bf = BNFolder(seed, self.device, dtype)
+        if state_dict is not None:
+            bf = CheckpointFolder(state_dict, *self.torchvision_names(config or CONFIG), self.device, dtype, eps=1e-3)
+        else:
+            bf = BNFolder(seed, self.device, dtype)
         w, b = bf.conv(3, 24, 3)
         self.stem = (bf.dev(w), bf.dev(b))
         self.stem_p = bf.pad_conv(w, b, 24, 8)
@@ -65,6 +70,25 @@ class EfficientNetV2S(ImageClassifier):
         self.head = tuple(map(bf.dev, bf.conv(256, 1280, 1)))
         fw, fb = bf.linear(1280, num_classes, std=0.01)
         self.fc_w, self.fc_b = bf.dev(fw), bf.dev(fb)
+        if state_dict is not None:
+            bf.finish(strict)
+
+    @staticmethod
+    def torchvision_names(config):
+        """(conv, BN) key pairs and linear keys in constructor call order."""
+        convs, lins = [("features.0.0", "features.0.1")], []
+        for si, (kind, e, _s, _ci, _co, n) in enumerate(config):
+            for i in range(n):
+                p = f"features.{si + 1}.{i}.block."
+                if kind == "fused":
+                    convs.append((p + "0.0", p + "0.1"))
+                    if e != 1:
+                        convs.append((p + "1.0", p + "1.1"))
+                else:
+                    convs += [(p + "0.0", p + "0.1"), (p + "1.0", p + "1.1"), (p + "3.0", p + "3.1")]
+                    lins += [p + "2.fc1", p + "2.fc2"]
+        convs.append((f"features.{len(config) + 1}.0", f"features.{len(config) + 1}.1"))
+        return convs, lins + ["classifier.1"]
 
     def _logits_hip(self, img):
         x = ops.image_to_nhwc(img, 8)

@@ -24,6 +24,8 @@ such models ship in and maps them onto this framework's kernel-layout models:
   input normalisation (HF ViT: mean = std = 0.5) is re-expressed in this
   model's ImageNet-normalised input space by folding the difference into the
   patch-embedding weights and bias (exact: the patch conv has no padding);
+* EfficientNetV2-S: torchvision ``efficientnet_v2_s`` keys (SE 1x1 convs as
+  FCs, BatchNorm eps 1e-3);
 * ShuffleNetV2 x1.0: torchvision ``shufflenet_v2_x1_0`` keys, BN folded and
   channel-padded by ``cnn_common.CheckpointFolder`` in the constructor;
 * ResNet-50: torchvision ``resnet50`` keys -> ``models.resnet.ResNet50`` with
@@ -47,7 +49,8 @@ StateDict = Dict[str, torch.Tensor]
 Source = Union[str, os.PathLike, Mapping[str, torch.Tensor]]
 
 __all__ = ["load_state_dict", "read_config", "load_bert_hf", "bert_from_hf", "load_llama_hf", "llama_from_hf",
-           "llama_rope_tables", "load_resnet50", "load_vit", "vit_from_hf", "shufflenet_v2_from_torchvision"]
+           "llama_rope_tables", "load_resnet50", "load_vit", "vit_from_hf", "shufflenet_v2_from_torchvision",
+           "efficientnet_v2s_from_torchvision"]
 
 
 # ---------------------------------------------------------------------------
@@ -421,3 +424,13 @@ def shufflenet_v2_from_torchvision(src: Source, *, device="cuda", dtype=torch.fl
     classes = sd["fc.weight"].shape[0] if "fc.weight" in sd else 1000
     return ShuffleNetV2(device=device, dtype=dtype, backend=backend, num_classes=classes, state_dict=sd,
                         strict=strict, **kw)
+
+
+def efficientnet_v2s_from_torchvision(src: Source, *, device="cuda", dtype=torch.float16, backend: str = "hip",
+                                      strict: bool = True, **kw):
+    from .efficientnet import EfficientNetV2S
+
+    sd = load_state_dict(src)
+    classes = sd["classifier.1.weight"].shape[0] if "classifier.1.weight" in sd else 1000
+    return EfficientNetV2S(device=device, dtype=dtype, backend=backend, num_classes=classes, state_dict=sd,
+                           strict=strict, **kw)

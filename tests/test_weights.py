@@ -425,3 +425,93 @@ def test_shufflenet_torchvision_weights_on_hip_kernels():
     m = W.shufflenet_v2_from_torchvision(ref.state_dict(), device="cuda", backend="hip")
     got = m.logits(img.cuda()).cpu()
     assert (got - want).abs().max().item() < 3e-2 * want.abs().max().item() + 1e-2
+
+
+def _cna(cin, cout, k, s=1, groups=1, act=True):
+    layers = [nn.Conv2d(cin, cout, k, s, (k - 1) // 2, groups=groups, bias=False), nn.BatchNorm2d(cout, eps=1e-3)]
+    return nn.Sequential(*(layers + ([nn.SiLU()] if act else [])))
+
+
+class _TVSE(nn.Module):
+    def __init__(self, hid, sq):
+        super().__init__()
+        self.fc1, self.fc2 = nn.Conv2d(hid, sq, 1), nn.Conv2d(sq, hid, 1)
+
+    def forward(self, x):
+        z = torch.sigmoid(self.fc2(nn.functional.silu(self.fc1(x.mean((2, 3), keepdim=True)))))
+        return x * z
+
+
+class _TVEffBlock(nn.Module):
+    """torchvision FusedMBConv / MBConv (module names; stochastic depth = identity in eval)."""
+
+    def __init__(self, kind, e, s, ci, co):
+        super().__init__()
+        hid = ci * e
+        self.res = s == 1 and ci == co
+        if kind == "fused":
+            blocks = [_cna(ci, co, 3, s)] if e == 1 else [_cna(ci, hid, 3, s), _cna(hid, co, 1, act=False)]
+        else:
+            blocks = [_cna(ci, hid, 1), _cna(hid, hid, 3, s, groups=hid), _TVSE(hid, max(1, ci // 4)),
+                      _cna(hid, co, 1, act=False)]
+        self.block = nn.Sequential(*blocks)
+
+    def forward(self, x):
+        y = self.block(x)
+        return y + x if self.res else y
+
+
+class _TVEfficientNetV2S(nn.Module):
+    def __init__(self, config, num_classes=1000):
+        super().__init__()
+        feats = [_cna(3, 24, 3, 2)]
+        for kind, e, s, ci, co, n in config:
+            feats.append(nn.Sequential(*[_TVEffBlock(kind, e, s if i == 0 else 1, ci if i == 0 else co, co)
+                                         for i in range(n)]))
+        feats.append(_cna(256, 1280, 1))
+        self.features = nn.Sequential(*feats)
+        self.classifier = nn.Sequential(nn.Dropout(0.2), nn.Linear(1280, num_classes))
+
+    def forward(self, x):
+        return self.classifier(self.features(x).mean((2, 3)))
+
+
+_EFF_SMALL = [("fused", 1, 1, 24, 24, 2), ("fused", 4, 2, 24, 48, 1), ("fused", 4, 2, 48, 64, 1),
+              ("mb", 4, 2, 64, 128, 2), ("mb", 6, 1, 128, 160, 1), ("mb", 6, 2, 160, 256, 2)]
+
+
+def _tv_effnet(config):
+    torch.manual_seed(7)
+    m = _TVEfficientNetV2S(config)
+    with torch.no_grad():
+        for mod in m.modules():
+            if isinstance(mod, nn.BatchNorm2d):
+                mod.running_mean.normal_(0, 0.05)
+                mod.running_var.uniform_(0.8, 1.2)
+                mod.weight.uniform_(0.5, 1.0)
+                mod.bias.normal_(0, 0.05)
+    return m.eval()
+
+
+def test_efficientnet_v2s_torchvision_weights():
+    ref = _tv_effnet(_EFF_SMALL)
+    img = torch.randint(0, 256, (2, 64, 64, 3), dtype=torch.uint8)
+    with torch.no_grad():
+        want = ref(_normalize(img))
+    m = W.efficientnet_v2s_from_torchvision(ref.state_dict(), device="cpu", backend="torch", image_size=64,
+                                            config=_EFF_SMALL)
+    got = m.logits(img)
+    assert torch.allclose(got, want, atol=2e-3 * want.abs().max().item(), rtol=1e-3), (got - want).abs().max()
+
+
+@pytest.mark.gpu
+def test_efficientnet_v2s_torchvision_weights_on_hip_kernels():
+    from ray_dynamic_batching_amd.models.efficientnet import CONFIG
+
+    ref = _tv_effnet(CONFIG)
+    img = torch.randint(0, 256, (2, 384, 384, 3), dtype=torch.uint8)
+    with torch.no_grad():
+        want = ref(_normalize(img))
+    m = W.efficientnet_v2s_from_torchvision(ref.state_dict(), device="cuda", backend="hip")
+    got = m.logits(img.cuda()).cpu()
+    assert (got - want).abs().max().item() < 5e-2 * want.abs().max().item() + 1e-2
