@@ -18,10 +18,12 @@ from .context import get_replica_context
 from .exceptions import BackPressureError, RayServeException, RequestCancelledError, RequestDroppedError
 from .handle import DeploymentHandle, DeploymentResponse, DeploymentResponseGenerator
 from .http_proxy import HTTPRequest
+from .ingress import ingress
 from .multiplex import get_multiplexed_model_id, multiplexed
 from .servable import TensorCodec, model_deployment
 
 __all__ = [
+    "ingress",
     "Application", "Deployment", "deployment", "batch", "run", "start", "shutdown", "delete", "status",
     "get_app_handle", "get_deployment_handle", "get_replica_context", "multiplexed", "get_multiplexed_model_id",
     "DeploymentHandle", "DeploymentResponse", "DeploymentResponseGenerator", "AutoscalingConfig",

@@ -29,10 +29,12 @@ logger = logging.getLogger("ray_dynamic_batching_amd.serve")
 class HTTPRequest:
     """Picklable subset of starlette's Request handed to the ingress deployment."""
 
-    def __init__(self, method: str, path: str, query_params: Dict[str, str], headers: Dict[str, str], body: bytes):
+    def __init__(self, method: str, path: str, query_params: Dict[str, str], headers: Dict[str, str], body: bytes,
+                 route_path: str = ""):
         self.method = method
         self.path = path
         self.url_path = path
+        self.route_path = route_path or path      # path below the application's route prefix
         self.query_params = query_params
         self.headers = headers
         self._body = body
@@ -99,7 +101,7 @@ class HTTPProxy:
             m = self._match(request.url.path)
             if m is None:
                 return JSONResponse({"error": f"no application at {request.url.path}"}, status_code=404)
-            app_name, _ = m
+            app_name, prefix = m
             try:
                 handle_ = self.controller.get_app_handle(app_name)
                 body = await request.body()
@@ -113,9 +115,15 @@ class HTTPProxy:
                     result = await handle_.remote(arr)
                     payload, ctype = _encode({"outputs": result})
                 else:
+                    sub = request.url.path[len(prefix):] or "/"
                     req = HTTPRequest(request.method, request.url.path, dict(request.query_params),
-                                      dict(request.headers), body)
+                                      dict(request.headers), body, route_path=sub)
                     result = await handle_.remote(req)
+                    from .ingress import ASGIResponse
+
+                    if isinstance(result, ASGIResponse):        # @serve.ingress app: its own status / headers
+                        hdrs = {k.decode(): v.decode() for k, v in result.headers if k.lower() != b"content-length"}
+                        return Response(result.body, status_code=result.status, headers=hdrs)
                     payload, ctype = _encode(result)
                 return Response(payload, media_type=ctype)
             except BackPressureError as e:

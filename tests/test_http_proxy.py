@@ -77,3 +77,65 @@ def test_http_tensor_servable_local():
 
     ref = MLP(device="cpu")(torch.from_numpy(x)[None])[0].numpy()
     assert st == 200 and np.allclose(got, ref, atol=1e-5)
+
+
+import sys  # noqa: E402
+
+import cloudpickle  # noqa: E402
+
+cloudpickle.register_pickle_by_value(sys.modules[__name__])   # replica processes cannot import tests/
+
+try:     # module level: pydantic keeps the defining namespace of a model, so a model
+    # (and app) defined inside a function would drag the app into the pickle
+    from fastapi import FastAPI, HTTPException
+    from pydantic import BaseModel
+
+    api = FastAPI()
+
+    class Item(BaseModel):
+        x: int
+        tag: str = "none"
+
+    @serve.deployment(num_replicas=2)
+    @serve.ingress(api)
+    class Api:
+        def __init__(self, k):
+            self.k = k
+
+        @api.get("/hello")
+        def hello(self, name: str = "world"):
+            return {"msg": f"hi {name}", "k": self.k}
+
+        @api.post("/items/{item_id}")
+        async def put(self, item_id: int, item: Item):
+            return {"id": item_id, "y": item.x * self.k, "tag": item.tag}
+
+        @api.get("/fail")
+        def fail(self):
+            raise HTTPException(status_code=418, detail="teapot")
+except ImportError:      # pragma: no cover
+    Api = None
+
+
+@pytest.mark.parametrize("mode", ["local", "process"])
+def test_serve_ingress_fastapi_class_routes(mode):
+    """@serve.ingress(FastAPI app): class-method routes bound to the replica
+    instance, path/query/body validation, status codes from the app."""
+    if Api is None:
+        pytest.skip("fastapi not installed")
+    serve.start(http_options={"host": "127.0.0.1", "port": 0})
+    port = serve.http_port()
+    serve.run(Api.bind(3), name="api", route_prefix="/api", mode=mode)
+    with urllib.request.urlopen(f"http://127.0.0.1:{port}/api/hello?name=mi355x", timeout=30) as r:
+        assert r.status == 200 and json.loads(r.read()) == {"msg": "hi mi355x", "k": 3}
+    st, body = _post(f"http://127.0.0.1:{port}/api/items/7", {"x": 5, "tag": "t"})
+    assert st == 200 and json.loads(body) == {"id": 7, "y": 15, "tag": "t"}
+    with pytest.raises(urllib.error.HTTPError) as e:
+        _post(f"http://127.0.0.1:{port}/api/items/7", {"tag": "no x"})       # pydantic validation
+    assert e.value.code == 422
+    with pytest.raises(urllib.error.HTTPError) as e:
+        urllib.request.urlopen(f"http://127.0.0.1:{port}/api/fail", timeout=30)
+    assert e.value.code == 418 and b"teapot" in e.value.read()
+    with pytest.raises(urllib.error.HTTPError) as e:
+        urllib.request.urlopen(f"http://127.0.0.1:{port}/api/missing", timeout=30)
+    assert e.value.code == 404
