@@ -1,4 +1,5 @@
-"""Model zoo of the serving stack (random init, synthetic inputs; no downloads).
+"""Model zoo of the serving stack (random init by default; ``create(name, checkpoint=path)``
+loads real weights through :mod:`.weights`).
 
 Every model follows the *servable* contract used by the replica engine:
 ``input_shape``, ``input_dtype``, ``output_shape``, ``output_dtype`` per request
@@ -52,45 +53,76 @@ def _mlp(**kw):
 
 
 @register("bert-base")
-def _bert(device="cuda", backend="hip", seq_len=128, layers=12, **kw):
+def _bert(device="cuda", backend="hip", seq_len=128, layers=12, checkpoint=None, **kw):
     from .bert import BertConfig, BertForSequenceClassification
 
+    if checkpoint:
+        from .weights import bert_from_hf
+
+        return bert_from_hf(checkpoint, seq_len=seq_len, device=device, backend=backend, **kw)
     return BertForSequenceClassification(BertConfig(seq_len=seq_len, layers=layers), device=device, backend=backend, **kw)
 
 
 @register("resnet50")
-def _resnet(device="cuda", backend="hip", **kw):
+def _resnet(device="cuda", backend="hip", checkpoint=None, **kw):
     from .resnet import ResNet50
 
-    return ResNet50(device=device, backend=backend, **kw)
+    m = ResNet50(device=device, backend=backend, **kw)
+    if checkpoint:
+        from .weights import load_resnet50
+
+        load_resnet50(m, checkpoint)
+    return m
 
 
 @register("llama3-8b")
-def _llama(device="cuda", backend="hip", tp_rank=0, tp_size=1, group_name=None, seq_len=512, layers=32, **kw):
+def _llama(device="cuda", backend="hip", tp_rank=0, tp_size=1, group_name=None, seq_len=512, layers=32,
+           checkpoint=None, **kw):
     from .llama import LlamaConfig, LlamaTP
 
+    if checkpoint:
+        from .weights import llama_from_hf
+
+        return llama_from_hf(checkpoint, seq_len=seq_len, tp_rank=tp_rank, tp_size=tp_size, group_name=group_name,
+                             device=device, backend=backend, **kw)
     return LlamaTP(LlamaConfig(seq_len=seq_len, layers=layers), tp_rank, tp_size, group_name, device=device,
                    backend=backend, **kw)
 
 
 @register("vit-b16")
-def _vit(device="cuda", backend="hip", **kw):
+def _vit(device="cuda", backend="hip", checkpoint=None, **kw):
     from .vit import ViT, ViTConfig
 
+    if checkpoint:
+        from .weights import load_state_dict, vit_from_hf
+
+        if "conv_proj.weight" in load_state_dict(checkpoint):     # torchvision vit_b_16
+            from .weights import load_vit
+
+            return load_vit(ViT(ViTConfig.b16(), device=device, backend=backend, **kw), checkpoint)
+        return vit_from_hf(checkpoint, device=device, backend=backend, **kw)
     return ViT(ViTConfig.b16(), device=device, backend=backend, **kw)
 
 
 @register("shufflenet-v2")
-def _shufflenet(device="cuda", backend="hip", **kw):
+def _shufflenet(device="cuda", backend="hip", checkpoint=None, **kw):
     from .shufflenet import ShuffleNetV2
 
+    if checkpoint:
+        from .weights import shufflenet_v2_from_torchvision
+
+        return shufflenet_v2_from_torchvision(checkpoint, device=device, backend=backend, **kw)
     return ShuffleNetV2(device=device, backend=backend, **kw)
 
 
 @register("efficientnet-v2s")
-def _efficientnet(device="cuda", backend="hip", **kw):
+def _efficientnet(device="cuda", backend="hip", checkpoint=None, **kw):
     from .efficientnet import EfficientNetV2S
 
+    if checkpoint:
+        from .weights import efficientnet_v2s_from_torchvision
+
+        return efficientnet_v2s_from_torchvision(checkpoint, device=device, backend=backend, **kw)
     return EfficientNetV2S(device=device, backend=backend, **kw)
 
 

@@ -515,3 +515,19 @@ def test_efficientnet_v2s_torchvision_weights_on_hip_kernels():
     m = W.efficientnet_v2s_from_torchvision(ref.state_dict(), device="cuda", backend="hip")
     got = m.logits(img.cuda()).cpu()
     assert (got - want).abs().max().item() < 5e-2 * want.abs().max().item() + 1e-2
+
+
+def test_registry_create_with_checkpoint(tmp_path):
+    from ray_dynamic_batching_amd import models
+
+    _hf_llama(tmp_path, scaling=False)
+    m = models.create("llama3-8b", checkpoint=str(tmp_path / "llama"), seq_len=16, device="cpu",
+                      dtype=torch.float32, backend="torch")
+    assert m.cfg.hidden == 256 and m.cfg.layers == 2
+    ref = _tv_shufflenet()
+    torch.save(ref.state_dict(), tmp_path / "sn.pth")
+    sn = models.create("shufflenet-v2", checkpoint=str(tmp_path / "sn.pth"), device="cpu", backend="torch",
+                       image_size=64)
+    img = torch.randint(0, 256, (1, 64, 64, 3), dtype=torch.uint8)
+    with torch.no_grad():
+        assert torch.allclose(sn.logits(img), ref(_normalize(img)), atol=1e-2, rtol=1e-2)
