@@ -151,6 +151,12 @@ def shutdown() -> None:
                 kill(h, _ctx_override=ctx)
             except Exception:
                 pass
+    from .util import _pg_mod as _pgm
+
+    with _pgm._lock:        # reservations die with this driver's allocator
+        for g in _pgm._groups.values():
+            g.state = "REMOVED"
+        _pgm._groups.clear()
     ctx.tasks.shutdown(wait=False, cancel_futures=True)
     shutil.rmtree(ctx.sock_dir, ignore_errors=True)
 
@@ -418,8 +424,29 @@ def _pending_timeout() -> float:
     return float(os.environ.get("RDB_CORE_PENDING_TIMEOUT_S", "30"))
 
 
-def _allocate(ctx: _Context, owner: str, num_gpus: float):
+def _pg_option(o: Dict[str, Any]):
+    """(placement group, bundle index) from ``scheduling_strategy=`` or the
+    legacy ``placement_group=`` / ``placement_group_bundle_index=`` options."""
+    st = o.get("scheduling_strategy")
+    if st is not None and hasattr(st, "placement_group"):
+        return st.placement_group, int(st.placement_group_bundle_index)
+    if o.get("placement_group") not in (None, "default"):
+        return o["placement_group"], int(o.get("placement_group_bundle_index", -1))
+    return None, -1
+
+
+def _allocate(ctx: _Context, owner: str, num_gpus: float, pg=None, bundle_index: int = -1):
     from ..runtime.resources import visible_devices_env
+
+    if pg is not None:       # carve the demand out of a reserved bundle
+        from ..runtime.resources import Allocation
+
+        _, gpus = pg._take(owner, float(num_gpus or 0), bundle_index)
+        gpus = gpus if num_gpus else []
+        env = dict(visible_devices_env(gpus)) if num_gpus else {}
+        env["RDB_CORE_GPU_IDS"] = ",".join(str(g) for g in gpus)
+        env["RDB_CORE_NAMESPACE"] = ctx.namespace
+        return Allocation(owner, gpus, float(num_gpus or 0), 0), env
 
     deadline = time.monotonic() + _pending_timeout()
     while True:   # like Ray, a creation that does not fit yet waits for resources
@@ -468,7 +495,8 @@ class ActorClass:
         args, kwargs = _resolve_args(args, kwargs)
         actor_id = uuid.uuid4().hex[:16]
         maxc = int(o.get("max_concurrency", 1))
-        a, env = _allocate(ctx, actor_id, o.get("num_gpus", 0))
+        pg, bidx = _pg_option(o)
+        a, env = _allocate(ctx, actor_id, o.get("num_gpus", 0), pg, bidx)
         try:
             if ctx.local_mode:
                 prev = getattr(_tls, "env", None)
@@ -484,6 +512,8 @@ class ActorClass:
                 h, pid = self._spawn(ctx, actor_id, args, kwargs, env, maxc, name, detached)
         except BaseException:
             ctx.allocator.release(actor_id)
+            if pg is not None:
+                pg._give_back(actor_id)
             raise
         ctx.owned.append(h)
         _register(ctx, h, pid, o.get("namespace"), a.gpus)
@@ -603,6 +633,11 @@ def kill(actor: ActorHandle, *, no_restart: bool = True, _ctx_override: Optional
         if ch is not None:
             ch.close()
     ctx.allocator.release(actor._actor_id)
+    from .util.placement_group import _owner_group
+
+    g = _owner_group(actor._actor_id)
+    if g is not None:
+        g._give_back(actor._actor_id)
     _unregister(ctx, actor)
     if actor in ctx.owned:
         ctx.owned.remove(actor)

@@ -82,6 +82,97 @@ class GpuAllocator:
             self.allocs[owner] = a
             return a
 
+    def allocate_bundles(self, owner: str, amounts: List[float], strategy: str = "PACK") -> Optional[List[Allocation]]:
+        """Gang (all-or-nothing) reservation of placement-group bundles, the
+        same per-GPU reading of the strategies as the native agent's
+        ``allocate_bundles`` (node_agent.cpp): STRICT_PACK = every bundle on one
+        GPU, STRICT_SPREAD = each bundle on its own GPU(s), PACK / SPREAD = try
+        the strict form, else place bundles one by one (best fit).  Bundle ``i``
+        is held as owner ``f"{owner}/{i}"``.  None if it does not fit now."""
+        if strategy not in ("PACK", "SPREAD", "STRICT_PACK", "STRICT_SPREAD"):
+            raise ValueError(f"unknown placement strategy {strategy!r}")
+        for a in amounts:
+            if a < 0 or (a > 1 and abs(a - round(a)) > _EPS):
+                raise ValueError("bundle GPU amounts must be fractions <= 1 or whole numbers")
+        with self._lock:
+            free = [s.free for s in self.slots]
+            plan = None
+            if strategy in ("STRICT_PACK", "PACK"):
+                plan = self._plan_pack(amounts, free)
+            elif strategy in ("STRICT_SPREAD", "SPREAD"):
+                plan = self._plan_spread(amounts, free)
+            if plan is None and strategy in ("PACK", "SPREAD"):
+                plan = self._plan_each(amounts, free)
+            if plan is None:
+                return None
+            out = []
+            for i, (gpus, per) in enumerate(plan):
+                name = f"{owner}/{i}"
+                for g in gpus:
+                    self.slots[g].used += per
+                    self.slots[g].holders[name] = per
+                a = Allocation(name, gpus, per if gpus else 0.0, 0)
+                self.allocs[name] = a
+                out.append(a)
+            return out
+
+    @staticmethod
+    def _plan_pack(amounts, free):
+        total = sum(amounts)
+        if total <= _EPS:
+            return [([], 0.0) for _ in amounts]
+        if total > 1 + _EPS:
+            return None                     # one GPU holds at most 1.0
+        fits = [g for g, f in enumerate(free) if f + _EPS >= total]
+        if not fits:
+            return None
+        g = min(fits, key=lambda i: (free[i] - total, i))
+        return [([g], a) if a > 0 else ([], 0.0) for a in amounts]
+
+    @staticmethod
+    def _plan_spread(amounts, free):
+        free, taken, plan = list(free), set(), [None] * len(amounts)
+        for i in sorted(range(len(amounts)), key=lambda j: -amounts[j]):
+            a = amounts[i]
+            if a <= _EPS:
+                plan[i] = ([], 0.0)
+                continue
+            need = int(round(a)) if a >= 1 else 1
+            per = 1.0 if a >= 1 else a
+            cand = sorted((g for g, f in enumerate(free) if g not in taken and f + _EPS >= per),
+                          key=lambda g: (free[g] - per, g))
+            if len(cand) < need:
+                return None
+            gs = cand[:need]
+            for g in gs:
+                free[g] -= per
+                taken.add(g)
+            plan[i] = (gs, per)
+        return plan
+
+    @staticmethod
+    def _plan_each(amounts, free):
+        free, plan = list(free), []
+        for a in amounts:
+            if a <= _EPS:
+                plan.append(([], 0.0))
+                continue
+            if a >= 1:
+                gs = [g for g, f in enumerate(free) if f >= 1 - _EPS][:int(round(a))]
+                if len(gs) < int(round(a)):
+                    return None
+                for g in gs:
+                    free[g] = 0.0
+                plan.append((gs, 1.0))
+            else:
+                fits = [g for g, f in enumerate(free) if f + _EPS >= a]
+                if not fits:
+                    return None
+                g = min(fits, key=lambda i: (free[i] - a, i))
+                free[g] -= a
+                plan.append(([g], a))
+        return plan
+
     def release(self, owner: str) -> None:
         with self._lock:
             a = self.allocs.pop(owner, None)

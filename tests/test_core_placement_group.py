@@ -1,0 +1,79 @@
+"""core.util.placement_group (reference python/ray/util/placement_group.py:145,
+scheduling_strategies.py:41): gang reservation with the per-GPU strategy
+reading shared with Serve's bundles, actors scheduled into bundles (GPU
+pinning, capacity), waiting / failing reservations, removal."""
+import os
+import sys
+import uuid
+
+import cloudpickle
+import pytest
+
+import ray_dynamic_batching_amd.core as ray
+from ray_dynamic_batching_amd.core.util import (get_placement_group, placement_group, placement_group_table,
+                                                 remove_placement_group)
+from ray_dynamic_batching_amd.core.util.scheduling_strategies import PlacementGroupSchedulingStrategy
+from ray_dynamic_batching_amd.runtime.resources import GpuAllocator
+
+cloudpickle.register_pickle_by_value(sys.modules[__name__])
+
+
+def test_allocator_bundle_strategies():
+    a = GpuAllocator(4)
+    sp = a.allocate_bundles("p", [0.5, 0.25], "STRICT_PACK")
+    assert sp[0].gpus == sp[1].gpus                      # one GPU
+    ss = a.allocate_bundles("s", [1, 1, 0.5], "STRICT_SPREAD")
+    used = [g for x in ss for g in x.gpus]
+    assert len(used) == len(set(used)) == 3 and sp[0].gpus[0] not in used
+    assert a.allocate_bundles("x", [0.5, 0.5], "STRICT_SPREAD") is None    # only 1 GPU has room for 2 x 0.5? no
+    assert a.allocate_bundles("y", [1, 1], "PACK") is None                 # no whole GPUs left
+    pk = a.allocate_bundles("z", [0.25, 0.25], "PACK")                     # fits on the packed GPU
+    assert pk is not None and pk[0].gpus == pk[1].gpus
+    for i in range(2):
+        a.release(f"p/{i}")
+    assert a.allocate_bundles("y2", [1], "PACK") is not None
+    with pytest.raises(ValueError):
+        a.allocate_bundles("bad", [1.5], "PACK")
+
+
+@pytest.fixture(params=["process", "local"])
+def rt(request):
+    ray.init(num_gpus=4, local_mode=request.param == "local", namespace="p" + uuid.uuid4().hex[:8])
+    yield request.param
+    ray.shutdown()
+
+
+class Pinned:
+    def gpus(self):
+        import ray_dynamic_batching_amd.core as r
+
+        return r.get_gpu_ids(), os.environ.get("HIP_VISIBLE_DEVICES")
+
+
+def test_placement_group_actors(rt):
+    pg = placement_group([{"GPU": 1}, {"GPU": 1}], strategy="STRICT_SPREAD", name="tp2")
+    assert ray.get(pg.ready()) is pg and pg.wait(5)
+    assert ray.available_resources()["GPU"] == 2
+    A = ray.remote(Pinned)
+    a0 = A.options(num_gpus=1, scheduling_strategy=PlacementGroupSchedulingStrategy(pg, 0)).remote()
+    a1 = A.options(num_gpus=1, placement_group=pg, placement_group_bundle_index=1).remote()
+    g0, g1 = ray.get(a0.gpus.remote())[0], ray.get(a1.gpus.remote())[0]
+    assert g0 == pg.bundle_gpus[0] and g1 == pg.bundle_gpus[1] and g0 != g1
+    with pytest.raises(ValueError):          # bundle 0 is full
+        A.options(num_gpus=1, scheduling_strategy=PlacementGroupSchedulingStrategy(pg, 0)).remote()
+    assert ray.available_resources()["GPU"] == 2    # actors in the group do not take free GPUs
+    assert get_placement_group("tp2") is pg
+    assert placement_group_table(pg)["state"] == "CREATED"
+    # fractional bundles: two half-GPU actors share one packed GPU
+    half = placement_group([{"GPU": 0.5}, {"GPU": 0.5}], strategy="STRICT_PACK")
+    assert half.wait(5) and half.bundle_gpus[0] == half.bundle_gpus[1]
+    h = [A.options(num_gpus=0.5, scheduling_strategy=PlacementGroupSchedulingStrategy(half)).remote()
+         for _ in range(2)]
+    assert ray.get(h[0].gpus.remote())[0] == ray.get(h[1].gpus.remote())[0] == half.bundle_gpus[0]
+    remove_placement_group(pg)
+    assert ray.available_resources()["GPU"] == 3.0
+    with pytest.raises(ray.RayError):
+        ray.get(a0.gpus.remote(), timeout=10)   # members die with their group
+    # a group that cannot fit fails its ready()
+    big = placement_group([{"GPU": 1}] * 5, strategy="STRICT_SPREAD", _timeout_s=0.5)
+    assert not big.wait(3) and big.state == "FAILED"
