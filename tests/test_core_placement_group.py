@@ -77,3 +77,31 @@ def test_placement_group_actors(rt):
     # a group that cannot fit fails its ready()
     big = placement_group([{"GPU": 1}] * 5, strategy="STRICT_SPREAD", _timeout_s=0.5)
     assert not big.wait(3) and big.state == "FAILED"
+
+
+class Sq:
+    def __init__(self, d):
+        self.d = d
+
+    def f(self, x):
+        import time
+
+        time.sleep(self.d * (x % 3))
+        return x * x
+
+
+def test_actor_pool(rt):
+    from ray_dynamic_batching_amd.core.util import ActorPool
+
+    S = ray.remote(Sq)
+    pool = ActorPool([S.remote(0.01), S.remote(0.01)])
+    assert list(pool.map(lambda a, v: a.f.remote(v), range(8))) == [x * x for x in range(8)]
+    assert sorted(pool.map_unordered(lambda a, v: a.f.remote(v), range(8))) == sorted(x * x for x in range(8))
+    for v in range(5):
+        pool.submit(lambda a, v: a.f.remote(v), v)          # 3 of them queue behind 2 actors
+    assert [pool.get_next() for _ in range(5)] == [0, 1, 4, 9, 16]
+    assert not pool.has_next() and pool.has_free()
+    a = pool.pop_idle()
+    with pytest.raises(ValueError):
+        pool.push(pool._idle[0])
+    pool.push(a)
