@@ -34,6 +34,7 @@ def main(argv=None):
     ap.add_argument("--requests", type=int, default=400)
     ap.add_argument("--concurrency", type=int, default=16)
     ap.add_argument("--json-out", default="")
+    ap.add_argument("--checkpoint", default="", help="Hugging Face Llama checkpoint dir (each rank loads its shard)")
     ap.add_argument("--allreduce", default="xgmi", choices=["xgmi", "rccl"],
                     help="TP all-reduce: custom push-based xGMI kernel (fused RMSNorm) or RCCL")
     a = ap.parse_args(argv)
@@ -55,7 +56,14 @@ def main(argv=None):
             col.enable_xgmi("tp", max_elems=8 * a.seq * 4096)
     cfg = LlamaConfig.llama3_8b(seq_len=a.seq, layers=a.layers)
     t0 = time.time()
-    m = LlamaTP(cfg, rank, world, "tp" if world > 1 else None, device=f"cuda:{local}", init="shard")
+    if a.checkpoint:
+        from ray_dynamic_batching_amd.models.weights import llama_from_hf
+
+        m = llama_from_hf(a.checkpoint, seq_len=a.seq, tp_rank=rank, tp_size=world,
+                          group_name="tp" if world > 1 else None, device=f"cuda:{local}")
+        cfg = m.cfg
+    else:
+        m = LlamaTP(cfg, rank, world, "tp" if world > 1 else None, device=f"cuda:{local}", init="shard")
     init_s = time.time() - t0
     if a.serve:
         return _serve(a, m, world, rank)
