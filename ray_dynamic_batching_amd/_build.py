@@ -46,7 +46,10 @@ def runtime_target() -> Path:
 
 
 def _ops_sources() -> list[Path]:
-    return sorted(OPS_SRC.glob("*.hip")) + sorted(OPS_SRC.glob("*.cpp"))
+    # largest translation units first (the GEMM template instantiations), so the
+    # longest compiles start at once on the job pool
+    srcs = sorted(OPS_SRC.glob("*.hip")) + sorted(OPS_SRC.glob("*.cpp"))
+    return sorted(srcs, key=lambda p: (not p.name.startswith(("conv", "gemm_bf16", "gemm_f16", "gemm_ln", "qkv")), p.name))
 
 
 def _deps(srcs: list[Path], extra_dirs: list[Path]) -> list[Path]:
