@@ -83,28 +83,64 @@ class GpuAllocator:
             return a
 
     def allocate_bundles(self, owner: str, amounts: List[float], strategy: str = "PACK") -> Optional[List[Allocation]]:
-        """Gang (all-or-nothing) reservation of placement-group bundles, the
-        same per-GPU reading of the strategies as the native agent's
-        ``allocate_bundles`` (node_agent.cpp): STRICT_PACK = every bundle on one
-        GPU, STRICT_SPREAD = each bundle on its own GPU(s), PACK / SPREAD = try
-        the strict form, else place bundles one by one (best fit).  Bundle ``i``
-        is held as owner ``f"{owner}/{i}"``.  None if it does not fit now."""
+        """Gang (all-or-nothing) reservation of placement-group bundles with the
+        native agent's algorithm (``GpuAllocator::allocate_bundles`` in
+        runtime/csrc/node_agent.cpp; the differential test pins them together):
+        bundles in order; a whole-GPU bundle takes free GPUs first-fit; a
+        fractional one goes best-fit with this group's GPUs preferred (PACK) or
+        avoided (SPREAD); STRICT_PACK keeps every bundle on one GPU, STRICT_SPREAD
+        never reuses a GPU of the group.  Bundle ``i`` is held as owner
+        ``f"{owner}/{i}"``.  None if the gang does not fit now."""
+        unit = 10000
         if strategy not in ("PACK", "SPREAD", "STRICT_PACK", "STRICT_SPREAD"):
             raise ValueError(f"unknown placement strategy {strategy!r}")
-        for a in amounts:
-            if a < 0 or (a > 1 and abs(a - round(a)) > _EPS):
-                raise ValueError("bundle GPU amounts must be fractions <= 1 or whole numbers")
+        spread = strategy in ("SPREAD", "STRICT_SPREAD")
         with self._lock:
-            free = [s.free for s in self.slots]
-            plan = None
-            if strategy in ("STRICT_PACK", "PACK"):
-                plan = self._plan_pack(amounts, free)
-            elif strategy in ("STRICT_SPREAD", "SPREAD"):
-                plan = self._plan_spread(amounts, free)
-            if plan is None and strategy in ("PACK", "SPREAD"):
-                plan = self._plan_each(amounts, free)
-            if plan is None:
-                return None
+            used = [int(round(sl.used * unit)) for sl in self.slots]
+            mine: List[int] = []
+            plan = []
+            pack_gpu = -1
+            for amount in amounts:
+                units = int(round(amount * unit))
+                if units <= 0:
+                    plan.append(([], 0.0))
+                    continue
+                if units >= unit:
+                    if units % unit:
+                        raise ValueError("bundle GPU amounts > 1 must be whole numbers")
+                    need = units // unit
+                    if strategy == "STRICT_PACK" and (len(amounts) > 1 or need > 1):
+                        return None
+                    got = [g for g in range(len(used)) if used[g] == 0][:need]
+                    if len(got) < need:
+                        return None
+                    for g in got:
+                        used[g] = unit
+                        if g not in mine:
+                            mine.append(g)
+                    plan.append((got, 1.0))
+                    continue
+                best, best_key = -1, None
+                for g in range(len(used)):
+                    left = unit - used[g] - units
+                    if left < 0:
+                        continue
+                    if strategy == "STRICT_PACK" and pack_gpu >= 0 and g != pack_gpu:
+                        continue
+                    if strategy == "STRICT_SPREAD" and g in mine:
+                        continue
+                    pref = (1 if spread else 0) if g in mine else (0 if spread else 1)
+                    key = pref * 2 * unit + left
+                    if best_key is None or key < best_key:
+                        best, best_key = g, key
+                if best < 0:
+                    return None
+                used[best] += units
+                if best not in mine:
+                    mine.append(best)
+                if strategy == "STRICT_PACK":
+                    pack_gpu = best
+                plan.append(([best], units / unit))
             out = []
             for i, (gpus, per) in enumerate(plan):
                 name = f"{owner}/{i}"
@@ -115,63 +151,6 @@ class GpuAllocator:
                 self.allocs[name] = a
                 out.append(a)
             return out
-
-    @staticmethod
-    def _plan_pack(amounts, free):
-        total = sum(amounts)
-        if total <= _EPS:
-            return [([], 0.0) for _ in amounts]
-        if total > 1 + _EPS:
-            return None                     # one GPU holds at most 1.0
-        fits = [g for g, f in enumerate(free) if f + _EPS >= total]
-        if not fits:
-            return None
-        g = min(fits, key=lambda i: (free[i] - total, i))
-        return [([g], a) if a > 0 else ([], 0.0) for a in amounts]
-
-    @staticmethod
-    def _plan_spread(amounts, free):
-        free, taken, plan = list(free), set(), [None] * len(amounts)
-        for i in sorted(range(len(amounts)), key=lambda j: -amounts[j]):
-            a = amounts[i]
-            if a <= _EPS:
-                plan[i] = ([], 0.0)
-                continue
-            need = int(round(a)) if a >= 1 else 1
-            per = 1.0 if a >= 1 else a
-            cand = sorted((g for g, f in enumerate(free) if g not in taken and f + _EPS >= per),
-                          key=lambda g: (free[g] - per, g))
-            if len(cand) < need:
-                return None
-            gs = cand[:need]
-            for g in gs:
-                free[g] -= per
-                taken.add(g)
-            plan[i] = (gs, per)
-        return plan
-
-    @staticmethod
-    def _plan_each(amounts, free):
-        free, plan = list(free), []
-        for a in amounts:
-            if a <= _EPS:
-                plan.append(([], 0.0))
-                continue
-            if a >= 1:
-                gs = [g for g, f in enumerate(free) if f >= 1 - _EPS][:int(round(a))]
-                if len(gs) < int(round(a)):
-                    return None
-                for g in gs:
-                    free[g] = 0.0
-                plan.append((gs, 1.0))
-            else:
-                fits = [g for g, f in enumerate(free) if f + _EPS >= a]
-                if not fits:
-                    return None
-                g = min(fits, key=lambda i: (free[i] - a, i))
-                free[g] -= a
-                plan.append(([g], a))
-        return plan
 
     def release(self, owner: str) -> None:
         with self._lock:

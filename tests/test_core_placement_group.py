@@ -24,14 +24,15 @@ def test_allocator_bundle_strategies():
     assert sp[0].gpus == sp[1].gpus                      # one GPU
     ss = a.allocate_bundles("s", [1, 1, 0.5], "STRICT_SPREAD")
     used = [g for x in ss for g in x.gpus]
-    assert len(used) == len(set(used)) == 3 and sp[0].gpus[0] not in used
-    assert a.allocate_bundles("x", [0.5, 0.5], "STRICT_SPREAD") is None    # only 1 GPU has room for 2 x 0.5? no
-    assert a.allocate_bundles("y", [1, 1], "PACK") is None                 # no whole GPUs left
-    pk = a.allocate_bundles("z", [0.25, 0.25], "PACK")                     # fits on the packed GPU
+    assert len(used) == len(set(used)) == 3
+    assert a.allocate_bundles("y", [1, 1], "PACK") is None                 # no two whole GPUs left
+    pk = a.allocate_bundles("z", [0.125, 0.125], "PACK")                   # packs onto one GPU
     assert pk is not None and pk[0].gpus == pk[1].gpus
+    assert a.allocate_bundles("x", [0.5, 0.5, 0.5], "STRICT_SPREAD") is None
     for i in range(2):
         a.release(f"p/{i}")
-    assert a.allocate_bundles("y2", [1], "PACK") is not None
+        a.release(f"z/{i}")
+    assert a.allocate_bundles("y2", [1], "PACK")[0].gpus == [0]
     with pytest.raises(ValueError):
         a.allocate_bundles("bad", [1.5], "PACK")
 
@@ -105,3 +106,38 @@ def test_actor_pool(rt):
     with pytest.raises(ValueError):
         pool.push(pool._idle[0])
     pool.push(a)
+
+
+def test_python_bundle_allocator_matches_native_agent():
+    """Differential: core placement groups (Python GpuAllocator.allocate_bundles)
+    and Serve bundles (native NodeAgent.allocate_bundles) place the same random
+    gang requests on the same GPUs, or both refuse them."""
+    import random
+
+    from ray_dynamic_batching_amd.runtime import agent as ragent
+
+    rng = random.Random(11)
+    nat = ragent.NodeAgent(8, 288.0)
+    py = GpuAllocator(8)
+    live = []
+    try:
+        for step in range(200):
+            if live and rng.random() < 0.35:
+                name, n = live.pop(rng.randrange(len(live)))
+                assert nat.release(name)
+                for i in range(n):
+                    py.release(f"{name}/{i}")
+                continue
+            n = rng.randint(1, 3)
+            amounts = [rng.choice([0.25, 0.5, 1, 2, 0.125]) for _ in range(n)]
+            strategy = rng.choice(["PACK", "SPREAD", "STRICT_PACK", "STRICT_SPREAD"])
+            name = f"g{step}"
+            got_n = nat.allocate_bundles(name, [(a, 0) for a in amounts], strategy)
+            got_p = py.allocate_bundles(name, amounts, strategy)
+            assert (got_n is None) == (got_p is None), (step, amounts, strategy, got_n, got_p)
+            if got_n is not None:
+                assert got_n["bundle_gpus"] == [a.gpus for a in got_p], (step, amounts, strategy)
+                live.append((name, n))
+            assert [round(g["used"], 6) for g in nat.resources()] == [round(s.used, 6) for s in py.slots], step
+    finally:
+        nat.shutdown()
