@@ -49,7 +49,7 @@ from multiprocessing.connection import Client as _ConnClient
 from typing import Any, Dict, List, Optional, Sequence, Tuple
 
 __all__ = ["init", "is_initialized", "shutdown", "remote", "get", "put", "wait", "kill", "get_actor",
-           "get_gpu_ids", "cluster_resources", "available_resources", "ObjectRef", "ActorHandle",
+           "get_gpu_ids", "cluster_resources", "available_resources", "timeline", "ObjectRef", "ActorHandle",
            "RayError", "RayTaskError", "RayActorError", "GetTimeoutError", "state", "util", "data", "dag"]
 
 
@@ -265,6 +265,42 @@ def wait(refs: Sequence[ObjectRef], *, num_returns: int = 1, timeout: Optional[f
         time.sleep(0.001)
 
 
+# ---------------------------------------------------------------------------
+# timeline (reference: ``ray.timeline`` -> _private/state.py:948, profiling.py:84)
+# ---------------------------------------------------------------------------
+_timeline: List[dict] = []
+_timeline_lock = threading.Lock()
+_TIMELINE_CAP = 100000
+
+
+def _traced(ref: ObjectRef, name: str, lane: str) -> ObjectRef:
+    """Record submit -> completion of an actor call / task as one span."""
+    t0 = time.time()
+
+    def done(f: Future):
+        ev = dict(name=name, cat="actor_call" if lane != "tasks" else "task", ph="X", ts=t0 * 1e6,
+                  dur=(time.time() - t0) * 1e6, pid="rdb-core", tid=lane,
+                  args={"ok": f.exception() is None})
+        with _timeline_lock:
+            if len(_timeline) < _TIMELINE_CAP:
+                _timeline.append(ev)
+
+    ref._fut.add_done_callback(done)
+    return ref
+
+
+def timeline(filename: Optional[str] = None) -> List[dict]:
+    """Chrome-trace events (``chrome://tracing`` / Perfetto) of the actor calls
+    and tasks this driver submitted, submit to completion, one row per actor;
+    written to ``filename`` as JSON if given (like ``ray timeline``)."""
+    with _timeline_lock:
+        events = list(_timeline)
+    if filename:
+        with open(filename, "w") as f:
+            json.dump(events, f)
+    return events
+
+
 def _resolve_args(args, kwargs):
     """Top-level ObjectRef arguments are passed by value (Ray semantics)."""
     args = tuple(get(a) if isinstance(a, ObjectRef) else a for a in args)
@@ -388,11 +424,12 @@ class ActorHandle:
 
                     raise RayTaskError(e, traceback.format_exc()) from e
 
-            return ObjectRef(pool.submit(run))
+            return _traced(ObjectRef(pool.submit(run)), f"{self._class_name}.{method}", self._actor_id)
         if not self._address:
             return _failed_ref(RayActorError(f"actor {self._actor_id} is not reachable from this process"))
         try:
-            return ObjectRef(self._channel().call(method, args, kwargs))
+            return _traced(ObjectRef(self._channel().call(method, args, kwargs)), f"{self._class_name}.{method}",
+                           self._actor_id)
         except (OSError, EOFError, ConnectionRefusedError) as e:
             return _failed_ref(RayActorError(f"cannot connect to actor {self._actor_id}: {e}"))
 
@@ -680,7 +717,7 @@ class RemoteFunction:
 
                     raise RayTaskError(e, traceback.format_exc()) from e
 
-            return ObjectRef(ctx.tasks.submit(run))
+            return _traced(ObjectRef(ctx.tasks.submit(run)), self.__name__, "tasks")
         # a GPU task runs in a one-shot process pinned to its GPUs
         host = ActorClass(_FnHost, {"num_gpus": num_gpus}).remote(self._fn)
         ref = host.run.remote(args, kwargs)

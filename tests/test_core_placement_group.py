@@ -141,3 +141,18 @@ def test_python_bundle_allocator_matches_native_agent():
             assert [round(g["used"], 6) for g in nat.resources()] == [round(s.used, 6) for s in py.slots], step
     finally:
         nat.shutdown()
+
+
+def test_timeline(rt, tmp_path):
+    import json
+
+    S = ray.remote(Sq)
+    a = S.remote(0.0)
+    ray.get([a.f.remote(i) for i in range(4)])
+    sq = ray.remote(lambda x: x + 1)
+    assert ray.get(sq.remote(1)) == 2
+    ev = ray.timeline(str(tmp_path / "tl.json"))
+    names = [e["name"] for e in ev]
+    assert names.count("Sq.f") >= 4 and "<lambda>" in names
+    assert all(e["ph"] == "X" and e["dur"] >= 0 for e in ev)
+    assert json.load(open(tmp_path / "tl.json")) == ev
