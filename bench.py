@@ -56,9 +56,23 @@ def parse():
     ap.add_argument("--rehearse-one-gpu", action="store_true",
                     help="rehearsal only: every rank's replica on cuda:0, gloo instead of RCCL (a 1-GPU box "
                          "running the N-rank protocol with real engines); never a measurement")
+    ap.add_argument("--tile-table", default="auto",
+                    help="GEMM tile table to replay (auto = the MI355X table shipped for this config when it "
+                         "exists; none = tune per shape and in context at start-up)")
     ap.add_argument("--json-out", default="")
     ap.add_argument("--trace-out", default="", help="write a Chrome trace of the replicas' batches")
     return ap.parse_args()
+
+
+def _tile_table(args) -> str:
+    if args.tile_table == "none" or args.backend != "hip":
+        return ""
+    if args.tile_table != "auto":
+        return args.tile_table
+    name = (f"mi355x_bert_L{args.layers}_S{args.seq}_B{args.max_batch}_"
+            f"cs{args.compute_streams}_d{args.pipeline_depth}.json")
+    p = os.path.join(os.path.dirname(os.path.abspath(__file__)), "ray_dynamic_batching_amd", "ops", "tuned", name)
+    return p if os.path.exists(p) else ""
 
 
 class _EchoRunner:
@@ -132,6 +146,12 @@ def main():
 
     cfg = BertConfig(seq_len=args.seq, layers=args.layers)
     os.environ.setdefault("RDB_TUNE_STREAMS", str(args.tune_streams or args.compute_streams))
+    tile_table = _tile_table(args)
+    if tile_table and "RDB_TUNE_FILE" not in os.environ:
+        # replay a tile table selected on MI355X (ops/tuned/README.md) instead of
+        # tuning at start-up: start-up tuning is timed on a few replays, so its
+        # picks -- and the served throughput -- vary run to run by up to ~10 %
+        os.environ["RDB_TUNE_FILE"] = tile_table
     if echo:
         runner = _EchoRunner(rjob.EchoServer(job, rank, [rank], args.max_batch, args.echo_service_us, 0.0, 8))
     else:
@@ -232,7 +252,8 @@ def main():
                        "global_batch": args.max_batch * n, "seq_len": args.seq,
                        "parallelism": f"dp{n}", "max_batch": args.max_batch,
                        "batch_wait_timeout_ms": args.max_wait_ms, "backend": args.backend,
-                       "load": (f"closed-loop x{args.concurrency}/GPU" if args.rate <= 0 else f"poisson {args.rate}/s/GPU")},
+                       "load": (f"closed-loop x{args.concurrency}/GPU" if args.rate <= 0 else f"poisson {args.rate}/s/GPU"),
+                       "tile_table": os.path.basename(os.environ.get("RDB_TUNE_FILE", "")) or "tuned at start-up"},
             "p50_ms": round(lat["p50_ms"], 3),
             "p99_ms": round(lat["p99_ms"], 3),
             "p999_ms": round(lat["p999_ms"], 3),
