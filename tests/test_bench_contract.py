@@ -26,3 +26,24 @@ def test_bench_two_ranks_echo_backend():
     assert d["completed"] == 40 * 32 * 2 and d["errors"] == 0
     assert abs(d["value"] - d["completed"] / (d["ms_per_step"] * d["steps"] / 1e3)) / d["value"] < 0.01
     assert min(d["per_replica_requests"]) > 0
+
+
+def test_bench_resolves_shipped_tile_table():
+    """bench.py's default (--tile-table auto) replays the MI355X table shipped for
+    the headline config; other configs / 'none' / non-HIP backends tune at start-up."""
+    import argparse
+    import importlib.util
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(root, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    a = argparse.Namespace(tile_table="auto", backend="hip", layers=12, seq=128, max_batch=32, compute_streams=2,
+                           pipeline_depth=4)
+    p = bench._tile_table(a)
+    assert p.endswith("mi355x_bert_L12_S128_B32_cs2_d4.json") and os.path.exists(p)
+    table = json.load(open(p))
+    assert any(k[0] == "gemm" and k[2:5] == [4096, 3072, 768] for k, _ in table)      # the bs32 FFN-up entry
+    assert bench._tile_table(argparse.Namespace(**dict(vars(a), layers=2))) == ""
+    assert bench._tile_table(argparse.Namespace(**dict(vars(a), tile_table="none"))) == ""
+    assert bench._tile_table(argparse.Namespace(**dict(vars(a), backend="torch"))) == ""
