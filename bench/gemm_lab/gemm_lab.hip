@@ -59,6 +59,15 @@ Variant pp(const char* nm) {
                                                                    ACT_NONE, s);
           }};
 }
+// one production-kernel tile, instantiated alone (core() instantiates the whole tile table)
+template <int BM, int BN, int WGM, int NW>
+Variant core1(const char* nm) {
+  return {nm, [](const bf16* A, const bf16* W, const bf16* b, bf16* C, int M, int N, int K, hipStream_t s) {
+            DenseParams p{A, K, M, K};
+            launch_one<bf16, bf16, DenseLoader, true, false, BM, BN, WGM, NW>(p, W, K, C, N, b, nullptr, 0, M, N, K,
+                                                                               1.f, ACT_NONE, s);
+          }};
+}
 Variant core(int cfg) {
   char nm[64];
   snprintf(nm, sizeof nm, "core cfg%d %dx%d/%dw", cfg, kTileBM[cfg], kTileBN[cfg], 4 * kTileNW[cfg] / 4);

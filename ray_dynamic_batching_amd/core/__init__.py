@@ -308,6 +308,88 @@ def _resolve_args(args, kwargs):
     return args, kwargs
 
 
+def _pending_deps(args, kwargs) -> List[Future]:
+    return [a._fut for a in list(args) + list(kwargs.values()) if isinstance(a, ObjectRef) and not a._fut.done()]
+
+
+def _upstream_error(args, kwargs) -> Optional[BaseException]:
+    for a in list(args) + list(kwargs.values()):
+        if isinstance(a, ObjectRef) and a._fut.done() and a._fut.exception() is not None:
+            return a._fut.exception()
+    return None
+
+
+def _all_done(futs: List[Future], fn) -> None:
+    if not futs:
+        fn()
+        return
+    left = [len(futs)]
+    lock = threading.Lock()
+
+    def one(_f):
+        with lock:
+            left[0] -= 1
+            last = left[0] == 0
+        if last:
+            fn()
+
+    for f in futs:
+        f.add_done_callback(one)
+
+
+# per-actor tail of deferred submissions: a call made while an earlier call on
+# the same actor still waits for its arguments is queued behind it, so actor
+# calls keep their submission order (Ray's per-caller actor-task ordering)
+_submit_tails: Dict[str, Future] = {}
+_submit_tails_lock = threading.Lock()
+
+
+def _deferred_submit(args, kwargs, submit_now, order_key: Optional[str] = None) -> Optional[ObjectRef]:
+    """``.remote()`` never blocks on argument refs (reference: ``ray.remote``
+    returns at once; dependencies resolve before the task runs): with every
+    argument ref resolved (or none), returns None and the caller submits at
+    once; otherwise the submission is chained on the pending refs and the
+    returned ref resolves with the call's result -- or with the upstream
+    exception, raised at ``get()`` like Ray's failed dependency."""
+    tail_prev: Optional[Future] = None
+    deps = _pending_deps(args, kwargs)
+    if order_key is not None:
+        with _submit_tails_lock:
+            tail_prev = _submit_tails.get(order_key)
+            if tail_prev is not None and tail_prev.done():
+                tail_prev = None
+                _submit_tails.pop(order_key, None)
+            if not deps and tail_prev is None:
+                return None
+            tail: Future = Future()
+            _submit_tails[order_key] = tail
+    elif not deps:
+        return None
+    else:
+        tail = Future()
+    out: Future = Future()
+
+    def go():
+        try:
+            err = _upstream_error(args, kwargs)
+            if err is not None:
+                out.set_exception(err)
+                return
+            a, kw = _resolve_args(args, kwargs)
+            try:
+                ref = submit_now(a, kw)
+            except BaseException as e:  # noqa: BLE001
+                out.set_exception(e)
+                return
+            ref._fut.add_done_callback(lambda r: out.set_exception(r.exception()) if r.exception() is not None
+                                       else out.set_result(r.result()))
+        finally:
+            tail.set_result(None)
+
+    _all_done(deps + ([tail_prev] if tail_prev is not None else []), go)
+    return ObjectRef(out)
+
+
 # ---------------------------------------------------------------------------
 # actors
 # ---------------------------------------------------------------------------
@@ -403,7 +485,16 @@ class ActorHandle:
             return ch
 
     def _call(self, method: str, args, kwargs) -> ObjectRef:
-        args, kwargs = _resolve_args(args, kwargs)
+        deferred = _deferred_submit(args, kwargs, lambda a, kw: self._call_now(method, a, kw),
+                                    order_key=self._actor_id)
+        if deferred is not None:
+            return deferred
+        err = _upstream_error(args, kwargs)
+        if err is not None:
+            return _failed_ref(err)
+        return self._call_now(method, *_resolve_args(args, kwargs))
+
+    def _call_now(self, method: str, args, kwargs) -> ObjectRef:
         if self._actor_id in _local_actors:
             obj, pool, env = _local_actors[self._actor_id]
             fn = getattr(obj, method)
@@ -704,7 +795,15 @@ class RemoteFunction:
 
     def remote(self, *args, **kwargs) -> ObjectRef:
         ctx = _require_ctx()
-        args, kwargs = _resolve_args(args, kwargs)
+        deferred = _deferred_submit(args, kwargs, lambda a, kw: self._remote_now(ctx, a, kw))
+        if deferred is not None:
+            return deferred
+        err = _upstream_error(args, kwargs)
+        if err is not None:
+            return _failed_ref(err)
+        return self._remote_now(ctx, *_resolve_args(args, kwargs))
+
+    def _remote_now(self, ctx, args, kwargs) -> ObjectRef:
         num_gpus = self._options.get("num_gpus", 0)
         if not num_gpus:
             fn = self._fn

@@ -164,7 +164,15 @@ class _Schedule:
             except BaseException as e:  # noqa: BLE001 - upstream failure propagates
                 f.set_exception(e)
                 return
-            ref = n.method.remote(*a, **kw)
+            # submit() runs as a Future done-callback, where concurrent.futures
+            # would log and swallow a synchronous failure (a missing method, a
+            # killed actor): route it into the node's future instead, so get()
+            # raises and the compiled DAG's in-flight slot is released
+            try:
+                ref = n.method.remote(*a, **kw)
+            except BaseException as e:  # noqa: BLE001
+                f.set_exception(e if isinstance(e, Exception) else RayError(repr(e)))
+                return
             ref._fut.add_done_callback(lambda r: f.set_exception(r.exception()) if r.exception() is not None
                                        else f.set_result(r.result()))
 

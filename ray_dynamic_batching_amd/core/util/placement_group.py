@@ -110,23 +110,41 @@ def placement_group(bundles: List[Dict[str, float]], strategy: str = "PACK", nam
         _groups[pg.id] = pg
     amounts = [float(b.get("GPU", 0)) for b in bundles]
 
+    def settle(state: str, result=None, exc: Optional[BaseException] = None) -> bool:
+        # state change + future resolution under _lock, and only while PENDING:
+        # remove_placement_group() may have run concurrently (it resolves the
+        # future itself and releases only what a CREATED group holds)
+        with _lock:
+            if pg.state != "PENDING":
+                return False
+            pg.state = state
+            if not pg._ready.done():
+                if exc is not None:
+                    pg._ready.set_exception(exc)
+                else:
+                    pg._ready.set_result(result)
+            return True
+
     def reserve():
         deadline = time.monotonic() + _timeout_s
         while pg.state == "PENDING":
             try:
                 allocs = ctx.allocator.allocate_bundles("pg:" + pg.id, amounts, strategy)
             except ValueError as e:
-                pg.state = "FAILED"
-                pg._ready.set_exception(e)
+                settle("FAILED", exc=e)
                 return
             if allocs is not None:
-                pg.bundle_gpus = [a.gpus for a in allocs]
-                pg.state = "CREATED"
-                pg._ready.set_result(pg)
+                with _lock:
+                    if pg.state == "PENDING":
+                        pg.bundle_gpus = [a.gpus for a in allocs]
+                committed = settle("CREATED", result=pg)
+                if not committed:
+                    # removed while allocate_bundles ran: give back what it just took
+                    for i in range(len(amounts)):
+                        ctx.allocator.release(f"pg:{pg.id}/{i}")
                 return
             if time.monotonic() > deadline:
-                pg.state = "FAILED"
-                pg._ready.set_exception(RuntimeError(
+                settle("FAILED", exc=RuntimeError(
                     f"placement group {bundles} ({strategy}) not satisfiable within {_timeout_s:.0f} s "
                     f"(allocator: {ctx.allocator.snapshot()})"))
                 return
@@ -143,6 +161,8 @@ def remove_placement_group(pg: PlacementGroup) -> None:
     with _lock:
         members = list(pg._members)
         prev, pg.state = pg.state, "REMOVED"
+        if not pg._ready.done():
+            pg._ready.set_exception(RuntimeError("placement group removed"))
     if _ctx is not None:
         for h in list(_ctx.owned):
             if h._actor_id in members:

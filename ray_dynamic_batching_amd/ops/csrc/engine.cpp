@@ -29,6 +29,8 @@
 #include <pybind11/stl.h>
 
 #include <algorithm>
+#include <array>
+#include <memory>
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
@@ -69,6 +71,7 @@ struct Session {
   std::vector<std::vector<hipGraphExec_t>> graphs;   // [bucket][slot]
   std::vector<std::vector<uintptr_t>> out_dev;       // [bucket][slot]
   std::vector<uintptr_t> in_dev;                     // [slot]
+  std::vector<void*> host_tbl, host_out;             // [slot] pinned gather table / output staging
   Ring ring;
   uint64_t peek_pos = 0;                             // next unread position
   // duty-cycle mode (Nexus): GPU time this session may use per cycle
@@ -76,17 +79,10 @@ struct Session {
   int64_t used_ns = 0;                               // charged in the current cycle
   uint64_t launched_cycle = UINT64_MAX;              // duty-cycle index of the last launch
   std::atomic<bool> active{true};                    // model loaded / unloaded by the planner
-  Session() = default;
-  Session(Session&& o) noexcept { *this = std::move(o); }
-  Session& operator=(Session&& o) noexcept {
-    queue = o.queue; max_batch = o.max_batch; max_wait_ns = o.max_wait_ns; buckets = std::move(o.buckets);
-    in_row_bytes = o.in_row_bytes; out_row_bytes = o.out_row_bytes; priority = o.priority; slo_ns = o.slo_ns;
-    drop_stale = o.drop_stale; est_ns = std::move(o.est_ns); graphs = std::move(o.graphs);
-    out_dev = std::move(o.out_dev); in_dev = std::move(o.in_dev); ring = o.ring; peek_pos = o.peek_pos;
-    duty_share_ns = o.duty_share_ns; used_ns = o.used_ns; launched_cycle = o.launched_cycle;
-    active.store(o.active.load());
-    return *this;
-  }
+  // live load / unload (planner re-placement): batches of this session between
+  // the launcher's pick and their completion; retire() waits for 0
+  std::atomic<int> inflight{0};
+  std::atomic<bool> retired{false};
 };
 
 enum Policy { POLICY_PRIORITY_EDF = 0, POLICY_DUTY_CYCLE = 1 };
@@ -168,8 +164,7 @@ class Engine {
     for (auto e : ev_copy_) hipEventDestroy(e);
     for (auto e : ev_start_) hipEventDestroy(e);
     for (auto e : ev_done_) hipEventDestroy(e);
-    for (auto p : host_ptrs_) hipHostFree(p);
-    for (auto p : host_out_) hipHostFree(p);
+    for (auto& sp : owned_) free_host(*sp);
     if (registered_) {
       std::lock_guard<std::mutex> lk(host_reg_mu());
       void* base = job_.request_region().first;
@@ -182,9 +177,14 @@ class Engine {
     for (auto st : compute_streams_) hipStreamDestroy(st);
   }
 
+  // Sessions may be added while the engine runs (planner load of a model at a
+  // batch boundary): a live-added session starts INACTIVE; the caller sets its
+  // inputs / graphs and then activates it.  A retired slot (retire_session) is
+  // reused; its old Session object stays allocated until the engine is destroyed
+  // (the launcher may still be reading its `active` flag), only its pinned
+  // buffers are freed at retirement.
   int add_session(uint32_t queue, int max_batch, double max_wait_s, std::vector<int> buckets,
                   int in_row_bytes, int out_row_bytes, int priority, double slo_ms, bool drop_stale) {
-    if (running_) throw std::runtime_error("add_session after start");
     if (queue >= job_.hdr()->n_queues) throw std::out_of_range("queue index");
     if (buckets.empty()) buckets.push_back(max_batch);
     std::sort(buckets.begin(), buckets.end());
@@ -192,7 +192,15 @@ class Engine {
     if (in_row_bytes % 16) throw std::invalid_argument("in_row_bytes must be a multiple of 16");
     Ring ring = job_.req_ring(queue);
     if ((uint32_t)in_row_bytes > ring.max_payload()) throw std::invalid_argument("request slot too small");
-    Session s;
+    std::lock_guard<std::mutex> api(api_mu_);
+    const int n = n_sess_.load();
+    for (int i = 0; i < n; ++i) {
+      Session* o = sess_ptr_[i].load();
+      if (o->retired.load() && o->queue == queue) throw std::invalid_argument("queue already has a retired session; reuse it");
+      if (!o->retired.load() && o->queue == queue) throw std::invalid_argument("queue already served by a session");
+    }
+    auto sp = std::make_unique<Session>();
+    Session& s = *sp;
     s.queue = queue;
     s.max_batch = max_batch;
     s.max_wait_ns = (int64_t)(max_wait_s * 1e9);
@@ -208,19 +216,96 @@ class Engine {
     s.in_dev.assign(depth_, 0);
     s.ring = ring;
     s.peek_pos = ring.h->tail.load();
-    sessions_.push_back(std::move(s));
-    const int sid = (int)sessions_.size() - 1;
+    s.active.store(!running_.load());
     // per-slot pinned gather tables and output staging
     for (int sl = 0; sl < depth_; ++sl) {
       void* p = nullptr;
       ENG_CHECK(hipHostMalloc(&p, sizeof(uint64_t) * max_batch, hipHostMallocDefault));
-      host_ptrs_.push_back(p);
+      s.host_tbl.push_back(p);
       void* o = nullptr;
       ENG_CHECK(hipHostMalloc(&o, (size_t)out_row_bytes * max_batch + 64, hipHostMallocDefault));
-      host_out_.push_back(o);
+      s.host_out.push_back(o);
     }
-    return sid;
+    if (n >= kMaxSessions) {
+      free_host(s);
+      throw std::runtime_error("engine: too many sessions");
+    }
+    sess_ptr_[n].store(sp.get(), std::memory_order_release);
+    owned_.push_back(std::move(sp));
+    n_sess_.store(n + 1, std::memory_order_release);
+    return n;
   }
+  // Re-arm a retired session for the same queue with new graphs (a model moved
+  // back onto this GPU): returns its sid, inactive until set_session_active.
+  int readd_session(uint32_t queue, int max_batch, double max_wait_s, std::vector<int> buckets, int in_row_bytes,
+                    int out_row_bytes, int priority, double slo_ms, bool drop_stale) {
+    int old = -1;
+    {
+      std::lock_guard<std::mutex> api(api_mu_);
+      for (int i = 0; i < n_sess_.load(); ++i)
+        if (sess_ptr_[i].load()->queue == queue && sess_ptr_[i].load()->retired.load()) old = i;
+    }
+    if (old < 0) return add_session(queue, max_batch, max_wait_s, buckets, in_row_bytes, out_row_bytes, priority,
+                                    slo_ms, drop_stale);
+    if (buckets.empty()) buckets.push_back(max_batch);
+    std::sort(buckets.begin(), buckets.end());
+    if (buckets.back() != max_batch) throw std::invalid_argument("largest bucket must equal max_batch");
+    auto sp = std::make_unique<Session>();
+    Session& s = *sp;
+    s.queue = queue;
+    s.max_batch = max_batch;
+    s.max_wait_ns = (int64_t)(max_wait_s * 1e9);
+    s.buckets = buckets;
+    s.in_row_bytes = in_row_bytes;
+    s.out_row_bytes = out_row_bytes;
+    s.priority = priority;
+    s.slo_ns = (int64_t)(slo_ms * 1e6);
+    s.drop_stale = drop_stale;
+    s.est_ns.assign(buckets.size(), 0.0);
+    s.graphs.assign(buckets.size(), std::vector<hipGraphExec_t>(depth_, nullptr));
+    s.out_dev.assign(buckets.size(), std::vector<uintptr_t>(depth_, 0));
+    s.in_dev.assign(depth_, 0);
+    s.ring = job_.req_ring(queue);
+    s.peek_pos = s.ring.h->tail.load();
+    s.active.store(false);
+    for (int sl = 0; sl < depth_; ++sl) {
+      void* p = nullptr;
+      ENG_CHECK(hipHostMalloc(&p, sizeof(uint64_t) * max_batch, hipHostMallocDefault));
+      s.host_tbl.push_back(p);
+      void* o = nullptr;
+      ENG_CHECK(hipHostMalloc(&o, (size_t)out_row_bytes * max_batch + 64, hipHostMallocDefault));
+      s.host_out.push_back(o);
+    }
+    std::lock_guard<std::mutex> api(api_mu_);
+    sess_ptr_[old].store(sp.get(), std::memory_order_release);   // the retired object stays owned
+    owned_.push_back(std::move(sp));
+    return old;
+  }
+  // Unload: stop picking the session, wait (bounded) until none of its batches
+  // is in flight, then drop its graph handles -- after this the caller may free
+  // the graphs, inputs and weights.  Requests still queued stay in the ring.
+  bool retire_session(int sid, double timeout_s) {
+    Session& s = sess(sid);
+    s.active.store(false, std::memory_order_seq_cst);
+    const int64_t end = now_ns() + (int64_t)(timeout_s * 1e9);
+    while (s.inflight.load(std::memory_order_seq_cst) != 0) {
+      if (now_ns() > end) {
+        s.active.store(true);   // could not drain: keep serving
+        return false;
+      }
+      std::this_thread::sleep_for(std::chrono::microseconds(100));
+    }
+    for (auto& row : s.graphs)
+      for (auto& g : row) g = nullptr;
+    for (auto& x : s.in_dev) x = 0;
+    s.retired.store(true);
+    free_host(s);
+    return true;
+  }
+  int session_inflight(int sid) { return sess(sid).inflight.load(); }
+  uint64_t session_pending(int sid) { return sess(sid).ring.depth(); }
+  bool session_retired(int sid) { return sess(sid).retired.load(); }
+  int num_sessions() const { return n_sess_.load(); }
   void set_input(int sid, int slot, uintptr_t dev_ptr) { sess(sid).in_dev.at(slot) = dev_ptr; }
   void set_graph(int sid, int bucket_idx, int slot, uintptr_t graph_exec, uintptr_t out_dev) {
     Session& s = sess(sid);
@@ -232,7 +317,17 @@ class Engine {
   // of GPU time (= occupancy x duty cycle); budgets reset at the cycle boundary.
   void set_duty_share(int sid, double ms) { sess(sid).duty_share_ns = (int64_t)(ms * 1e6); }
   void set_duty_cycle(double ms) { duty_cycle_ns_.store((int64_t)(ms * 1e6)); }
-  void set_session_active(int sid, bool on) { sess(sid).active.store(on); }
+  void set_session_active(int sid, bool on) {
+    Session& s = sess(sid);
+    if (on) {
+      if (s.retired.load()) throw std::runtime_error("session is retired (readd_session first)");
+      for (size_t b = 0; b < s.buckets.size(); ++b)
+        for (int sl = 0; sl < depth_; ++sl)
+          if (!s.graphs[b][sl] || !s.in_dev[sl])
+            throw std::runtime_error("engine: activating a session with a missing graph/input");
+    }
+    s.active.store(on, std::memory_order_seq_cst);
+  }
   int compute_streams() const { return (int)compute_streams_.size(); }
   void set_max_batch(int sid, int b) {
     Session& s = sess(sid);
@@ -243,11 +338,14 @@ class Engine {
 
   void start() {
     if (running_) return;
-    for (size_t i = 0; i < sessions_.size(); ++i)
-      for (size_t b = 0; b < sessions_[i].buckets.size(); ++b)
+    for (int i = 0; i < n_sess_.load(); ++i) {
+      Session& s = *sess_ptr_[i].load();
+      if (s.retired.load()) continue;
+      for (size_t b = 0; b < s.buckets.size(); ++b)
         for (int sl = 0; sl < depth_; ++sl)
-          if (!sessions_[i].graphs[b][sl] || !sessions_[i].in_dev[sl])
+          if (!s.graphs[b][sl] || !s.in_dev[sl])
             throw std::runtime_error("engine: missing graph/input for a (session, bucket, slot)");
+    }
     running_ = true;
     ReplicaState* rs = job_.replica(replica_);
     rs->gpu.store(device_);
@@ -260,7 +358,7 @@ class Engine {
   void stop() {
     if (!running_) return;
     running_ = false;
-    for (auto& s : sessions_) s.ring.ring_bell();
+    for (int i = 0; i < n_sess_.load(); ++i) sess_ptr_[i].load()->ring.ring_bell();
     cv_.notify_all();
     if (launcher_.joinable()) launcher_.join();
     {
@@ -291,8 +389,14 @@ class Engine {
 
  private:
   Session& sess(int sid) {
-    if (sid < 0 || sid >= (int)sessions_.size()) throw std::out_of_range("session id");
-    return sessions_[sid];
+    if (sid < 0 || sid >= n_sess_.load(std::memory_order_acquire)) throw std::out_of_range("session id");
+    return *sess_ptr_[sid].load(std::memory_order_acquire);
+  }
+  static void free_host(Session& s) {
+    for (auto p : s.host_tbl) hipHostFree(p);
+    for (auto p : s.host_out) hipHostFree(p);
+    s.host_tbl.clear();
+    s.host_out.clear();
   }
   int bucket_for(const Session& s, int n) const {
     for (size_t i = 0; i < s.buckets.size(); ++i)
@@ -311,11 +415,13 @@ class Engine {
     int best = -1;
     int best_pri = INT32_MIN;
     int64_t best_dl = INT64_MAX;
-    for (size_t i = 0; i < sessions_.size(); ++i) {
-      if (!sessions_[i].active.load(std::memory_order_relaxed)) continue;
-      const int64_t dl = head_deadline(sessions_[i]);
+    const int ns = n_sess_.load(std::memory_order_acquire);
+    for (int i = 0; i < ns; ++i) {
+      Session& si = *sess_ptr_[i].load(std::memory_order_acquire);
+      if (!si.active.load(std::memory_order_acquire)) continue;
+      const int64_t dl = head_deadline(si);
       if (dl == INT64_MAX) continue;
-      const int pri = sessions_[i].priority;
+      const int pri = si.priority;
       if (pri > best_pri || (pri == best_pri && dl < best_dl)) {
         best = (int)i;
         best_pri = pri;
@@ -336,14 +442,15 @@ class Engine {
     if (cyc > 0 && now - cycle_start_ns_ >= cyc) {
       cycle_start_ns_ = now - cycle_start_ns_ < 2 * cyc ? cycle_start_ns_ + cyc : now;
       ++cycle_idx_;
-      for (auto& s : sessions_) s.used_ns = 0;
+      for (int i = 0; i < n_sess_.load(std::memory_order_acquire); ++i) sess_ptr_[i].load()->used_ns = 0;
     }
-    const size_t n = sessions_.size();
+    const size_t n = (size_t)n_sess_.load(std::memory_order_acquire);
+    if (n == 0) return -1;
     bool waiting = false;
     for (size_t k = 0; k < n; ++k) {
       const size_t i = (rr_next_ + k) % n;
-      Session& s = sessions_[i];
-      if (!s.active.load(std::memory_order_relaxed) || !s.ring.peek(s.peek_pos)) continue;
+      Session& s = *sess_ptr_[i].load(std::memory_order_acquire);
+      if (!s.active.load(std::memory_order_acquire) || !s.ring.peek(s.peek_pos)) continue;
       if (cyc > 0 && s.duty_share_ns > 0 &&
           (s.launched_cycle == cycle_idx_ || s.used_ns >= s.duty_share_ns)) {
         waiting = true;
@@ -363,8 +470,8 @@ class Engine {
       int best = -1;
       double best_key = 1e300;
       for (size_t i = 0; i < n; ++i) {
-        Session& s = sessions_[i];
-        if (!s.active.load(std::memory_order_relaxed)) continue;
+        Session& s = *sess_ptr_[i].load(std::memory_order_acquire);
+        if (!s.active.load(std::memory_order_acquire)) continue;
         SlotHeader* h = s.ring.peek(s.peek_pos);
         if (!h) continue;
         const uint64_t depth = s.ring.h->head.load(std::memory_order_relaxed) - s.peek_pos;
@@ -444,18 +551,33 @@ class Engine {
         // wait for any work
         int sid = pick_session();
         if (sid < 0) {
-          Session& s0 = sessions_[0];
           for (int i = 0; i < 4000 && sid < 0; ++i) {  // short spin
             cpu_relax();
             if ((i & 63) == 63) sid = pick_session();
           }
           if (sid < 0) {
-            s0.ring.wait_for(s0.peek_pos, sessions_.size() == 1 ? 20000000LL : 200000LL, 0);
+            // sleep on the doorbell of the only active session, else poll briefly
+            Session* only = nullptr;
+            int n_active = 0;
+            for (int i = 0; i < n_sess_.load(std::memory_order_acquire); ++i) {
+              Session* c = sess_ptr_[i].load(std::memory_order_acquire);
+              if (c->active.load(std::memory_order_acquire)) { only = c; ++n_active; }
+            }
+            if (n_active == 1) only->ring.wait_for(only->peek_pos, 20000000LL, 0);
+            else if (n_active > 1) only->ring.wait_for(only->peek_pos, 200000LL, 0);
+            else std::this_thread::sleep_for(std::chrono::microseconds(200));
             continue;
           }
         }
+        Session& s = *sess_ptr_[sid].load(std::memory_order_acquire);
+        // Dekker pair with retire_session(): count the batch first, then re-check
+        // `active` (both seq_cst) -- either retire sees the count or we see the flag
+        s.inflight.fetch_add(1, std::memory_order_seq_cst);
+        if (!s.active.load(std::memory_order_seq_cst)) {
+          s.inflight.fetch_sub(1, std::memory_order_seq_cst);
+          continue;
+        }
         job_.replica(replica_)->heartbeat_ns.store(now_ns(), std::memory_order_relaxed);
-        Session& s = sessions_[sid];
         roctxRangePushA("rdb:form_batch");
         InFlight f;
         f.session = sid;
@@ -463,7 +585,7 @@ class Engine {
         f.pos_begin = s.peek_pos;
         f.t_form_start = now_ns();
         const int64_t flush_at = f.t_form_start + s.max_wait_ns;
-        uint64_t* tbl = reinterpret_cast<uint64_t*>(host_ptrs_[sid * depth_ + slot]);
+        uint64_t* tbl = reinterpret_cast<uint64_t*>(s.host_tbl[slot]);
         int n = 0;
         while (n < s.max_batch) {
           SlotHeader* h = s.ring.peek(s.peek_pos);
@@ -530,7 +652,7 @@ class Engine {
           ENG_CHECK(hipStreamWaitEvent(cs, ev_copy_[slot], 0));
           ENG_CHECK(hipEventRecord(ev_start_[slot], cs));
           ENG_CHECK(hipGraphLaunch(s.graphs[bi][slot], cs));
-          ENG_CHECK(hipMemcpyAsync(host_out_[sid * depth_ + slot],
+          ENG_CHECK(hipMemcpyAsync(s.host_out[slot],
                                    reinterpret_cast<void*>(s.out_dev[bi][slot]),
                                    (size_t)n * s.out_row_bytes, hipMemcpyDeviceToHost, cs));
           ENG_CHECK(hipEventRecord(ev_done_[slot], cs));
@@ -568,7 +690,7 @@ class Engine {
           f = std::move(inflight_.front());
           inflight_.pop_front();
         }
-        Session& s = sessions_[f.session];
+        Session& s = *sess_ptr_[f.session].load(std::memory_order_acquire);
         const int n = (int)f.req_pos.size();
         if (f.gpu) {
           // low-latency wait: spin on the event, yielding
@@ -588,7 +710,7 @@ class Engine {
             double& est = s.est_ns[f.bucket_idx];
             est = est == 0.0 ? ms * 1e6 : 0.9 * est + 0.1 * ms * 1e6;
           }
-          const char* out = reinterpret_cast<const char*>(host_out_[f.session * depth_ + f.slot]);
+          const char* out = reinterpret_cast<const char*>(s.host_out[f.slot]);
           const int64_t t_done = now_ns();
           QueueState* qs = job_.queue(s.queue);
           for (int i = 0; i < n; ++i) {
@@ -616,6 +738,7 @@ class Engine {
           std::lock_guard<std::mutex> lk(mu_);
           slot_busy_[f.slot] = false;
         }
+        s.inflight.fetch_sub(1, std::memory_order_seq_cst);
         cv_.notify_all();
       }
     } catch (const std::exception& e) {
@@ -645,8 +768,11 @@ class Engine {
   std::atomic<uint64_t> backfills_{0};
   size_t rr_next_ = 0;
   std::vector<hipEvent_t> ev_copy_, ev_start_, ev_done_;
-  std::vector<void*> host_ptrs_, host_out_;
-  std::vector<Session> sessions_;
+  static constexpr int kMaxSessions = 64;
+  std::array<std::atomic<Session*>, kMaxSessions> sess_ptr_{};
+  std::atomic<int> n_sess_{0};
+  std::vector<std::unique_ptr<Session>> owned_;   // every Session ever created (api_mu_)
+  std::mutex api_mu_;
   std::vector<bool> slot_busy_;
   std::deque<InFlight> inflight_;
   std::mutex mu_;
@@ -676,6 +802,15 @@ void register_engine(py::module_& m) {
       .def("set_duty_share", &Engine::set_duty_share)
       .def("set_duty_cycle", &Engine::set_duty_cycle)
       .def("set_session_active", &Engine::set_session_active)
+      .def("readd_session", &Engine::readd_session, py::arg("queue"), py::arg("max_batch"), py::arg("max_wait_s"),
+           py::arg("buckets"), py::arg("in_row_bytes"), py::arg("out_row_bytes"), py::arg("priority") = 0,
+           py::arg("slo_ms") = 0.0, py::arg("drop_stale") = false)
+      .def("retire_session", &Engine::retire_session, py::arg("sid"), py::arg("timeout_s") = 10.0,
+           py::call_guard<py::gil_scoped_release>())
+      .def("session_inflight", &Engine::session_inflight)
+      .def("session_pending", &Engine::session_pending)
+      .def("session_retired", &Engine::session_retired)
+      .def("num_sessions", &Engine::num_sessions)
       .def("compute_streams", &Engine::compute_streams)
       .def("set_max_batch", &Engine::set_max_batch)
       .def("set_max_wait", &Engine::set_max_wait)

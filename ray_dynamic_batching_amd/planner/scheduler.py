@@ -59,6 +59,16 @@ class DutyCycleExecutor(threading.Thread):
         self.stop_flag = threading.Event()
         self.stats = dict(processed_batches=0, total_requests=0, dropped=0, processing_ms=[])
         self.consumers: Dict[str, Any] = {}
+        self.footprint: Dict[str, int] = {}
+        self.loads = 0
+        self.unloads = 0
+        self.rerouted = 0
+
+    def resident_bytes(self) -> int:
+        return sum(self.footprint.get(m, 0) for m in self.models)
+
+    def estimate_bytes(self, m: str) -> int:
+        return self.footprint.get(m) or self.sched.footprint_estimate(m)
 
     def update(self, node: Optional[Node]) -> None:
         with self._lock:
@@ -72,11 +82,17 @@ class DutyCycleExecutor(threading.Thread):
         new_models = set(new.models())
         for m in list(self.models):
             if m not in new_models:           # unload (fork: .cpu(); del; empty_cache)
+                cons = self.consumers.pop(m, None)
                 del self.models[m]
-                self.consumers.pop(m, None)
+                self.unloads += 1
+                if cons is not None:
+                    # queued requests follow the model to a GPU that serves it
+                    self.rerouted += self.sched._reroute_queue(self.sched.queue_id(self.gpu, m), m, cons)
         for m in new_models:
             if m not in self.models:          # load
                 self.models[m] = self.sched.model_factories[m]()
+                self.footprint[m] = model_footprint_bytes(self.models[m])
+                self.loads += 1
                 q = self.sched.queue_id(self.gpu, m)
                 self.consumers[m] = rjob.Consumer(self.sched.job, [q])
         self.node = new
@@ -144,52 +160,173 @@ class DutyCycleExecutor(threading.Thread):
         self.stats["processing_ms"] = (self.stats["processing_ms"] + [dt])[-100:]
 
 
-class EngineExecutor:
-    """GPU worker on the native replica engine (ops/csrc/engine.cpp) with the
-    Nexus duty-cycle policy in C++: every model of the scheduler is resident
-    and graph-captured on this GPU (288 GB HBM makes "load" an activation
-    flip instead of a weight copy + re-capture); a plan node activates its
-    sessions, sets their batch sizes and GPU-time shares (duty x occupancy) and
-    the engine enforces them per cycle, dropping stale requests natively."""
-
-    def __init__(self, sched: "SLOScheduler", gpu: int, device: int, max_batch: Dict[str, int]):
+def model_footprint_bytes(model: Any) -> int:
+    """Resident bytes of a model's parameters and buffers (torch modules, or
+    objects exposing ``parameters()`` / ``footprint_bytes()``); 0 if unknown."""
+    fb = getattr(model, "footprint_bytes", None)
+    if callable(fb):
+        return int(fb())
+    total = 0
+    seen = set()
+    for attr in ("parameters", "buffers"):
+        fn = getattr(model, attr, None)
+        if not callable(fn):
+            continue
+        try:
+            for t in fn():
+                if id(t) not in seen:
+                    seen.add(id(t))
+                    total += t.numel() * t.element_size()
+        except TypeError:
+            pass
+    if total == 0 and hasattr(model, "__dict__"):
         import torch
 
-        from ..runtime.engine import EngineRunner, SessionSpec
+        for v in vars(model).values():
+            if isinstance(v, torch.Tensor) and id(v) not in seen:
+                seen.add(id(v))
+                total += v.numel() * v.element_size()
+    return total
+
+
+class PlanRejected(RuntimeError):
+    """A plan whose per-GPU resident model set exceeds the GPU's HBM budget."""
+
+
+class EngineExecutor:
+    """GPU worker on the native replica engine (ops/csrc/engine.cpp) with the
+    Nexus duty-cycle policy in C++.  Models are loaded and unloaded as plans
+    move them (the fork's ``_check_for_updates``, 293-project/src/scheduler.py:
+    483-523: ``.to(device)`` on load, ``.cpu(); del; empty_cache`` on unload):
+
+    * arriving model: weights created on this GPU, graphs captured into private
+      pools BESIDE the sessions that keep serving, session registered inactive
+      (``prepare``), activated once the router sends its queue traffic
+      (``update``);
+    * leaving model: its queue is already inactive in the router, so the engine
+      drains what is queued, retires the session at a batch boundary (no batch
+      in flight), drops graphs + weights and empties the cache: the HBM really
+      returns (``resident_bytes`` / ``torch.cuda.memory_allocated`` drop).
+      Requests that reached the queue after the drain are re-routed to a GPU
+      that serves the model.
+
+    Every load records its measured footprint (allocated bytes across weights +
+    capture) and capture time; the scheduler refuses plans whose per-GPU
+    resident set would exceed ``hbm_budget_bytes``."""
+
+    def __init__(self, sched: "SLOScheduler", gpu: int, device: int, max_batch: Dict[str, int],
+                 compute_streams: int = 1):
+        import torch
+
+        from ..runtime.engine import EngineRunner
 
         self.sched = sched
         self.gpu = gpu
+        self.device = device
         self.node: Optional[Node] = None
-        with torch.cuda.device(device):
-            self.models = {m: sched.model_factories[m](device=f"cuda:{device}") for m in sched.models}
-            specs = [SessionSpec(model=self.models[m], queue=sched.queue_id(gpu, m), max_batch=max_batch[m],
-                                 max_wait_s=0.0, slo_ms=float(sched.slos[m]), drop_stale=sched.drop_stale, name=m)
-                     for m in sched.models]
-            self.runner = EngineRunner(sched.job_name, gpu, specs, pipeline_depth=2, device=device,
-                                       policy=EngineRunner.POLICY_DUTY_CYCLE).build()
         self.max_batch = dict(max_batch)
-        for i in range(len(specs)):
-            self.runner.set_active(i, False)
+        self.models: Dict[str, Any] = {}
+        self.index: Dict[str, int] = {}            # model -> EngineRunner.sessions index (resident)
+        self.footprint: Dict[str, int] = {}        # model -> measured resident bytes
+        self.capture_s: Dict[str, float] = {}      # model -> last load + capture time
+        self.loads = 0
+        self.unloads = 0
+        self.rerouted = 0
+        with torch.cuda.device(device):
+            self.runner = EngineRunner(sched.job_name, gpu, [], pipeline_depth=2, device=device,
+                                       policy=EngineRunner.POLICY_DUTY_CYCLE, compute_streams=compute_streams)
+            self.runner.tune_in_context = False
+            self.runner.pools = [torch.cuda.graph_pool_handle() for _ in range(self.runner.compute_streams)]
         self.runner.start()
 
+    # ------------------------------------------------------------ memory
+    def resident_bytes(self) -> int:
+        return sum(self.footprint.get(m, 0) for m in self.index)
+
+    def estimate_bytes(self, m: str) -> int:
+        return self.footprint.get(m) or self.sched.footprint_estimate(m)
+
+    # ------------------------------------------------------------ load / unload
+    def load(self, m: str) -> None:
+        """Load + capture ``m`` (inactive until ``update`` activates it)."""
+        import torch
+
+        from ..runtime.engine import SessionSpec
+
+        if m in self.index:
+            return
+        t0 = time.perf_counter()
+        with torch.cuda.device(self.device):
+            torch.cuda.synchronize(self.device)
+            before = torch.cuda.memory_allocated(self.device)
+            model = self.sched.model_factories[m](device=f"cuda:{self.device}")
+            spec = SessionSpec(model=model, queue=self.sched.queue_id(self.gpu, m), max_batch=self.max_batch[m],
+                               max_wait_s=0.0, slo_ms=float(self.sched.slos[m]), drop_stale=self.sched.drop_stale,
+                               name=m)
+            idx = self.runner.add_session(spec, activate=False)
+            torch.cuda.synchronize(self.device)
+            self.footprint[m] = max(1, torch.cuda.memory_allocated(self.device) - before)
+        self.models[m] = model
+        self.index[m] = idx
+        self.capture_s[m] = time.perf_counter() - t0
+        self.loads += 1
+
+    def unload(self, m: str, drain_timeout_s: float = 10.0) -> bool:
+        """Drain, retire at a batch boundary, free.  False if it could not drain."""
+        if m not in self.index:
+            return True
+        idx = self.index[m]
+        sid = self.runner.sessions[idx].sid
+        eng = self.runner.engine
+        t_end = time.monotonic() + drain_timeout_s
+        while time.monotonic() < t_end and (eng.session_pending(sid) > 0 or eng.session_inflight(sid) > 0):
+            time.sleep(0.002)
+        if not self.runner.retire_session(idx, max(0.1, t_end - time.monotonic())):
+            return False
+        self.models.pop(m, None)
+        del self.index[m]
+        self.unloads += 1
+        # requests routed here after the drain: hand them to a GPU serving m
+        self.rerouted += self.sched._reroute_queue(self.sched.queue_id(self.gpu, m), m)
+        return True
+
+    def prepare(self, node: Optional[Node]) -> None:
+        """Phase 1 of a plan change (before the router's queues flip): load the
+        models arriving on this GPU."""
+        for m in (node.models() if node else []):
+            if m not in self.index:
+                self.load(m)
+
     def update(self, node: Optional[Node]) -> None:
+        """Phase 2 (after the queues flipped): activate the planned sessions with
+        their batch sizes and GPU-time shares, unload the models that left."""
         self.node = node
-        shares = []
-        for i, m in enumerate(self.sched.models):
-            sess = [(s, occ) for s, occ in (node.sessions if node else []) if s.model_name == m]
-            on = bool(sess)
-            if on:
-                b = max(1, min(self.max_batch[m], max(s.batch_size for s, _ in sess)))
-                self.runner.engine.set_max_batch(self.runner.sessions[i].sid, b)
-                shares.append(node.duty_cycle * sum(occ for _, occ in sess))
-            else:
-                shares.append(0.0)
-            self.runner.set_active(i, on)
-        self.runner.set_duty_cycle(node.duty_cycle if node else 0.0, shares)
+        planned = set(node.models()) if node else set()
+        for m in planned:
+            if m not in self.index:
+                self.load(m)
+        shares = {}
+        for m in planned:
+            sess = [(s, occ) for s, occ in node.sessions if s.model_name == m]
+            spec = self.runner.sessions[self.index[m]]
+            b = max(1, min(self.max_batch[m], max(s.batch_size for s, _ in sess)))
+            self.runner.engine.set_max_batch(spec.sid, b)
+            shares[m] = node.duty_cycle * sum(occ for _, occ in sess)
+            self.runner.engine.set_duty_share(spec.sid, shares[m])
+        self.runner.engine.set_duty_cycle(node.duty_cycle if node else 0.0)
+        for m in planned:
+            self.runner.engine.set_session_active(self.runner.sessions[self.index[m]].sid, True)
+        for m in list(self.index):
+            if m not in planned:
+                self.unload(m)
 
     @property
     def stats(self) -> Dict[str, Any]:
-        return self.runner.stats()
+        st = dict(self.runner.stats())
+        st.update(resident_models=sorted(self.index), resident_bytes=self.resident_bytes(),
+                  loads=self.loads, unloads=self.unloads, rerouted=self.rerouted,
+                  capture_s=dict(self.capture_s))
+        return st
 
     def stop(self) -> None:
         self.runner.stop()
@@ -202,13 +339,26 @@ class SLOScheduler:
                  compat: bool = False, slo_divisor: float = 1.0, drop_stale: bool = True,
                  gpu_mem_gb: Optional[float] = None, queue_capacity: int = 2048, job_name: Optional[str] = None,
                  executor: str = "python", devices: Optional[List[int]] = None,
-                 max_batch: Optional[Dict[str, int]] = None, plan_path: Optional[str] = None):
+                 max_batch: Optional[Dict[str, int]] = None, plan_path: Optional[str] = None,
+                 hbm_budget_gb: Optional[float] = None, model_footprint_gb: Optional[Dict[str, float]] = None,
+                 compute_streams: int = 1):
         """``executor``: "python" (DutyCycleExecutor threads; CPU / arbitrary torch
         models) or "engine" (native GPU engines, one per entry of ``devices``;
         ``max_batch`` = largest batch captured per model).  ``plan_path``: every
         applied plan is checkpointed there, and a plan found there at start-up
-        is restored (resume after a restart)."""
+        is restored (resume after a restart).  ``hbm_budget_gb``: per-GPU bytes
+        the resident models may take (default: the node agent's per-GPU HBM
+        budget, 288 GB on MI355X); a plan whose per-GPU resident set -- measured
+        footprints of loaded models, else ``model_footprint_gb`` estimates, else
+        the parameter bytes of a probe instance -- exceeds it is refused and the
+        current plan stays (``rejected_plans``); the fork's planner caps the same
+        way at packing time (293-project/src/nexus.py:223-227)."""
         self.plan_path = plan_path
+        from ..runtime.resources import MI355X_HBM_BYTES as DEFAULT_HBM_BYTES
+
+        self.hbm_budget_bytes = int((hbm_budget_gb * 1e9) if hbm_budget_gb is not None else DEFAULT_HBM_BYTES)
+        self._footprint_hint = {m: int(v * 1e9) for m, v in (model_footprint_gb or {}).items()}
+        self.rejected_plans: List[Dict[str, Any]] = []
         self.profiles = profiles
         self.slos = dict(slos_ms)
         self.model_factories = model_factories
@@ -219,6 +369,8 @@ class SLOScheduler:
         self.threshold = rate_change_threshold
         self.slo_divisor = slo_divisor
         self.drop_stale = drop_stale
+        if gpu_mem_gb is None and hbm_budget_gb is not None:
+            gpu_mem_gb = hbm_budget_gb      # the planner packs against the same per-GPU cap
         self.planner = SquishyPlanner(profiles, gpu_mem_gb=gpu_mem_gb, compat=compat)
         self.trackers = {m: RateTracker(rate_window_s) for m in self.models}
         self.sessions: Dict[str, Session] = {}
@@ -243,7 +395,8 @@ class SLOScheduler:
         if executor == "engine":
             devices = list(devices if devices is not None else range(num_gpus))
             mb = {m: (max_batch or {}).get(m, 32) for m in self.models}
-            self.executors = [EngineExecutor(self, g, devices[g], mb) for g in range(num_gpus)]
+            self.executors = [EngineExecutor(self, g, devices[g], mb, compute_streams=compute_streams)
+                              for g in range(num_gpus)]
         else:
             self.executors = [DutyCycleExecutor(self, g) for g in range(num_gpus)]
             for e in self.executors:
@@ -359,9 +512,50 @@ class SLOScheduler:
                 if prev > 0 and abs(diff) / prev > thr:
                     update[m] = r
         if update:
-            self.replan(update)
+            try:
+                self.replan(update)
+            except PlanRejected:
+                return False        # the current plan stays (rejected_plans records why)
             return True
         return False
+
+    def footprint_estimate(self, m: str) -> int:
+        """Resident bytes of model ``m`` on one GPU: measured by an executor that
+        loaded it, else the user's hint, else the profile's peak memory (the
+        fork's profiler records torch.cuda.max_memory_allocated per batch,
+        weights included: 293-project/profiling/ModelProfiler.py:114-178)."""
+        for e in self.executors:
+            fp = getattr(e, "footprint", {}).get(m)
+            if fp:
+                return fp
+        if m in self._footprint_hint:
+            return self._footprint_hint[m]
+        rows = self.profiles.get(m, {})
+        return int(max((r.get("peak_memory_mb", 0.0) for r in rows.values()), default=0.0) * 2**20)
+
+    def over_budget(self, placed: List[Optional[Node]]) -> Dict[int, Dict[str, Any]]:
+        """GPUs whose planned resident set exceeds the HBM budget."""
+        out = {}
+        for g, node in enumerate(placed):
+            if node is None:
+                continue
+            need = {m: self.footprint_estimate(m) for m in set(node.models())}
+            if sum(need.values()) > self.hbm_budget_bytes:
+                out[g] = dict(models=need, total=sum(need.values()), budget=self.hbm_budget_bytes)
+        return out
+
+    def _reroute_queue(self, q: int, m: str, consumer: Any = None) -> int:
+        """Move the requests left in queue ``q`` (model ``m`` just left that GPU)
+        to the least-loaded GPU queue that serves ``m`` (native
+        ``Consumer.forward``: headers kept, completions reach the original
+        client); held in the ring if no GPU serves ``m`` right now."""
+        targets = [self.queue_id(g, m) for g in range(self.num_gpus)
+                   if self.queue_id(g, m) != q and self.slots[g] is not None and m in self.slots[g].models()]
+        if not targets:
+            return 0
+        to = min(targets, key=self.job.queue_depth)
+        cons = consumer if consumer is not None else rjob.Consumer(self.job, [q])
+        return int(cons.forward(to))
 
     def replan(self, update: Dict[str, float]) -> Plan:
         plan = self._replan_locked(update)
@@ -392,6 +586,12 @@ class SLOScheduler:
                 self.unplaced_nodes = 0
             placed = assign_to_slots(self.slots, nodes)[: self.num_gpus]
             placed += [None] * (self.num_gpus - len(placed))
+            over = self.over_budget(placed)
+            if over:
+                self.rejected_plans.append(dict(time=time.time(), update=dict(update), over=over))
+                logger.warning("plan refused: resident models exceed the HBM budget on GPU(s) %s", over)
+                raise PlanRejected(f"plan exceeds the per-GPU HBM budget ({self.hbm_budget_bytes / 1e9:.1f} GB): "
+                                   f"{over}")
             transfers = total_transfers(self.slots, placed)
             self.sessions = {s.model_name: s for s in sessions}
             self.slots = placed
@@ -404,6 +604,14 @@ class SLOScheduler:
             return plan
 
     def _apply(self, placed: List[Optional[Node]]) -> None:
+        # phase 1: models arriving on a GPU are loaded + captured (inactive)
+        # while every session keeps serving; only then does the router see their
+        # queues, so no request waits for a capture
+        for g, node in enumerate(placed):
+            prep = getattr(self.executors[g], "prepare", None)
+            if prep is not None:
+                prep(node)
+        # phase 2: flip the router's queues, then activate / drain + unload
         for g, node in enumerate(placed):
             models = set(node.models()) if node else set()
             for m in self.models:
@@ -474,6 +682,8 @@ class SLOScheduler:
                 continue
             slots.append(Node([(mk(s), float(s["occupancy"])) for s in n["sessions"]], float(n["duty_cycle"]),
                               n.get("gpu_type", "MI355X"), float(n.get("gpu_mem", 288.0))))
+        if self.over_budget(slots):
+            return False
         with self.lock:
             self.sessions = {m: mk(d) for m, d in state["sessions"].items()}
             self.slots = slots

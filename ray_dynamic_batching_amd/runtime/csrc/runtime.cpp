@@ -644,6 +644,46 @@ class Consumer {
                               std::get<4>(t), std::get<5>(t), py::bytes(std::get<6>(t))));
     return l;
   }
+  // Move up to max_n queued requests of the served queues into queue `to`
+  // (planner unload: requests that reached a GPU's queue after its model was
+  // drained go to a GPU that still serves the model).  Every header field is
+  // preserved, so the completion reaches the ORIGINAL client under its request
+  // id; the per-queue submitted counters move with the request.  Stops early
+  // when the target ring is full.  Returns the number moved.
+  size_t forward(uint32_t to, size_t max_n) {
+    if (to >= job_.hdr()->n_queues) throw std::out_of_range("queue index");
+    py::gil_scoped_release nogil;
+    Ring dst = job_.req_ring(to);
+    size_t moved = 0;
+    for (size_t k = 0; k < rings_.size() && moved < max_n; ++k) {
+      Ring& r = rings_[k];
+      if (queues_[k] == to) continue;
+      while (moved < max_n) {
+        SlotHeader* s = r.peek(pos_[k]);
+        if (!s || s->len > dst.max_payload()) break;
+        uint64_t pos;
+        SlotHeader* d = dst.reserve(&pos);
+        if (!d) break;
+        d->req_id = s->req_id;
+        d->t_submit_ns = s->t_submit_ns;
+        d->deadline_ns = s->deadline_ns;
+        d->len = s->len;
+        d->kind = s->kind;
+        d->client = s->client;
+        d->queue = to;
+        d->status = 0;
+        d->t_aux_ns = 0;
+        if (s->len) memcpy(dst.payload(d), r.payload(s), s->len);
+        job_.queue(to)->submitted.fetch_add(1, std::memory_order_relaxed);
+        job_.queue(queues_[k])->submitted.fetch_sub(1, std::memory_order_relaxed);
+        dst.publish(d, pos);
+        ++pos_[k];
+        ++moved;
+      }
+      r.commit(pos_[k]);
+    }
+    return moved;
+  }
   // Publish a completion. Returns false if the result does not fit.
   bool complete(uint16_t client, uint64_t req_id, uint32_t queue, uint32_t status,
                 int64_t t_submit_ns, py::bytes payload, uint16_t kind) {
@@ -836,6 +876,7 @@ PYBIND11_MODULE(_rdb_runtime, m) {
       .def("pop", &Consumer::pop, py::arg("max_n") = 64, py::arg("timeout_ns") = 10000000)
       .def("complete", &Consumer::complete, py::arg("client"), py::arg("req_id"), py::arg("queue"),
            py::arg("status"), py::arg("t_submit_ns"), py::arg("payload"), py::arg("kind") = 0)
-      .def("record_batch", &Consumer::record_batch);
+      .def("record_batch", &Consumer::record_batch)
+      .def("forward", &Consumer::forward, py::arg("to"), py::arg("max_n") = 1 << 20);
   rdb::register_node_agent(m);
 }

@@ -40,6 +40,8 @@ class SessionSpec:
     name: str = ""
     # filled by the runner
     sid: int = -1
+    capture_s: float = 0.0
+    pools: list = field(default_factory=list)
     graphs: list = field(default_factory=list)
     inputs: list = field(default_factory=list)
     outputs: list = field(default_factory=list)
@@ -92,82 +94,10 @@ class EngineRunner:
         return n * torch.empty((), dtype=dtype).element_size()
 
     def build(self) -> "EngineRunner":
-        import os
-
         t0 = time.perf_counter()
-        dev = torch.device("cuda", self.device)
         self.pools = [torch.cuda.graph_pool_handle() for _ in range(self.compute_streams)]
         for s in self.sessions:
-            m = s.model
-            if getattr(m, "fold_ln_auto", False):
-                # deferred LayerNorm (models/bert.py) shortens ONE batch's forward
-                # (-3.5 % at bs32) but its heavier GEMM epilogues cost throughput
-                # when batches overlap on several compute streams, where the
-                # LayerNorm kernels already hide under the other stream's GEMMs
-                # (profiles/bert_fold_ln_ab.json)
-                m.fold_ln = m.auto_fold_ln(self.compute_streams) if hasattr(m, "auto_fold_ln") \
-                    else self.compute_streams == 1
-                if os.environ.get("RDB_FOLD_LN") in ("0", "1"):      # A/B override
-                    m.fold_ln = os.environ["RDB_FOLD_LN"] == "1"
-            if hasattr(m, "refresh_folded_weights"):
-                m.refresh_folded_weights()   # graphs capture weights derived from the CURRENT ones
-            buckets = sorted(set(s.buckets or default_buckets(s.max_batch)))
-            if buckets[-1] != s.max_batch:
-                buckets.append(s.max_batch)
-            s.buckets = buckets
-            in_bytes = self._bytes(m.input_shape, m.input_dtype)
-            out_bytes = self._bytes(m.output_shape, m.output_dtype)
-            s.sid = self.engine.add_session(s.queue, s.max_batch, s.max_wait_s, buckets, in_bytes, out_bytes,
-                                            s.priority, s.slo_ms, s.drop_stale)
-            s.inputs = []
-            for slot in range(self.depth):
-                x = torch.zeros((s.max_batch,) + tuple(m.input_shape), dtype=m.input_dtype, device=dev)
-                if hasattr(m, "example_input") and m.input_dtype in (torch.int32, torch.int64):
-                    x.copy_(m.example_input(s.max_batch, seed=slot, device=dev))
-                s.inputs.append(x)
-                self.engine.set_input(s.sid, slot, x.data_ptr())
-            # warm up every bucket eagerly on a side stream (lazy init, caches,
-            # per-shape kernel autotuning)
-            side = torch.cuda.Stream(device=dev)
-            side.wait_stream(torch.cuda.current_stream())
-            with torch.cuda.stream(side):
-                for b in buckets:
-                    for _ in range(self.warmup_iters):
-                        m.forward(s.inputs[0][:b])
-            torch.cuda.current_stream().wait_stream(side)
-            torch.cuda.synchronize()
-            if self.tune_in_context and not self._tune_loaded:
-                ctx_streams = int(os.environ.get("RDB_TUNE_CONTEXT_STREAMS", self.compute_streams))
-                self.tuning_changes.update(self._tune_in_context(m, s.inputs[0][:buckets[-1]], dev, ctx_streams))
-            s.graphs = [[None] * self.depth for _ in buckets]
-            s.outputs = [[None] * self.depth for _ in buckets]
-            for bi, b in enumerate(buckets):
-                for slot in range(self.depth):
-                    g = torch.cuda.CUDAGraph()
-                    with torch.cuda.graph(g, pool=self.pools[slot % self.compute_streams]):
-                        y = m.forward(s.inputs[slot][:b])
-                    if not y.is_contiguous():
-                        raise RuntimeError("servable model output must be contiguous")
-                    s.graphs[bi][slot] = g
-                    s.outputs[bi][slot] = y
-                    self.engine.set_graph(s.sid, bi, slot, g.raw_cuda_graph_exec(), y.data_ptr())
-            # first launch of a graph exec uploads it (kernel-arg buffers, AQL
-            # packet templates); do that here for every (bucket, slot) so no
-            # served batch pays it
-            for row in s.graphs:
-                for g in row:
-                    g.replay()
-            torch.cuda.synchronize()
-            # latency estimates per bucket (used for stale-request dropping)
-            for bi, b in enumerate(buckets):
-                g = s.graphs[bi][0]
-                g.replay()
-                torch.cuda.synchronize()
-                t = time.perf_counter()
-                for _ in range(3):
-                    g.replay()
-                torch.cuda.synchronize()
-                self.engine.set_latency_estimate(s.sid, bi, (time.perf_counter() - t) / 3 * 1e3)
+            self._capture(s, live=False)
         torch.cuda.synchronize()
         if self.tune_file and not self._tune_loaded:
             from .. import ops
@@ -175,6 +105,124 @@ class EngineRunner:
             ops.save_tuning(self.tune_file)
         self.capture_s = time.perf_counter() - t0
         return self
+
+    def _capture(self, s: SessionSpec, live: bool) -> None:
+        """Warm up, (tune,) capture and register one session's graphs.  ``live``:
+        the engine is already serving other sessions -- the session gets its own
+        graph memory pools (so unloading frees them), captures in thread-local
+        mode (the engine's threads keep launching meanwhile) and is registered
+        inactive; ``add_session`` activates it once every graph is in place."""
+        import os
+
+        dev = torch.device("cuda", self.device)
+        m = s.model
+        if getattr(m, "fold_ln_auto", False):
+            # deferred LayerNorm (models/bert.py) shortens ONE batch's forward
+            # (-3.5 % at bs32) but its heavier GEMM epilogues cost throughput
+            # when batches overlap on several compute streams, where the
+            # LayerNorm kernels already hide under the other stream's GEMMs
+            # (profiles/bert_fold_ln_ab.json)
+            m.fold_ln = m.auto_fold_ln(self.compute_streams) if hasattr(m, "auto_fold_ln") \
+                else self.compute_streams == 1
+            if os.environ.get("RDB_FOLD_LN") in ("0", "1"):      # A/B override
+                m.fold_ln = os.environ["RDB_FOLD_LN"] == "1"
+        if hasattr(m, "refresh_folded_weights"):
+            m.refresh_folded_weights()   # graphs capture weights derived from the CURRENT ones
+        buckets = sorted(set(s.buckets or default_buckets(s.max_batch)))
+        if buckets[-1] != s.max_batch:
+            buckets.append(s.max_batch)
+        s.buckets = buckets
+        in_bytes = self._bytes(m.input_shape, m.input_dtype)
+        out_bytes = self._bytes(m.output_shape, m.output_dtype)
+        add = self.engine.readd_session if live else self.engine.add_session
+        s.sid = add(s.queue, s.max_batch, s.max_wait_s, buckets, in_bytes, out_bytes, s.priority, s.slo_ms,
+                    s.drop_stale)
+        pools = [torch.cuda.graph_pool_handle() for _ in range(self.compute_streams)] if live else self.pools
+        s.pools = pools
+        s.inputs = []
+        for slot in range(self.depth):
+            x = torch.zeros((s.max_batch,) + tuple(m.input_shape), dtype=m.input_dtype, device=dev)
+            if hasattr(m, "example_input") and m.input_dtype in (torch.int32, torch.int64):
+                x.copy_(m.example_input(s.max_batch, seed=slot, device=dev))
+            s.inputs.append(x)
+            self.engine.set_input(s.sid, slot, x.data_ptr())
+        # warm up every bucket eagerly on a side stream (lazy init, caches,
+        # per-shape kernel autotuning)
+        side = torch.cuda.Stream(device=dev)
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for b in buckets:
+                for _ in range(self.warmup_iters):
+                    m.forward(s.inputs[0][:b])
+        side.synchronize()
+        if self.tune_in_context and not self._tune_loaded and not live:
+            ctx_streams = int(os.environ.get("RDB_TUNE_CONTEXT_STREAMS", self.compute_streams))
+            self.tuning_changes.update(self._tune_in_context(m, s.inputs[0][:buckets[-1]], dev, ctx_streams))
+        s.graphs = [[None] * self.depth for _ in buckets]
+        s.outputs = [[None] * self.depth for _ in buckets]
+        mode = "thread_local" if live else "global"
+        for bi, b in enumerate(buckets):
+            for slot in range(self.depth):
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, pool=pools[slot % self.compute_streams], stream=side,
+                                      capture_error_mode=mode):
+                    y = m.forward(s.inputs[slot][:b])
+                if not y.is_contiguous():
+                    raise RuntimeError("servable model output must be contiguous")
+                s.graphs[bi][slot] = g
+                s.outputs[bi][slot] = y
+                self.engine.set_graph(s.sid, bi, slot, g.raw_cuda_graph_exec(), y.data_ptr())
+        # first launch of a graph exec uploads it (kernel-arg buffers, AQL
+        # packet templates); do that here for every (bucket, slot) so no
+        # served batch pays it
+        with torch.cuda.stream(side):
+            for row in s.graphs:
+                for g in row:
+                    g.replay()
+        side.synchronize()
+        # latency estimates per bucket (used for stale-request dropping)
+        for bi, b in enumerate(buckets):
+            g = s.graphs[bi][0]
+            with torch.cuda.stream(side):
+                g.replay()
+            side.synchronize()
+            t = time.perf_counter()
+            with torch.cuda.stream(side):
+                for _ in range(3):
+                    g.replay()
+            side.synchronize()
+            self.engine.set_latency_estimate(s.sid, bi, (time.perf_counter() - t) / 3 * 1e3)
+
+    def add_session(self, spec: SessionSpec, activate: bool = True) -> int:
+        """Load a model into the RUNNING engine (planner placement): capture its
+        graphs beside the live sessions, then activate it at the launcher's next
+        batch boundary.  Returns the index into ``self.sessions``."""
+        t0 = time.perf_counter()
+        self._capture(spec, live=True)
+        spec.capture_s = time.perf_counter() - t0
+        self.sessions.append(spec)
+        if activate:
+            self.engine.set_session_active(spec.sid, True)
+        return len(self.sessions) - 1
+
+    def retire_session(self, index: int, timeout_s: float = 10.0) -> bool:
+        """Unload: stop the session at a batch boundary, wait for its in-flight
+        batches, then drop its graphs, buffers and (our reference to) the model,
+        so its HBM -- weights and private graph pools -- returns to the allocator
+        (``torch.cuda.empty_cache`` releases it to the device)."""
+        s = self.sessions[index]
+        if s.sid < 0 or s.graphs is None:
+            return True
+        if not self.engine.retire_session(s.sid, timeout_s):
+            return False
+        s.graphs = None
+        s.outputs = None
+        s.inputs = None
+        s.pools = None
+        s.model = None
+        torch.cuda.synchronize(self.device)
+        torch.cuda.empty_cache()
+        return True
 
     @staticmethod
     def _tune_in_context(m, x, dev, streams: int = 1) -> dict:

@@ -73,6 +73,52 @@ def test_actor_calls_ordering_errors_and_gpu_pinning(rt):
     assert ray.available_resources()["GPU"] == 0.0
 
 
+class Log:
+    def __init__(self):
+        self.seen = []
+
+    def put(self, x):
+        self.seen.append(x)
+        return x
+
+    def seen_all(self):
+        return list(self.seen)
+
+
+def test_remote_never_blocks_on_arg_refs(rt):
+    """.remote() with an unresolved ref argument returns at once (reference:
+    ray.remote submission is asynchronous; the dependency resolves before the
+    call runs); calls on one actor keep their submission order even when an
+    earlier one waits for its argument; an upstream failure surfaces at get()
+    on the dependent ref, not at submit time."""
+    import threading
+    from concurrent.futures import Future
+
+    L = ray.remote(Log).remote()
+    gate: Future = Future()
+    slow = ray.ObjectRef(gate)
+    t0 = time.monotonic()
+    r1 = L.put.remote(slow)          # waits for `slow`
+    r2 = L.put.remote("b")           # no deps, but queued behind r1
+    assert time.monotonic() - t0 < 0.5
+    threading.Timer(0.2, lambda: gate.set_result("a")).start()
+    assert ray.get([r1, r2], timeout=30) == ["a", "b"]
+    assert ray.get(L.seen_all.remote())[-2:] == ["a", "b"]
+    # failure propagates through the dependent ref
+    bad = ray.ObjectRef(Future())
+    r3 = L.put.remote(bad)
+    bad._fut.set_exception(ValueError("upstream"))
+    with pytest.raises(ValueError):
+        ray.get(r3, timeout=30)
+    assert ray.get(L.put.remote("c"), timeout=30) == "c"
+    # tasks chain the same way
+    sq = ray.remote(lambda x: x * x)
+    g2: Future = Future()
+    r4 = sq.remote(ray.ObjectRef(g2))
+    g2.set_result(7)
+    assert ray.get(r4, timeout=30) == 49
+
+
 def test_tasks_put_get_wait(rt):
     @ray.remote
     def add(x, y):

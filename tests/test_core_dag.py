@@ -73,6 +73,26 @@ def test_dag_execute_and_compile(rt):
     cbad.teardown()
 
 
+def test_dag_submit_failure_releases_slot(rt):
+    """A stage whose submission itself raises (a typo'd method) fails that
+    execution's ref; the compiled DAG's in-flight slot is released, so later
+    executions still run (one slot: a leak would block the second execute)."""
+    S = ray.remote(num_gpus=1)(Stage)
+    a = S.remote(2)
+    with InputNode() as inp:
+        bad = a.no_such_method.bind(inp)
+    cd = bad.experimental_compile(_max_inflight_executions=1)
+    for i in range(3):
+        with pytest.raises(Exception):
+            ray.get(cd.execute(i), timeout=30)
+    cd.teardown(timeout=5)
+    with InputNode() as inp:
+        good = a.fwd.bind(inp)
+    cg = good.experimental_compile(_max_inflight_executions=1)
+    assert [ray.get(cg.execute(i), timeout=30) for i in range(3)] == [1, 3, 5]
+    cg.teardown()
+
+
 def test_dag_validation():
     with pytest.raises(ValueError):
         MultiOutputNode([])

@@ -80,6 +80,41 @@ def test_placement_group_actors(rt):
     assert not big.wait(3) and big.state == "FAILED"
 
 
+def test_remove_races_reservation():
+    """remove_placement_group() landing while the reserve thread is inside
+    allocate_bundles: the bundles it then takes are given back, the group stays
+    REMOVED and ready() raises (no InvalidStateError in the thread, no leak)."""
+    import threading
+
+    ray.init(num_gpus=2, local_mode=True, namespace="r" + uuid.uuid4().hex[:8])
+    try:
+        ctx = ray._require_ctx()
+        inside, go = threading.Event(), threading.Event()
+        real = ctx.allocator.allocate_bundles
+
+        def slow(owner, amounts, strategy="PACK"):
+            inside.set()
+            go.wait(10)
+            return real(owner, amounts, strategy)
+
+        ctx.allocator.allocate_bundles = slow
+        pg = placement_group([{"GPU": 1}, {"GPU": 1}], strategy="SPREAD")
+        assert inside.wait(10)
+        remove_placement_group(pg)
+        go.set()
+        with pytest.raises(RuntimeError):
+            ray.get(pg.ready(), timeout=10)
+        import time
+
+        deadline = time.monotonic() + 5
+        while time.monotonic() < deadline and ray.available_resources()["GPU"] != 2:
+            time.sleep(0.02)
+        assert pg.state == "REMOVED"
+        assert ray.available_resources()["GPU"] == 2        # nothing leaked
+    finally:
+        ray.shutdown()
+
+
 class Sq:
     def __init__(self, d):
         self.d = d

@@ -220,3 +220,86 @@ def test_tp_replica_serves_llama_tp1_through_rings():
         assert rep.batches >= 3
     finally:
         j.close()
+
+
+def test_engine_executor_moves_bert_between_gpus_under_load():
+    """Planner load/unload on the native engine (reference: GPUWorker
+    _check_for_updates, 293-project/src/scheduler.py:483-523): BERT moves
+    slot 0 -> 1 -> 0 (two engines on this one GPU) while requests arrive.
+    Arriving copies are captured beside the serving sessions, leaving copies
+    drain, retire at a batch boundary and free their HBM; every request
+    completes OK with the right logits; capture time and footprint are recorded."""
+    import threading
+    import time
+
+    import torch
+
+    from ray_dynamic_batching_amd.models.bert import BertConfig, BertForSequenceClassification
+    from ray_dynamic_batching_amd.planner import synthetic_profile
+    from ray_dynamic_batching_amd.planner.scheduler import SLOScheduler
+    from ray_dynamic_batching_amd.serve.servable import TensorCodec
+
+    def fac(device):
+        return BertForSequenceClassification(BertConfig.tiny(seq_len=64), device=device, backend="hip", seed=3)
+
+    m0 = fac("cuda")
+    codec = TensorCodec.for_model(m0)
+    prof = {"bert": synthetic_profile(0.3, 0.01, 50, 1, batches=(1, 2, 4, 8, 16)),
+            "other": synthetic_profile(0.3, 0.01, 50, 1, batches=(1, 2, 4, 8, 16))}
+    s = SLOScheduler(prof, {"bert": 500.0, "other": 500.0}, {"bert": fac, "other": fac},
+                     {"bert": codec, "other": codec}, num_gpus=2, executor="engine", devices=[0, 0],
+                     max_batch={"bert": 16, "other": 16})
+
+    def plan(gpu):
+        st = s.plan_state()
+        sess = dict(model="bert", slo_ms=500.0, rate=200.0, batch=16, occupancy=0.5)
+        st["slots"] = [None, None]
+        st["slots"][gpu] = dict(duty_cycle=10.0, gpu_type="MI355X", gpu_mem=288.0, sessions=[sess])
+        st["sessions"] = {"bert": dict(model="bert", slo_ms=500.0, rate=200.0, batch=16)}
+        return st
+
+    try:
+        assert s.restore_plan(plan(0))
+        ex = s.executors
+        assert "bert" in ex[0].index and ex[0].capture_s["bert"] > 0 and ex[0].footprint["bert"] > 0
+        ids = m0.example_input(8, seed=2).cpu()
+        ref = m0(ids.cuda()).float().cpu().numpy()
+        rids, stop = {}, threading.Event()
+
+        def load():
+            i = 0
+            while not stop.is_set():
+                rids[s.submit("bert", ids[i % 8].numpy())] = i % 8
+                i += 1
+                time.sleep(0.002)
+
+        t = threading.Thread(target=load)
+        t.start()
+        mem = []
+        try:
+            for gpu in (1, 0):
+                time.sleep(0.5)
+                assert s.restore_plan(plan(gpu))
+                torch.cuda.synchronize()
+                mem.append(torch.cuda.memory_allocated())
+            time.sleep(0.5)
+        finally:
+            stop.set()
+            t.join()
+        got = {}
+        t_end = time.time() + 60
+        while len(got) < len(rids) and time.time() < t_end:
+            for c in s.poll(512, 0.2):
+                got[c[0]] = c
+        assert len(got) == len(rids) and len(rids) > 200
+        assert all(c[1] == 0 for c in got.values()), sorted({c[1] for c in got.values()})
+        for rid, c in got.items():
+            assert np.allclose(np.frombuffer(c[7], dtype=np.float32), ref[rids[rid]], atol=2e-2)
+        assert ex[0].unloads == 1 and ex[1].unloads == 1 and ex[0].loads == 2 and ex[1].loads == 1
+        assert "bert" in ex[0].index and "bert" not in ex[1].index
+        # one copy resident at the end: memory after the second move is not above
+        # the first (the copy on slot 1 was freed, slot 0's re-captured)
+        assert mem[1] <= mem[0] + 16 * 2**20, mem
+        assert ex[1].resident_bytes() == 0 and ex[0].resident_bytes() > 0
+    finally:
+        s.shutdown()
