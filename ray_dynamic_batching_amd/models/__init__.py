@@ -30,9 +30,16 @@ def register(name: str):
 
 
 def create(name: str, **kw):
+    """``backend="torch32"``: the PyTorch path in fp32 on the same (upcast)
+    weights -- the numerics anchor of the HIP kernels (models/reference.py)."""
     _load_all()
     if name not in REGISTRY:
         raise KeyError(f"unknown model {name!r}; known: {sorted(REGISTRY)}")
+    if kw.get("backend") == "torch32":
+        from .reference import fp32_reference
+
+        kw["backend"] = "torch"
+        return fp32_reference(REGISTRY[name](**kw))
     return REGISTRY[name](**kw)
 
 

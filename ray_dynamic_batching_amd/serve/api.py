@@ -70,6 +70,13 @@ class Deployment:
             d.servable = self.servable
         return d
 
+    def _with_config(self, config: DeploymentConfig) -> "Deployment":
+        """Copy with a whole config replaced (controller recovery)."""
+        d = Deployment(self.func_or_class, config, self._name)
+        if hasattr(self, "servable"):
+            d.servable = self.servable
+        return d
+
     def bind(self, *args, **kwargs) -> "Application":
         return Application(self, args, kwargs)
 

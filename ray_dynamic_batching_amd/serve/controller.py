@@ -148,8 +148,16 @@ class ServeController:
         self.jobs: Dict[str, Any] = {}            # app -> job segment handle (process mode)
         self.lock = threading.RLock()
         self.workdir = tempfile.mkdtemp(prefix="rdb_serve_")
+        # RDB_SERVE_KV names a STABLE checkpoint location (the GCS-KV role): the
+        # JSON document for the CLI and, beside it, the agent's persistent KV --
+        # a controller started later on the same path recovers from them
         self.kv_path = os.environ.get("RDB_SERVE_KV", os.path.join(self.workdir, "serve_kv.json"))
-        self.agent = ragent.NodeAgent(detect_num_gpus(), 0.0, os.path.join(self.workdir, "agent_kv.bin"))
+        agent_kv = (self.kv_path + ".agent.bin") if os.environ.get("RDB_SERVE_KV") else \
+            os.path.join(self.workdir, "agent_kv.bin")
+        self.agent = ragent.NodeAgent(detect_num_gpus(), 0.0, agent_kv)
+        self.app_modes: Dict[str, str] = {}
+        self.app_blobs: Dict[str, Dict[str, Any]] = {}     # app -> how to rebuild it (checkpoint)
+        self.recovered: List[str] = []
         self.agent_socket = os.path.join(self.workdir, "agent.sock")
         try:
             self.agent.serve(self.agent_socket)
@@ -163,6 +171,11 @@ class ServeController:
         self._thread = threading.Thread(target=self._control_loop, name="rdb-serve-controller", daemon=True)
         self._thread.start()
         atexit.register(self.shutdown)
+        if os.environ.get("RDB_SERVE_KV") and os.environ.get("RDB_SERVE_RECOVER", "1") != "0":
+            try:
+                self.recover()
+            except Exception:  # pragma: no cover - a bad checkpoint must not block start-up
+                logger.error("serve: recovery from %s failed:\n%s", self.kv_path, traceback.format_exc())
 
     def configure(self, mode: str = None, http_options: Optional[Dict[str, Any]] = None,
                   grpc_options: Optional[Dict[str, Any]] = None, **_):
@@ -230,6 +243,8 @@ class ServeController:
                 self._write_routing_table(name)
             for st in states.values():
                 self._reconcile(st, wait=True)
+            self.app_modes[name] = mode
+            self.app_blobs[name] = self._rebuild_recipe(app)
             self._checkpoint()
             return DeploymentHandle(app.deployment.name, name)
 
@@ -589,6 +604,8 @@ class ServeController:
             states = self.apps.pop(name, None)
             self.ingress.pop(name, None)
             self.route_prefixes.pop(name, None)
+            self.app_modes.pop(name, None)
+            self.app_blobs.pop(name, None)
             if not states:
                 return
             for st in states.values():
@@ -641,11 +658,34 @@ class ServeController:
                 _CONTROLLER = None
 
     # ------------------------------------------------------------ checkpoint
+    @staticmethod
+    def _rebuild_recipe(app: Application) -> Dict[str, Any]:
+        """How a later controller rebuilds this application: its import path when
+        it came from a config (reference: the checkpointed deploy schema is
+        re-imported), else the application graph itself, cloudpickled (user
+        classes by value, as process-mode replicas receive them)."""
+        ip = getattr(app, "_import_path", None)
+        if ip:
+            return dict(import_path=ip, args=getattr(app, "_import_args", None) or {})
+        import base64
+
+        import cloudpickle
+
+        try:
+            return dict(pickle=base64.b64encode(cloudpickle.dumps(app)).decode())
+        except Exception as e:  # noqa: BLE001 - unpicklable app: recorded, not recoverable
+            return dict(error=f"not picklable: {e}")
+
     def _checkpoint(self) -> None:
-        """Persist the applied config (reference: controller KV checkpoint)."""
+        """Persist the applied config (reference: controller KV checkpoint,
+        serve/_private/controller.py:510-563): per application its route prefix,
+        mode, ingress, every deployment's config and a rebuild recipe."""
         data = {}
         for app_name, states in self.apps.items():
             data[app_name] = dict(ingress=self.ingress.get(app_name),
+                                  route_prefix=self.route_prefixes.get(app_name),
+                                  mode=self.app_modes.get(app_name),
+                                  app=self.app_blobs.get(app_name, {}),
                                   deployments={n: st.config.model_dump(mode="json") for n, st in states.items()})
         blob = json.dumps(dict(version=1, time=time.time(), applications=data), default=str)
         try:
@@ -656,6 +696,68 @@ class ServeController:
             os.replace(tmp, self.kv_path)
         except OSError:  # pragma: no cover
             pass
+
+    def read_checkpoint(self) -> Optional[Dict[str, Any]]:
+        """The last checkpoint: the agent's persistent KV first (the GCS KV of
+        the reference), else the JSON document."""
+        blob = None
+        try:
+            blob = self.agent.kv_get("serve/checkpoint")
+        except Exception:  # noqa: BLE001
+            blob = None
+        if not blob:
+            try:
+                with open(self.kv_path, "rb") as f:
+                    blob = f.read()
+            except OSError:
+                return None
+        try:
+            doc = json.loads(blob)
+        except ValueError:
+            return None
+        return doc if doc.get("version") == 1 else None
+
+    def recover(self) -> List[str]:
+        """Redeploy every application of the last checkpoint that is not running
+        (controller restart, reference serve/_private/controller.py:510-563):
+        rebuilt from its import path or pickled graph, with the checkpointed
+        deployment configs re-applied (autoscaled replica counts and later
+        ``options()`` included), route prefix and mode.  Returns the names."""
+        doc = self.read_checkpoint()
+        if not doc:
+            return []
+        out = []
+        for name, a in doc.get("applications", {}).items():
+            if name in self.apps:
+                continue
+            recipe = a.get("app") or {}
+            try:
+                if recipe.get("import_path"):
+                    from .schema import ServeApplicationSchema, build_application
+
+                    app = build_application(ServeApplicationSchema(import_path=recipe["import_path"], name=name,
+                                                                   args=recipe.get("args") or {}))
+                    app._import_path = recipe["import_path"]
+                elif recipe.get("pickle"):
+                    import base64
+
+                    import cloudpickle
+
+                    app = cloudpickle.loads(base64.b64decode(recipe["pickle"]))
+                else:
+                    logger.warning("serve: application %r has no rebuild recipe (%s)", name, recipe.get("error"))
+                    continue
+                cfgs = a.get("deployments", {})
+                for node in app.walk():
+                    c = cfgs.get(node.deployment.name)
+                    if c:
+                        node.deployment = node.deployment._with_config(DeploymentConfig(**c))
+                self.deploy_application(app, name=name, route_prefix=a.get("route_prefix", "/"), mode=a.get("mode"))
+                out.append(name)
+            except Exception:  # noqa: BLE001 - one bad app must not stop the others
+                logger.error("serve: could not recover application %r:\n%s", name, traceback.format_exc())
+        self.recovered = out
+        return out
 
 
 def _codec_for_servable(sv) -> Any:

@@ -60,9 +60,18 @@ def main(argv=None) -> int:
 
         user_metrics.start_publisher(os.environ["RDB_AGENT_SOCKET"], os.environ["RDB_METRICS_KEY"])
 
+    parent = os.getppid()
+
     def heartbeat():
         while not stop.is_set():
             job.heartbeat(r)
+            # orphaned (the controller / node agent process died without
+            # terminating us): leave instead of serving a job nobody supervises;
+            # a recovering controller starts its own replicas
+            if os.getppid() != parent:
+                logger.warning("node agent (pid %d) is gone: replica exits", parent)
+                stop.set()
+                os._exit(3)
             time.sleep(0.25)
     threading.Thread(target=heartbeat, daemon=True).start()
 

@@ -96,6 +96,8 @@ def build_application(app_schema: ServeApplicationSchema):
             node.deployment = node.deployment.options(**ov)
     if overrides:
         raise ValueError(f"deployments {sorted(overrides)} not found in {app_schema.import_path}")
+    target._import_path = app_schema.import_path       # the controller checkpoints how to rebuild it
+    target._import_args = dict(app_schema.args or {})
     return target
 
 

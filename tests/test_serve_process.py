@@ -79,3 +79,68 @@ def test_replica_crash_is_restarted_and_requests_retried():
     assert new_pid != pid
     st = serve.status()["applications"]["default"]["deployments"]["Echo"]
     assert st["replicas"][0]["restarts"] >= 1
+
+
+_CRASHING_DRIVER = r"""
+import os, sys
+sys.path.insert(0, {repo!r})
+from ray_dynamic_batching_amd import serve
+
+@serve.deployment(num_replicas=2, max_ongoing_requests=16)
+class Scaled:
+    def __init__(self, k):
+        self.k = k
+
+    def __call__(self, x):
+        return x * self.k
+
+h = serve.run(Scaled.bind(3), name="calc", route_prefix="/calc", mode="process")
+assert h.remote(5).result(timeout_s=30) == 15
+# a later options() change is part of the checkpointed config
+h = serve.run(Scaled.options(num_replicas=1).bind(4), name="calc", route_prefix="/calc", mode="process")
+assert h.remote(5).result(timeout_s=30) == 20
+print("deployed", flush=True)
+os._exit(0)          # controller dies: no shutdown, no checkpoint clean-up
+"""
+
+
+def test_controller_recovers_applications_from_checkpoint(tmp_path, monkeypatch):
+    """A controller started on the same checkpoint location (RDB_SERVE_KV:
+    the agent's persistent KV + JSON, the GCS-KV role) after the previous one
+    died redeploys its applications -- graph, configs, route prefix, mode
+    (reference serve/_private/controller.py:510-563)."""
+    import subprocess
+    import sys
+
+    kv = str(tmp_path / "serve_kv.json")
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, RDB_SERVE_KV=kv, RDB_SERVE_DISCOVERY=str(tmp_path / "disc.json"))
+    r = subprocess.run([sys.executable, "-c", _CRASHING_DRIVER.format(repo=repo)], env=env,
+                       capture_output=True, text=True, timeout=180)
+    assert "deployed" in r.stdout, r.stdout + r.stderr
+    assert os.path.exists(kv) and os.path.exists(kv + ".agent.bin")
+    monkeypatch.setenv("RDB_SERVE_KV", kv)
+    monkeypatch.setenv("RDB_SERVE_DISCOVERY", str(tmp_path / "disc2.json"))
+    from ray_dynamic_batching_amd.serve.controller import get_controller
+
+    ctrl = get_controller()
+    assert ctrl.recovered == ["calc"]
+    h = serve.get_app_handle("calc")
+    assert h.remote(6).result(timeout_s=30) == 24          # the later config (k=4) came back
+    st = serve.status()["applications"]["calc"]["deployments"]["Scaled"]
+    assert st["mode"] == "process" and st["running_replicas"] == 1
+    assert ctrl.route_prefixes["calc"] == "/calc"
+    # an explicit shutdown empties the checkpoint: the next controller starts clean
+    serve.shutdown()
+    assert get_controller().recovered == []
+
+
+def test_controller_recovery_disabled(tmp_path, monkeypatch):
+    from ray_dynamic_batching_amd.serve.controller import ServeController
+
+    monkeypatch.setenv("RDB_SERVE_KV", str(tmp_path / "kv.json"))
+    monkeypatch.setenv("RDB_SERVE_DISCOVERY", str(tmp_path / "d.json"))
+    serve.run(Down.bind(), name="d1", mode="local")
+    assert serve.get_app_handle("d1").remote(1).result(timeout_s=10) == 2
+    doc = serve.api._controller().read_checkpoint()
+    assert "d1" in doc["applications"] and doc["applications"]["d1"]["app"].get("pickle")
