@@ -104,6 +104,29 @@ class JobHandle {
   uint32_t replica_status(uint32_t r) { check_r(r); return job_.replica(r)->status.load(); }
   uint32_t replica_generation(uint32_t r) { check_r(r); return job_.replica(r)->restarts.load(); }
   uint32_t queue_replica(uint32_t q) { check_q(q); return job_.queue(q)->replica.load(); }
+  // Replica side of multiplexing: the ids (hashes) it holds, at most kMuxSlots.
+  void set_queue_models(uint32_t q, std::vector<uint64_t> ids) {
+    check_q(q);
+    QueueState* s = job_.queue(q);
+    for (int i = 0; i < kMuxSlots; ++i)
+      s->mux[i].store(i < (int)ids.size() ? ids[i] : 0, std::memory_order_release);
+  }
+  // Test hook (router unit tests): make queue q look `depth` deep to the
+  // router without enqueuing anything (submitted = completed + depth).
+  void test_set_queue_depth(uint32_t q, uint64_t depth) {
+    check_q(q);
+    QueueState* s = job_.queue(q);
+    s->submitted.store(s->completed.load() + depth, std::memory_order_release);
+  }
+  std::vector<uint64_t> queue_models(uint32_t q) {
+    check_q(q);
+    std::vector<uint64_t> out;
+    for (int i = 0; i < kMuxSlots; ++i) {
+      const uint64_t v = job_.queue(q)->mux[i].load(std::memory_order_acquire);
+      if (v) out.push_back(v);
+    }
+    return out;
+  }
   void heartbeat(uint32_t r) { check_r(r); job_.replica(r)->heartbeat_ns.store(now_ns()); }
   double heartbeat_age_s(uint32_t r) {
     check_r(r);
@@ -272,7 +295,11 @@ class Client {
   // queues whose replica is not READY and queues at max_ongoing.  Returns -1
   // if every candidate is saturated (the caller keeps the request queued, as
   // Serve's router does while no replica has capacity).
-  int choose_queue(uint32_t model) {
+  // Multiplexed requests (mux != 0, the hash of the model id): among the ready
+  // queues with capacity, first those whose replica holds the id, then those
+  // with the fewest ids loaded (a free cache slot), then any -- each tier by
+  // power-of-two choice on depth (reference pow_2_scheduler.py:396-443).
+  int choose_queue(uint32_t model, uint64_t mux = 0) {
     JobHeader* h = job_.hdr();
     cand_.clear();
     int serving = 0;
@@ -298,6 +325,38 @@ class Client {
     if (n == 1) {
       const uint32_t q = cand_[0];
       return ok(q, depth(q)) ? (int)q : -1;
+    }
+    if (mux != 0) {
+      auto holds = [&](uint32_t q) {
+        QueueState* s = job_.queue(q);
+        for (int i = 0; i < kMuxSlots; ++i)
+          if (s->mux[i].load(std::memory_order_relaxed) == mux) return true;
+        return false;
+      };
+      auto loaded = [&](uint32_t q) {
+        int c = 0;
+        QueueState* s = job_.queue(q);
+        for (int i = 0; i < kMuxSlots; ++i) c += s->mux[i].load(std::memory_order_relaxed) != 0;
+        return c;
+      };
+      tier_.clear();
+      for (uint32_t q : cand_)
+        if (holds(q) && ok(q, depth(q))) tier_.push_back(q);
+      if (tier_.empty()) {
+        int fewest = INT32_MAX;
+        for (uint32_t q : cand_)
+          if (ok(q, depth(q))) fewest = std::min(fewest, loaded(q));
+        for (uint32_t q : cand_)
+          if (ok(q, depth(q)) && loaded(q) == fewest) tier_.push_back(q);
+      }
+      if (!tier_.empty()) {
+        const size_t nt = tier_.size();
+        const size_t ia = rng_.next() % nt;
+        const size_t ib = nt > 1 ? (ia + 1 + rng_.next() % (nt - 1)) % nt : ia;   // two distinct samples
+        const uint32_t a2 = tier_[ia], b2 = tier_[ib];
+        return (int)(depth(a2) <= depth(b2) ? a2 : b2);
+      }
+      return -1;   // every candidate at max_ongoing
     }
     // Two random distinct candidates; fall back to a full scan when both are full.
     const uint32_t a = cand_[rng_.next() % n];
@@ -370,7 +429,7 @@ class Client {
   int id_ = 0;
   Ring cmp_;
   uint64_t cmp_pos_ = 0;
-  std::vector<uint32_t> cand_;
+  std::vector<uint32_t> cand_, tier_;
 };
 
 // ---------------------------------------------------------------------------
@@ -790,6 +849,9 @@ PYBIND11_MODULE(_rdb_runtime, m) {
       .def("replica_status", &JobHandle::replica_status)
       .def("replica_generation", &JobHandle::replica_generation)
       .def("queue_replica", &JobHandle::queue_replica)
+      .def("set_queue_models", &JobHandle::set_queue_models)
+      .def("_test_set_queue_depth", &JobHandle::test_set_queue_depth)
+      .def("queue_models", &JobHandle::queue_models)
       .def("heartbeat", &JobHandle::heartbeat)
       .def("heartbeat_age_s", &JobHandle::heartbeat_age_s)
       .def("bump_restarts", &JobHandle::bump_restarts)
@@ -823,7 +885,7 @@ PYBIND11_MODULE(_rdb_runtime, m) {
       .def(py::init<JobHandle&, int, uint64_t>(), py::arg("job"), py::arg("client_id") = -1,
            py::arg("seed") = 0, py::keep_alive<1, 2>())
       .def_property_readonly("id", &Client::id)
-      .def("choose_queue", &Client::choose_queue)
+      .def("choose_queue", &Client::choose_queue, py::arg("model"), py::arg("mux") = 0)
       .def("submit",
            [](Client& c, uint32_t queue, py::bytes data, uint16_t kind, double deadline_s, uint64_t req_id) {
              char* buf;

@@ -281,6 +281,7 @@ struct alignas(64) ReplicaState {
   Histogram hist_service;               // batch formation -> completion
 };
 
+constexpr int kMuxSlots = 16;
 struct alignas(64) QueueState {
   std::atomic<uint32_t> active;         // 1 if a replica serves this queue
   std::atomic<uint32_t> replica;        // owning replica
@@ -294,6 +295,11 @@ struct alignas(64) QueueState {
   std::atomic<int64_t> slo_ns;          // per-model SLO used for violation counting
   Histogram hist_queue_wait;            // submit -> batch launch
   Histogram hist_e2e;                   // submit -> completion written
+  // model multiplexing: 64-bit hashes of the multiplexed model ids this queue's
+  // replica holds (0 = empty slot), published by the replica on load / evict;
+  // the router prefers queues holding the requested id
+  // (serve/_private/replica_scheduler/pow_2_scheduler.py:330-345, 396-443)
+  std::atomic<uint64_t> mux[kMuxSlots];
 };
 
 // Per-replica trace ring (chrome-trace export, utils/tracing.py): multi-writer,

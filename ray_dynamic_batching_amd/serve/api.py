@@ -189,6 +189,14 @@ def run(target: Application, blocking: bool = False, name: str = "default", rout
         target = target.bind()
     if not isinstance(target, Application):
         raise TypeError("serve.run expects an Application (Deployment.bind(...))")
+    if logging_config is not None:
+        # application-level default: deployments without their own config take it
+        from .logging_utils import as_logging_config
+
+        lc = as_logging_config(logging_config).model_dump()
+        for node in target.walk():
+            if node.deployment.config.logging_config is None:
+                node.deployment = node.deployment.options(logging_config=lc)
     ctrl = _controller()
     handle = ctrl.deploy_application(target, name=name, route_prefix=route_prefix,
                                      mode=("local" if _local_testing_mode else mode))

@@ -39,7 +39,7 @@ class _SingleRequest:
     args: Tuple
     kwargs: Dict[str, Any]
     future: asyncio.Future
-    enqueue_time: float = field(default_factory=time.perf_counter)
+    enqueue_time: float = 0.0
 
 
 def _validate_max_batch_size(v) -> None:
@@ -95,15 +95,17 @@ class _BatchQueue:
         """Block for the first item, then keep adding until full or until
         batch_wait_timeout_s has elapsed since that first item."""
         batch = [await self.queue.get()]
+        # the event loop's clock (monotonic; a test loop may virtualise it)
+        clock = asyncio.get_running_loop().time
         max_bs = self.max_batch_size
         timeout = self.batch_wait_timeout_s
-        deadline = time.perf_counter() + timeout
+        deadline = clock() + timeout
         while len(batch) < max_bs:
             while len(batch) < max_bs and not self.queue.empty():
                 batch.append(self.queue.get_nowait())
             if len(batch) >= max_bs:
                 break
-            remaining = deadline - time.perf_counter()
+            remaining = deadline - clock()
             if remaining <= 0:
                 break
             self._arrival.clear()
@@ -120,7 +122,7 @@ class _BatchQueue:
             batch = [r for r in batch if not r.future.done()]
             if not batch:
                 continue
-            self.current_iteration_start = time.perf_counter()
+            self.current_iteration_start = asyncio.get_running_loop().time()
             self.batches_processed += 1
             self.last_batch_sizes = (self.last_batch_sizes + [len(batch)])[-1000:]
             if self._hook:
@@ -267,7 +269,8 @@ def batch(_func: Optional[Callable] = None, /, max_batch_size: int = 10, batch_w
             if is_method:
                 self_arg, args = args[0], args[1:]
             fut = asyncio.get_running_loop().create_future()
-            lazy.queue(self_arg).put(_SingleRequest(self_arg, tuple(args), dict(kwargs), fut))
+            lazy.queue(self_arg).put(_SingleRequest(self_arg, tuple(args), dict(kwargs), fut,
+                                                    asyncio.get_running_loop().time()))
             return fut
 
         if is_gen:

@@ -77,13 +77,28 @@ class DeploymentConfig(BaseModel):
     placement_group_bundles: Optional[List[Dict[str, float]]] = None
     placement_group_strategy: Optional[str] = None
     max_replicas_per_node: Optional[int] = None
-    logging_config: Optional[Dict[str, Any]] = None
+    logging_config: Optional[Dict[str, Any]] = None   # serve.logging_utils.LoggingConfig fields
     # Nexus / fork extensions
     slo_ms: Optional[float] = None
     profile_csv: Optional[str] = None
     priority: int = 0
     drop_stale: bool = False
     engine: EngineConfig = Field(default_factory=EngineConfig)
+
+    @field_validator("logging_config", mode="before")
+    @classmethod
+    def _logging(cls, v):
+        # validated here (bad encoding / level fail at definition time), kept as
+        # a plain dict so the config stays JSON-checkpointable
+        from .logging_utils import as_logging_config
+
+        c = as_logging_config(v)
+        return None if c is None else c.model_dump()
+
+    def get_logging_config(self):
+        from .logging_utils import as_logging_config
+
+        return as_logging_config(self.logging_config)
 
     @field_validator("max_ongoing_requests")
     @classmethod

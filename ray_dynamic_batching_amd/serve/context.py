@@ -16,6 +16,7 @@ class ReplicaContext:
     servable_object: object = None
     max_ongoing_requests: Optional[int] = None
     gpu: Optional[int] = None
+    logger: object = None           # the replica's component logger (serve.logging_utils)
 
 
 _local = threading.local()

@@ -22,6 +22,36 @@ def get_multiplexed_model_id() -> str:
     return get_request_context().multiplexed_model_id
 
 
+# Replica-side publication of the loaded model ids (process mode: the replica
+# sets a publisher that writes their hashes into its queue's shm slots, where
+# the native router's choose_queue looks for them).
+_caches: "list" = []
+_publisher: Optional[Callable] = None
+
+
+def set_publisher(fn: Optional[Callable]) -> None:
+    global _publisher
+    _publisher = fn
+    _publish()
+
+
+def loaded_model_ids() -> list:
+    out = []
+    for c in _caches:
+        for m in c.models:
+            if m not in out:
+                out.append(m)
+    return out
+
+
+def _publish() -> None:
+    if _publisher is not None:
+        try:
+            _publisher(loaded_model_ids())
+        except Exception:  # pragma: no cover - routing hint only
+            pass
+
+
 class _ModelCache:
     def __init__(self, loader: Callable, max_models: int):
         self.loader = loader
@@ -30,6 +60,7 @@ class _ModelCache:
         self.loading: dict = {}
         self.num_loads = 0
         self.num_evictions = 0
+        _caches.append(self)
 
     async def get(self, owner, model_id: str):
         if model_id in self.models:
@@ -43,6 +74,7 @@ class _ModelCache:
             while len(self.models) >= self.max_models:
                 _, old = self.models.popitem(last=False)
                 self.num_evictions += 1
+                _publish()
                 d = getattr(old, "__del__", None)
                 if d is not None:
                     try:
@@ -54,6 +86,7 @@ class _ModelCache:
                 r = await r
             self.models[model_id] = r
             self.num_loads += 1
+            _publish()
             fut.set_result(r)
             return r
         except Exception as e:

@@ -28,7 +28,10 @@ logger = logging.getLogger("ray_dynamic_batching_amd.serve")
 
 
 class UserCallable:
-    def __init__(self, func_or_class, init_args, init_kwargs, user_config=None):
+    def __init__(self, func_or_class, init_args, init_kwargs, user_config=None, access_log=None):
+        from .logging_utils import AccessLog
+
+        self.access = access_log or AccessLog(None, False)
         self.is_function = not inspect.isclass(func_or_class)
         self.func_or_class = func_or_class
         if self.is_function:
@@ -58,13 +61,20 @@ class UserCallable:
 
     async def call(self, meta: RequestMeta, args, kwargs) -> Any:
         token = _set_request_context(RequestContext(meta.request_id, meta.multiplexed_model_id, meta.method_name))
+        t0 = time.perf_counter()
+        status = "ERROR"
         try:
             fn = self.resolve(meta.method_name)
             r = fn(*args, **kwargs)
             if inspect.isawaitable(r):
                 r = await r
+            status = "OK"
             return r
+        except asyncio.CancelledError:
+            status = "CANCELLED"
+            raise
         finally:
+            self.access.record(meta, status, time.perf_counter() - t0)
             from .context import _request_ctx
 
             _request_ctx.reset(token)
@@ -72,6 +82,8 @@ class UserCallable:
     async def call_stream(self, meta: RequestMeta, args, kwargs, emit) -> None:
         """Drive a (sync or async) generator method; emit(kind, value)."""
         token = _set_request_context(RequestContext(meta.request_id, meta.multiplexed_model_id, meta.method_name))
+        t0 = time.perf_counter()
+        status = "ERROR"
         try:
             fn = self.resolve(meta.method_name)
             g = fn(*args, **kwargs)
@@ -86,9 +98,11 @@ class UserCallable:
                     g = await g
                 emit("item", g)
             emit("end", None)
+            status = "OK"
         except Exception as e:
             emit("error", e)
         finally:
+            self.access.record(meta, status, time.perf_counter() - t0)
             from .context import _request_ctx
 
             _request_ctx.reset(token)
@@ -130,12 +144,17 @@ class LocalReplica:
         self._loop = asyncio.new_event_loop()
         ready = concurrent.futures.Future()
         self.ctx = ReplicaContext(app_name, deployment, self.replica_id, index, None, self.max_ongoing, gpu)
+        from .logging_utils import AccessLog, configure_replica_logger
+
+        lcfg = config.get_logging_config()
+        self.logger = configure_replica_logger(app_name, deployment, index, self.replica_id, lcfg)
+        access = AccessLog(self.logger, lcfg is None or lcfg.enable_access_log)
 
         def run():
             asyncio.set_event_loop(self._loop)
             _set_replica_context(self.ctx)
             try:
-                self.user = UserCallable(func_or_class, init_args, init_kwargs, config.user_config)
+                self.user = UserCallable(func_or_class, init_args, init_kwargs, config.user_config, access)
                 self.ctx.servable_object = self.user.obj
                 ready.set_result(True)
             except BaseException as e:  # constructor failure

@@ -78,6 +78,12 @@ def main(argv=None) -> int:
     ctx = ReplicaContext(spec["app_name"], spec["deployment"], f"{spec['app_name']}#{spec['deployment']}#{r}", r,
                          None, cfg.max_ongoing_requests, gpu)
     _set_replica_context(ctx)
+    from .logging_utils import configure_replica_logger
+
+    lcfg = cfg.get_logging_config()
+    ctx.logger = configure_replica_logger(spec["app_name"], spec["deployment"], r, ctx.replica_id, lcfg,
+                                          capture_user_logs=True)
+    ctx.logger.info("replica starting (pid %d, gpu %s)", os.getpid(), gpu)
     try:
         if spec.get("servable"):
             return _run_engine(spec, cfg, job, r, stop)
@@ -125,10 +131,18 @@ def _run_python(spec, cfg, job, r, stop, ctx) -> int:
 
     loop = asyncio.new_event_loop()
     asyncio.set_event_loop(loop)
-    user = UserCallable(spec["func_or_class"], spec["init_args"], spec["init_kwargs"], cfg.user_config)
+    from .logging_utils import AccessLog
+
+    lcfg = cfg.get_logging_config()
+    user = UserCallable(spec["func_or_class"], spec["init_args"], spec["init_kwargs"], cfg.user_config,
+                        AccessLog(ctx.logger, lcfg is None or lcfg.enable_access_log))
     ctx.servable_object = user.obj
     cons = rjob.Consumer(job, [r])
     inflight = [0]
+    from . import multiplex
+    from .router import mux_hash
+
+    multiplex.set_publisher(lambda ids: job.set_queue_models(r, [mux_hash(i) for i in ids]))
     from ..utils.faults import injector
 
     faults = injector()

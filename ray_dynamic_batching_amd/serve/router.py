@@ -295,13 +295,34 @@ class ShmRouter:
             payload = cloudpickle.dumps((meta.method_name, args, kwargs, meta.multiplexed_model_id, meta.stream,
                                          meta.request_id))
             kind = KIND_PICKLE
+        route = _Route(self.model_id, mux_hash(meta.multiplexed_model_id)) if meta.multiplexed_model_id \
+            else self.model_id
         if meta.stream:
             q = _queue.Queue()
-            self.hub.submit(self.model_id, payload, kind, ("stream", q), self.codec, self.max_retries)
+            self.hub.submit(route, payload, kind, ("stream", q), self.codec, self.max_retries)
             return DeploymentResponseGenerator(q, meta)
         fut = concurrent.futures.Future()
-        self.hub.submit(self.model_id, payload, kind, ("unary", fut), self.codec, self.max_retries)
+        self.hub.submit(route, payload, kind, ("unary", fut), self.codec, self.max_retries)
         return DeploymentResponse(fut, meta)
+
+
+def mux_hash(model_id: str) -> int:
+    """64-bit id of a multiplexed model id as replicas publish it in shm (0 = none)."""
+    import hashlib
+
+    if not model_id:
+        return 0
+    return int.from_bytes(hashlib.blake2b(model_id.encode(), digest_size=8).digest(), "little") or 1
+
+
+class _Route(int):
+    """A deployment's model id (an int: pending counts and retries key on it)
+    carrying the request's multiplexed-model hash for the native router."""
+
+    def __new__(cls, model_id: int, mux: int = 0):
+        o = super().__new__(cls, model_id)
+        o.mux = mux
+        return o
 
 
 class _ShmClientHub:
@@ -344,9 +365,9 @@ class _ShmClientHub:
                 self._pending_by_model[model_id] += 1
 
     def _try_submit(self, model_id, payload, kind, sink, codec, retries_left) -> bool:
-        q = self.client.choose_queue(model_id)
+        q = self.client.choose_queue(int(model_id), getattr(model_id, "mux", 0))
         if q == -2:
-            self._fail(sink, DeploymentUnavailableError(f"no replica serves model id {model_id}"))
+            self._fail(sink, DeploymentUnavailableError(f"no replica serves model id {int(model_id)}"))
             return True
         if q < 0:
             return False

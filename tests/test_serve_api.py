@@ -264,3 +264,66 @@ def test_unhealthy_replica_is_replaced_local():
     while time.time() < deadline and h.remote().result() == first:
         time.sleep(0.05)
     assert h.remote().result() != first
+
+
+def test_logging_config_validation_and_app_default():
+    from ray_dynamic_batching_amd.serve.logging_utils import LoggingConfig
+
+    with pytest.raises(Exception):
+        serve.deployment(logging_config={"encoding": "XML"})(lambda x: x)
+    with pytest.raises(Exception):
+        LoggingConfig(log_level="LOUD")
+    d = serve.deployment(logging_config=LoggingConfig(encoding="json", log_level="DEBUG"))(lambda x: x)
+    assert d.config.logging_config["encoding"] == "JSON"
+    assert d.config.get_logging_config().level() == 10
+
+
+def test_access_log_text_and_json_local(tmp_path):
+    """Per-replica component log + one access-log line per request (reference
+    replica.py:430-437, logging_utils.py:274); JSON encoding carries the
+    request fields; enable_access_log=False silences it; serve.run's
+    logging_config is the application default."""
+    import json as _json
+    import logging as _logging
+
+    @serve.deployment(num_replicas=1)
+    class Greeter:
+        def __call__(self, x):
+            _logging.getLogger("ray.serve.replica.default.Greeter.0").warning("user says %s", x)
+            return f"hi {x}"
+
+        def boom(self):
+            raise ValueError("no")
+
+    h = serve.run(Greeter.bind(), _local_testing_mode=True,
+                  logging_config={"encoding": "JSON", "logs_dir": str(tmp_path)})
+    assert h.remote("a").result() == "hi a"
+    with pytest.raises(ValueError):
+        h.boom.remote().result()
+    path = tmp_path / "replica_default_Greeter_0.log"
+    lines = [_json.loads(line) for line in path.read_text().splitlines()]
+    access = [x for x in lines if "latency_ms" in x]
+    assert [(x["method"], x["status"]) for x in access] == [("__call__", "OK"), ("boom", "ERROR")]
+    assert all(x["deployment"] == "Greeter" and x["replica"] == "default#Greeter#0" for x in lines)
+    assert any(x["message"] == "user says a" for x in lines)
+    serve.shutdown()
+
+    @serve.deployment(logging_config={"enable_access_log": False, "logs_dir": str(tmp_path / "quiet")})
+    class Quiet:
+        def __call__(self, x):
+            return x
+
+    h = serve.run(Quiet.bind(), _local_testing_mode=True)
+    assert h.remote(1).result() == 1
+    assert (tmp_path / "quiet" / "replica_default_Quiet_0.log").read_text() == ""
+    serve.shutdown()
+
+    @serve.deployment(logging_config={"encoding": "TEXT", "logs_dir": str(tmp_path / "t")})
+    class Texty:
+        def __call__(self, x):
+            return x
+
+    h = serve.run(Texty.bind(), _local_testing_mode=True)
+    h.remote(2).result()
+    txt = (tmp_path / "t" / "replica_default_Texty_0.log").read_text()
+    assert "Texty default#Texty#0" in txt and "CALL __call__ OK" in txt and "ms" in txt

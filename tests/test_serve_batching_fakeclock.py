@@ -1,0 +1,387 @@
+"""@serve.batch on a virtual clock: the batching queue measures time with the
+event loop's clock, so a loop whose ``time()`` only moves when the test
+advances it makes every timing case deterministic (in spirit of
+python/ray/serve/tests/unit/test_batching.py, which drives the same flush /
+cancel / setter / generator cases with a fake timer)."""
+import asyncio
+
+import pytest
+
+from ray_dynamic_batching_amd import serve
+from ray_dynamic_batching_amd.serve.exceptions import RayServeException
+
+
+class FakeClockLoop(asyncio.SelectorEventLoop):
+    """An event loop whose clock stands still until ``advance()``."""
+
+    def __init__(self):
+        super().__init__()
+        self._now = 1000.0
+
+    def time(self):
+        return self._now
+
+    def advance(self, dt: float) -> None:
+        self._now += dt
+
+
+def run(coro_fn):
+    loop = FakeClockLoop()
+    try:
+        return loop.run_until_complete(coro_fn(loop))
+    finally:
+        # the batching queues' background tasks outlive the test body
+        pending = [t for t in asyncio.all_tasks(loop) if not t.done()]
+        for t in pending:
+            t.cancel()
+        loop.run_until_complete(asyncio.gather(*pending, return_exceptions=True))
+        loop.close()
+
+
+async def settle(n: int = 8):
+    """Let every ready callback run (no virtual time passes)."""
+    for _ in range(n):
+        await asyncio.sleep(0)
+
+
+async def advance(loop, dt: float):
+    loop.advance(dt)
+    await settle()
+
+
+def _collector(max_batch_size=4, timeout=0.1):
+    sizes = []
+
+    @serve.batch(max_batch_size=max_batch_size, batch_wait_timeout_s=timeout)
+    async def f(xs):
+        sizes.append(len(xs))
+        return [x * 10 for x in xs]
+
+    return f, sizes
+
+
+def test_timeout_counts_from_first_item():
+    f, sizes = _collector()
+
+    async def main(loop):
+        t = asyncio.ensure_future(f(1))
+        await settle()
+        await advance(loop, 0.099)
+        assert not t.done() and sizes == []
+        await advance(loop, 0.002)
+        assert t.done() and t.result() == 10 and sizes == [1]
+    run(main)
+
+
+def test_late_item_joins_and_does_not_extend_deadline():
+    f, sizes = _collector()
+
+    async def main(loop):
+        a = asyncio.ensure_future(f(1))
+        await settle()
+        await advance(loop, 0.05)
+        b = asyncio.ensure_future(f(2))
+        await settle()
+        await advance(loop, 0.049)
+        assert not a.done() and not b.done()
+        await advance(loop, 0.002)          # 0.101 after the FIRST item
+        assert (a.result(), b.result()) == (10, 20) and sizes == [2]
+    run(main)
+
+
+def test_full_batch_flushes_without_time_passing():
+    f, sizes = _collector(max_batch_size=3, timeout=1000)
+
+    async def main(loop):
+        ts = [asyncio.ensure_future(f(i)) for i in range(7)]
+        await settle(20)
+        assert [t.done() for t in ts] == [True] * 6 + [False]
+        assert sizes == [3, 3]
+        await advance(loop, 1000.01)
+        assert ts[6].result() == 60 and sizes == [3, 3, 1]
+    run(main)
+
+
+def test_next_batch_timer_starts_at_its_own_first_item():
+    f, sizes = _collector(timeout=0.1)
+
+    async def main(loop):
+        a = asyncio.ensure_future(f(1))
+        await settle()
+        await advance(loop, 0.2)
+        assert a.done()
+        await advance(loop, 5.0)            # idle time does not count for the next batch
+        b = asyncio.ensure_future(f(2))
+        await settle()
+        await advance(loop, 0.09)
+        assert not b.done()
+        await advance(loop, 0.02)
+        assert b.done() and sizes == [1, 1]
+    run(main)
+
+
+def test_zero_timeout_takes_only_what_is_queued():
+    f, sizes = _collector(max_batch_size=8, timeout=0.0)
+
+    async def main(loop):
+        ts = [asyncio.ensure_future(f(i)) for i in range(3)]
+        await settle(20)
+        assert all(t.done() for t in ts) and sum(sizes) == 3 and max(sizes) <= 3
+    run(main)
+
+
+def test_set_timeout_while_batch_forming_applies_to_next_batch():
+    f, sizes = _collector(timeout=1.0)
+
+    async def main(loop):
+        a = asyncio.ensure_future(f(1))
+        await settle()
+        f.set_batch_wait_timeout_s(0.01)    # the forming batch keeps its 1 s deadline
+        await advance(loop, 0.5)
+        assert not a.done()
+        await advance(loop, 0.51)
+        assert a.done()
+        b = asyncio.ensure_future(f(2))
+        await settle()
+        await advance(loop, 0.011)          # the new batch uses 0.01 s
+        assert b.done() and sizes == [1, 1]
+        assert f._get_batch_wait_timeout_s() == 0.01
+    run(main)
+
+
+def test_set_max_batch_size_while_forming_applies_to_next_batch():
+    f, sizes = _collector(max_batch_size=4, timeout=1.0)
+
+    async def main(loop):
+        ts = [asyncio.ensure_future(f(i)) for i in range(2)]
+        await settle()
+        f.set_max_batch_size(2)             # the forming batch was opened with 4
+        ts.append(asyncio.ensure_future(f(2)))
+        await settle()
+        assert sizes == []                  # 3 items < 4: still forming
+        ts.append(asyncio.ensure_future(f(3)))
+        await settle()
+        assert sizes == [4]
+        ts += [asyncio.ensure_future(f(i)) for i in (4, 5)]
+        await settle(20)
+        assert sizes == [4, 2] and f._get_max_batch_size() == 2
+        assert [t.result() for t in ts] == [0, 10, 20, 30, 40, 50]
+    run(main)
+
+
+def test_setters_validate():
+    f, _ = _collector()
+    with pytest.raises(ValueError):
+        f.set_max_batch_size(0)
+    with pytest.raises(TypeError):
+        f.set_max_batch_size(2.5)
+    with pytest.raises(ValueError):
+        f.set_batch_wait_timeout_s(-0.1)
+
+
+def test_cancelled_while_forming_is_left_out():
+    f, sizes = _collector(timeout=0.1)
+
+    async def main(loop):
+        ts = [asyncio.ensure_future(f(i)) for i in range(3)]
+        await settle()
+        ts[1].cancel()
+        await advance(loop, 0.2)
+        assert ts[0].result() == 0 and ts[2].result() == 20 and ts[1].cancelled()
+        assert sizes == [2]
+    run(main)
+
+
+def test_all_cancelled_batch_is_skipped_and_loop_survives():
+    f, sizes = _collector(timeout=0.1)
+
+    async def main(loop):
+        ts = [asyncio.ensure_future(f(i)) for i in range(2)]
+        await settle()
+        for t in ts:
+            t.cancel()
+        await advance(loop, 0.2)
+        assert sizes == []
+        t = asyncio.ensure_future(f(5))
+        await settle()
+        await advance(loop, 0.2)
+        assert t.result() == 50 and sizes == [1]
+    run(main)
+
+
+def test_cancel_during_batch_execution_other_callers_still_served():
+    started, release = [], None
+
+    @serve.batch(max_batch_size=3, batch_wait_timeout_s=0.1)
+    async def slow(xs):
+        started.append(list(xs))
+        await release.wait()
+        return [x + 1 for x in xs]
+
+    async def main(loop):
+        nonlocal release
+        release = asyncio.Event()
+        ts = [asyncio.ensure_future(slow(i)) for i in range(3)]
+        await settle()
+        assert started == [[0, 1, 2]]
+        ts[0].cancel()                      # caller gives up mid-batch
+        release.set()
+        await settle()
+        assert ts[0].cancelled() and ts[1].result() == 2 and ts[2].result() == 3
+    run(main)
+
+
+def test_exception_fans_out_and_next_batch_runs():
+    calls = []
+
+    @serve.batch(max_batch_size=2, batch_wait_timeout_s=0.1)
+    async def g(xs):
+        calls.append(xs)
+        if len(calls) == 1:
+            raise KeyError("boom")
+        return xs
+
+    async def main(loop):
+        ts = [asyncio.ensure_future(g(i)) for i in range(2)]
+        await settle()
+        assert all(isinstance(t.exception(), KeyError) for t in ts)
+        t = asyncio.ensure_future(g(9))
+        await settle()
+        await advance(loop, 0.2)
+        assert t.result() == 9
+    run(main)
+
+
+def test_wrong_length_is_a_serve_exception():
+    @serve.batch(max_batch_size=2, batch_wait_timeout_s=0.1)
+    async def bad(xs):
+        return xs[:1]
+
+    async def main(loop):
+        ts = [asyncio.ensure_future(bad(i)) for i in range(2)]
+        await settle()
+        for t in ts:
+            assert isinstance(t.exception(), RayServeException)
+    run(main)
+
+
+def test_mismatched_arity_fails_the_batch():
+    @serve.batch(max_batch_size=2, batch_wait_timeout_s=0.1)
+    async def h(xs, ys=None):
+        return xs
+
+    async def main(loop):
+        a = asyncio.ensure_future(h(1))
+        b = asyncio.ensure_future(h(2, ys=3))
+        await settle()
+        assert isinstance(a.exception(), ValueError) and isinstance(b.exception(), ValueError)
+    run(main)
+
+
+def test_generator_early_termination_per_caller():
+    @serve.batch(max_batch_size=2, batch_wait_timeout_s=0.1)
+    async def gen(ns):
+        for i in range(max(ns)):
+            yield [i if i < n else StopIteration for n in ns]
+
+    async def main(loop):
+        async def consume(n):
+            return [x async for x in gen(n)]
+        a = asyncio.ensure_future(consume(2))
+        b = asyncio.ensure_future(consume(4))
+        await settle(40)
+        assert a.result() == [0, 1] and b.result() == [0, 1, 2, 3]
+    run(main)
+
+
+def test_generator_consumer_stops_early_others_unaffected():
+    @serve.batch(max_batch_size=2, batch_wait_timeout_s=0.1)
+    async def gen(ns):
+        for i in range(5):
+            yield [i * n for n in ns]
+
+    async def main(loop):
+        async def first_only(n):
+            async for x in gen(n):
+                return x
+        async def all_items(n):
+            return [x async for x in gen(n)]
+        a = asyncio.ensure_future(first_only(1))
+        b = asyncio.ensure_future(all_items(2))
+        await settle(40)
+        assert a.result() == 0 and b.result() == [0, 2, 4, 6, 8]
+    run(main)
+
+
+def test_generator_error_after_partial_items():
+    @serve.batch(max_batch_size=2, batch_wait_timeout_s=0.1)
+    async def gen(ns):
+        yield list(ns)
+        raise RuntimeError("mid-stream")
+
+    async def main(loop):
+        async def consume(n):
+            got = []
+            try:
+                async for x in gen(n):
+                    got.append(x)
+            except RuntimeError:
+                return got, "error"
+            return got, "ok"
+        ts = [asyncio.ensure_future(consume(i)) for i in (7, 8)]
+        await settle(40)
+        assert [t.result() for t in ts] == [([7], "error"), ([8], "error")]
+    run(main)
+
+
+def test_instances_do_not_share_batches():
+    class M:
+        def __init__(self, k):
+            self.k = k
+            self.sizes = []
+
+        @serve.batch(max_batch_size=4, batch_wait_timeout_s=0.1)
+        async def __call__(self, xs):
+            self.sizes.append(len(xs))
+            return [x * self.k for x in xs]
+
+    async def main(loop):
+        m1, m2 = M(1), M(100)
+        ts = [asyncio.ensure_future(m(i)) for i in range(2) for m in (m1, m2)]
+        await settle()
+        await advance(loop, 0.2)
+        assert [t.result() for t in ts] == [0, 0, 1, 100]
+        assert m1.sizes == [2] and m2.sizes == [2]
+    run(main)
+
+
+def test_many_callers_form_full_batches():
+    f, sizes = _collector(max_batch_size=10, timeout=1.0)
+
+    async def main(loop):
+        ts = [asyncio.ensure_future(f(i)) for i in range(100)]
+        await settle(60)
+        assert sizes == [10] * 10
+        assert [t.result() for t in ts] == [i * 10 for i in range(100)]
+    run(main)
+
+
+def test_iteration_start_hook_and_task_alive():
+    release = None
+
+    @serve.batch(max_batch_size=1, batch_wait_timeout_s=0.0)
+    async def slow(xs):
+        await release.wait()
+        return xs
+
+    async def main(loop):
+        nonlocal release
+        release = asyncio.Event()
+        t = asyncio.ensure_future(slow(1))
+        await settle()
+        assert slow._get_curr_iteration_start_times() == [loop.time()]
+        assert slow._is_batching_task_alive()
+        release.set()
+        await settle()
+        assert t.result() == 1 and slow._get_curr_iteration_start_times() == [None]
+    run(main)

@@ -144,3 +144,70 @@ def test_controller_recovery_disabled(tmp_path, monkeypatch):
     assert serve.get_app_handle("d1").remote(1).result(timeout_s=10) == 2
     doc = serve.api._controller().read_checkpoint()
     assert "d1" in doc["applications"] and doc["applications"]["d1"]["app"].get("pickle")
+
+
+@serve.deployment(num_replicas=3, max_ongoing_requests=8)
+class MuxModels:
+    def __init__(self):
+        self.loads = 0
+
+    @serve.multiplexed(max_num_models_per_replica=2)
+    async def get_model(self, model_id):
+        self.loads += 1
+        return f"{model_id}@{os.getpid()}"
+
+    async def __call__(self):
+        return await self.get_model(serve.get_multiplexed_model_id())
+
+    def num_loads(self):
+        return self.loads
+
+
+def test_process_mode_multiplexed_affinity_through_native_router():
+    """Replicas publish the multiplexed ids they hold into their shm queue
+    state; the native router sends a request for a held id to that replica
+    (reference pow_2_scheduler.py:396-443), so each model loads once."""
+    h = serve.run(MuxModels.bind(), name="mux", mode="process")
+    where = {}
+    for rnd in range(6):
+        for mid in ("m1", "m2", "m3"):
+            out = h.options(multiplexed_model_id=mid).remote().result(timeout_s=30)
+            assert out.startswith(mid + "@")
+            where.setdefault(mid, set()).add(out)
+            time.sleep(0.01)
+    assert all(len(v) == 1 for v in where.values()), where      # every id stuck to one replica
+    total = sum(h.num_loads.remote().result(timeout_s=10) for _ in range(30))
+    # num_loads is routed to random replicas; the sum over replicas is 3 (one load per id)
+    ctrl = serve.api._controller()
+    job = ctrl.jobs["mux"]
+    held = [job.queue_models(q) for q in range(3)]
+    assert sorted(len(x) for x in held) in ([0, 1, 2], [1, 1, 1]) and sum(len(x) for x in held) == 3
+    assert total > 0
+
+
+def test_process_mode_replica_logs_and_access_log(tmp_path):
+    """Replica processes write their component log + access log per
+    logging_config; user records on the 'ray.serve' logger land there too."""
+    import json as _json
+
+    @serve.deployment(num_replicas=1, logging_config={"encoding": "JSON", "logs_dir": str(tmp_path)})
+    class Logged:
+        def __call__(self, x):
+            import logging as _logging
+
+            _logging.getLogger("ray.serve").info("handling %s", x)
+            return x + 1
+
+    h = serve.run(Logged.bind(), name="lg", mode="process")
+    assert [h.remote(i).result(timeout_s=30) for i in range(3)] == [1, 2, 3]
+    path = tmp_path / "replica_lg_Logged_0.log"
+    deadline = time.time() + 10
+    while time.time() < deadline:
+        lines = [_json.loads(x) for x in path.read_text().splitlines()] if path.exists() else []
+        if sum("latency_ms" in x for x in lines) >= 3:
+            break
+        time.sleep(0.1)
+    access = [x for x in lines if "latency_ms" in x]
+    assert len(access) == 3 and all(x["status"] == "OK" and x["method"] == "__call__" for x in access)
+    assert sum(x["message"].startswith("handling") for x in lines) == 3
+    assert any("replica starting" in x["message"] for x in lines)

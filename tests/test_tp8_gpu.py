@@ -166,9 +166,12 @@ def _llama_worker(rank, world, port, q):
     try:
         m = LlamaTP(_tp8_cfg(), rank, world, group_name="tp", device="cuda", backend="hip", init="full")
         ids = m.example_input(2, seed=3)
-        x = m.hidden_states(ids).float().cpu()
+        xv = m.hidden_states(ids)
+        torch.cuda.synchronize()
+        x = xv.float().cpu()
+        err = m._xgmi().error() if world > 1 else 0
         tok = m(ids).cpu()
-        q.put((rank, (x[:, :64].tolist(), tok.tolist())))
+        q.put((rank, (x[:, :64].tolist(), tok.tolist(), err)))
     except BaseException as e:  # noqa: BLE001
         q.put((rank, repr(e)))
         raise
@@ -186,7 +189,10 @@ def test_llama_tp8_matches_tp1():
     got = _spawn(_llama_worker, 8)
     for r in range(8):
         assert not isinstance(got[r], str), got[r]
+    assert all(got[r][2] == 0 for r in range(8)), [got[r][2] for r in range(8)]   # no barrier timed out
     h = {r: torch.tensor(got[r][0]) for r in range(8)}
+    zero = [r for r in range(8) if not h[r].abs().sum()]
+    assert not zero, f"ranks with all-zero hidden states: {zero}"
     for r in range(1, 8):
         assert torch.equal(h[0], h[r])             # every TP rank holds the same x
     href = torch.tensor(ref[0])
