@@ -59,6 +59,11 @@ Variant pp(const char* nm) {
                                                                    ACT_NONE, s);
           }};
 }
+Variant e8(const char* nm) {
+  return {nm, [](const bf16* A, const bf16* W, const bf16* b, bf16* C, int M, int N, int K, hipStream_t s) {
+            launch_gemm_8ph<bf16, bf16>(A, K, W, K, C, N, b, nullptr, 0, M, N, K, 1.f, ACT_NONE, s);
+          }};
+}
 // one production-kernel tile, instantiated alone (core() instantiates the whole tile table)
 template <int BM, int BN, int WGM, int NW>
 Variant core1(const char* nm) {

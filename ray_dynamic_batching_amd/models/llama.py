@@ -69,6 +69,10 @@ class LlamaTP:
         self.rank, self.tp = tp_rank, tp_size
         self.group = group_name
         self.use_xgmi = True          # custom xGMI all-reduce when the group has one (collective.enable_xgmi)
+        # called before every xGMI all-reduce of an EAGER forward (tests that run
+        # several TP ranks on ONE GPU: a rank spinning in the all-reduce kernel
+        # can hold the CU slots a peer's GEMM needs, so they line up first)
+        self.pre_collective = None
         self.device = torch.device(device)
         self.dtype = dtype
         self.backend = backend
@@ -209,9 +213,13 @@ class LlamaTP:
             ops.rope_(qkv, self.cos, self.sin, B, S, self.Hl, self.Hkvl, Dh)
             a = ops.attention(qkv, B, S, self.Hl, self.Hkvl, Dh, causal=True)
             o = ops.linear(a, L["w_o"], residual=x if first else None)
+            if self.pre_collective is not None:
+                self.pre_collective()
             x, h = xg.all_reduce_rmsnorm(o, L["mlp_norm"], c.eps)
             g = ops.linear(h, L["w_gu"], act="swiglu")
             d = ops.linear(g, L["w_down"], residual=x if first else None)
+            if self.pre_collective is not None:
+                self.pre_collective()
             if i + 1 < n:
                 x, h = xg.all_reduce_rmsnorm(d, self.layers[i + 1]["attn_norm"], c.eps)
             else:

@@ -864,6 +864,7 @@ mfma_gemm_kernel(typename LoaderT<T, 1>::Params ap, const T* __restrict__ W, int
 
 }  // namespace rdb
 #include "gemm_pp.h"
+#include "gemm_8ph.h"
 namespace rdb {
 
 // Tile table (index = the `cfg` argument): BM x BN with WGM waves along M.

@@ -22,7 +22,9 @@ import torch
 
 class TPReplica:
     def __init__(self, model, job_name: Optional[str], replica: int, queue: int, buckets: List[int],
-                 group: Optional[str] = None, max_wait_s: float = 0.002):
+                 group: Optional[str] = None, max_wait_s: float = 0.002, use_graphs: bool = True):
+        """``use_graphs=False`` runs each batch eagerly instead of replaying the
+        bucket's hipGraph (tests with several TP ranks sharing one GPU)."""
         from ..parallel import collective as col
 
         self.model = model
@@ -50,8 +52,13 @@ class TPReplica:
             self.cons = rjob.Consumer(self.job, [queue])
         self.batches = 0
         self.requests = 0
+        self.use_graphs = use_graphs
 
     def capture(self) -> "TPReplica":
+        if not self.use_graphs:
+            if self.job is not None:
+                self.job.set_replica_status(self.replica, 2, torch.cuda.current_device(), 0)
+            return self
         with torch.no_grad():
             for b in self.buckets:
                 x = self.ids[b]
@@ -108,7 +115,11 @@ class TPReplica:
             return 0
         if self.world > 1:
             self.col.broadcast(self.ids[b], 0, self.group)
-        self.graphs[b].replay()
+        if self.use_graphs:
+            self.graphs[b].replay()
+        else:
+            with torch.no_grad():
+                self.out[b] = self.model(self.ids[b])
         xg = self.col.get_xgmi(self.group) if self.world > 1 else None
         if xg is not None:
             # a timed-out xGMI barrier leaves partial sums in this replay's output:

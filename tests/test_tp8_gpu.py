@@ -51,6 +51,14 @@ def _digest(t):
     return hashlib.sha1(t.contiguous().view(torch.int16).cpu().numpy().tobytes()).hexdigest()
 
 
+def _log(rank, msg):
+    """Progress to stderr (visible with -s; keeps long multi-process GPU runs observably alive)."""
+    import sys
+    import time
+
+    print(f"[tp8 rank {rank} {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def _spawn(target, world, *args):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -76,6 +84,7 @@ def _allreduce_worker(rank, world, port, q):
 
     torch.cuda.set_device(0)
     col.init_collective_group(world, rank, backend="gloo", group_name="tp")
+    _log(rank, "allreduce worker ready")
     res = []
     try:
         xg = col.enable_xgmi("tp", max_elems=1 << 21, timeout_s=20.0)
@@ -152,6 +161,20 @@ def _tp8_cfg():
     return LlamaConfig.tiny(heads=8, kv_heads=8, head_dim=64, hidden=512, intermediate=1024, vocab_size=1024)
 
 
+def _line_up():
+    """Eight TP ranks share ONE GPU here: a rank already spinning in the xGMI
+    all-reduce kernel holds wave slots / VGPRs that a peer's 8-wave GEMM needs
+    to reach the same all-reduce, so before each all-reduce every rank drains
+    its stream and meets the others (gloo).  On an 8-GPU node each rank has its
+    own GPU and nothing is lined up."""
+    import torch
+
+    from ray_dynamic_batching_amd.parallel import collective as col
+
+    torch.cuda.synchronize()
+    col.barrier("tp")
+
+
 def _llama_worker(rank, world, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     import torch
@@ -160,14 +183,20 @@ def _llama_worker(rank, world, port, q):
     from ray_dynamic_batching_amd.parallel import collective as col
 
     torch.cuda.set_device(0)
+    _log(rank, "started")
     if world > 1:
         col.init_collective_group(world, rank, backend="gloo", group_name="tp")
         col.enable_xgmi("tp", max_elems=1 << 20, timeout_s=20.0)
+    _log(rank, "group ready")
     try:
         m = LlamaTP(_tp8_cfg(), rank, world, group_name="tp", device="cuda", backend="hip", init="full")
+        if world > 1:
+            m.pre_collective = _line_up
         ids = m.example_input(2, seed=3)
+        _log(rank, "model built")
         xv = m.hidden_states(ids)
         torch.cuda.synchronize()
+        _log(rank, "forward done")
         x = xv.float().cpu()
         err = m._xgmi().error() if world > 1 else 0
         tok = m(ids).cpu()
@@ -211,15 +240,21 @@ def _replica_worker(rank, world, port, q, job_name, n_prompts):
     from ray_dynamic_batching_amd.runtime.tp_replica import TPReplica
 
     torch.cuda.set_device(0)
+    _log(rank, "replica worker started")
     col.init_collective_group(world, rank, backend="gloo", group_name="tp")
     col.enable_xgmi("tp", max_elems=1 << 20, timeout_s=20.0)
     try:
         m = LlamaTP(_tp8_cfg(), rank, world, group_name="tp", device="cuda", backend="hip", init="full")
-        rep = TPReplica(m, job_name if rank == 0 else None, 0, 0, [1, 2, 4, 8], group="tp").capture()
+        m.pre_collective = _line_up
+        _log(rank, "model built")
+        # eager batches (no bucket graphs): a graph replay cannot line the ranks up
+        rep = TPReplica(m, job_name if rank == 0 else None, 0, 0, [1, 2, 4, 8], group="tp",
+                        use_graphs=False).capture()
         served = 0
         if rank == 0:
             while served < n_prompts:
                 served += max(0, rep.step(0.05))
+                _log(rank, f"served {served}")
             rep.stop_all()
         else:
             while rep.step(0.05) >= 0:
