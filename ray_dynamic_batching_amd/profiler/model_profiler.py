@@ -194,10 +194,12 @@ class ModelProfiler:
         return results
 
     def save_results(self, results: List[dict], model_name: str = "unnamed_model", model_info: dict = None,
-                     dataset_info: dict = None) -> dict:
+                     dataset_info: dict = None, plot: bool = True) -> dict:
         ts = datetime.now().strftime("%Y%m%d_%H%M%S")
         base = os.path.join(self.output_dir, f"{model_name}_{ts}")
         paths = dict(report=base + "_report.txt", json=base + "_detailed.json", csv=base + "_summary.csv")
+        if plot and plot_results(results, base + "_plot.png", title=model_name):
+            paths["plot"] = base + "_plot.png"
         write_profile_csv(paths["csv"], results)
         full = dict(model_name=model_name, timestamp=ts, device=self.gpu_info, model_info=model_info or {},
                     dataset_info=dataset_info or {}, mode=self.mode, include_h2d=self.include_h2d,
@@ -208,6 +210,42 @@ class ModelProfiler:
         with open(paths["report"], "w") as f:
             f.write(ResultsFormatter.format(full))
         return paths
+
+
+def plot_results(results: List[dict], path: str, title: str = "") -> bool:
+    """The reference's 4-panel figure (293-project/profiling/run_profiler.py:
+    110-156): throughput, latency, peak memory and per-item efficiency vs batch
+    size.  Returns False when matplotlib is unavailable or nothing succeeded."""
+    ok = [r for r in results if r.get("status") == "success"]
+    if not ok:
+        return False
+    try:
+        import matplotlib
+
+        matplotlib.use("Agg")
+        import matplotlib.pyplot as plt
+    except ImportError:
+        return False
+    bs = [r["batch_size"] for r in ok]
+    thr = [r["throughput"] for r in ok]
+    panels = [("Throughput vs Batch Size", "Throughput (samples/sec)", thr, "b-"),
+              ("Latency vs Batch Size", "Latency (ms)", [r["avg_latency_ms"] for r in ok], "r-"),
+              ("Memory Usage vs Batch Size", "Peak Memory (MB)", [r["peak_memory_mb"] for r in ok], "g-"),
+              ("Efficiency vs Batch Size", "Throughput per Batch Item", [t / b for t, b in zip(thr, bs)], "m-")]
+    fig, axes = plt.subplots(2, 2, figsize=(15, 10))
+    for ax, (ttl, ylab, ys, style) in zip(axes.flat, panels):
+        ax.plot(bs, ys, style)
+        ax.set_title(ttl)
+        ax.set_xlabel("Batch Size")
+        ax.set_ylabel(ylab)
+        ax.grid(True)
+    if title:
+        fig.suptitle(title)
+    fig.tight_layout()
+    os.makedirs(os.path.dirname(path) or ".", exist_ok=True)
+    fig.savefig(path)
+    plt.close(fig)
+    return True
 
 
 class ResultsFormatter:

@@ -126,6 +126,14 @@ class EngineRunner:
                 else self.compute_streams == 1
             if os.environ.get("RDB_FOLD_LN") in ("0", "1"):      # A/B override
                 m.fold_ln = os.environ["RDB_FOLD_LN"] == "1"
+        if getattr(m, "fuse_residual_ln", False) and self.compute_streams > 1:
+            # the LayerNorm GEMM epilogue's row-panel wait assumes the whole grid
+            # is resident; a second compute stream sharing the CUs breaks that
+            # (a timed-out wait would give a wrong LayerNorm): refuse it here
+            import warnings
+
+            warnings.warn("RDB_BERT_LNOUT needs compute_streams == 1; using the LayerNorm kernels")
+            m.fuse_residual_ln = False
         if hasattr(m, "refresh_folded_weights"):
             m.refresh_folded_weights()   # graphs capture weights derived from the CURRENT ones
         buckets = sorted(set(s.buckets or default_buckets(s.max_batch)))
@@ -155,6 +163,7 @@ class EngineRunner:
                 for _ in range(self.warmup_iters):
                     m.forward(s.inputs[0][:b])
         side.synchronize()
+        self.check_model_errors(m)
         if self.tune_in_context and not self._tune_loaded and not live:
             ctx_streams = int(os.environ.get("RDB_TUNE_CONTEXT_STREAMS", self.compute_streams))
             self.tuning_changes.update(self._tune_in_context(m, s.inputs[0][:buckets[-1]], dev, ctx_streams))
@@ -192,6 +201,20 @@ class EngineRunner:
                     g.replay()
             side.synchronize()
             self.engine.set_latency_estimate(s.sid, bi, (time.perf_counter() - t) / 3 * 1e3)
+        self.check_model_errors(m)
+
+    def check_model_errors(self, m=None) -> None:
+        """Raise if a kernel reported a silent-wrong-result condition: the
+        LayerNorm GEMM epilogue's bounded row-panel wait timed out (its output
+        is then wrong, ops.ln_out_error).  Run after warm-up, after the latency
+        replays, and periodically by the replica process."""
+        models = [m] if m is not None else [s.model for s in self.sessions if s.model is not None]
+        if any(getattr(x, "fuse_residual_ln", False) for x in models):
+            from .. import ops
+
+            if ops.ln_out_error(self.device):
+                raise RuntimeError("LayerNorm GEMM epilogue: a row-panel wait timed out (wrong LayerNorm); "
+                                   "run without RDB_BERT_LNOUT")
 
     def add_session(self, spec: SessionSpec, activate: bool = True) -> int:
         """Load a model into the RUNNING engine (planner placement): capture its

@@ -114,6 +114,11 @@ def _run_engine(spec, cfg, job, r, stop) -> int:
     runner.start()   # sets the replica READY in shm
     while not stop.is_set():
         err = runner.error()
+        if not err:
+            try:
+                runner.check_model_errors()
+            except RuntimeError as e:
+                err = str(e)
         if err:
             logger.error("engine error: %s", err)
             return 2

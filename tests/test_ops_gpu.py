@@ -533,3 +533,35 @@ def test_layer_norm_row_strided_view_and_embed_zeroes_stats():
     y = ops.embed_ln(ids, word, pos, typ, g, b, zero_stats=st)
     _close(y, ops.embed_ln_ref(ids, word, pos, typ, g, b), 2e-2, 2e-2)
     assert st.abs().max().item() == 0.0
+
+
+@pytest.mark.parametrize("readback", ["sdma", "blit"])
+def test_graph_replayed_plain_store_kernel_visible_to_d2h(readback):
+    """A graph-replayed kernel writing with plain (L2 write-back) stores -- a
+    GEMM with the staged epilogue -- must be read back correctly by the
+    device->host copy that follows, replay after replay with new inputs:
+    the regression guard for the xGMI fused-norm readback finding
+    (parallel/xgmi.py norm_store).  ``blit``: read through a device-side copy
+    kernel first (what a copy engine that bypassed the L2 would not see)."""
+    ops = _ops()
+    torch.manual_seed(0)
+    M, N, K = 4096, 768, 768
+    x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    w = torch.randn(N, K, device="cuda", dtype=torch.bfloat16) * (K ** -0.5)
+    b = torch.randn(N, device="cuda", dtype=torch.bfloat16)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        ops.linear(x, w, b)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            y = ops.linear(x, w, b, act="gelu")
+    torch.cuda.synchronize()
+    for it in range(5):
+        x.copy_(torch.randn(M, K, device="cuda", dtype=torch.bfloat16))
+        torch.cuda.synchronize()
+        g.replay()
+        torch.cuda.synchronize()
+        got = (y.clone() if readback == "blit" else y).cpu()
+        ref = ops.linear_ref(x, w, b, act="gelu").cpu()
+        _close(got, ref, 2e-2, 2e-2)

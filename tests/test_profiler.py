@@ -22,6 +22,8 @@ def test_profiler_cpu_writes_planner_contract(tmp_path):
     plan = SquishyPlanner({"mlp": prof}).plan([Session("mlp", 100.0, 500.0)])
     assert len(plan) >= 1
     assert "Best throughput" in open(paths["report"]).read()
+    # the reference's 4-panel figure (run_profiler.py:110-156)
+    assert os.path.getsize(paths["plot"]) > 10_000 and open(paths["plot"], "rb").read(4) == b"\x89PNG"
 
 
 def test_profiler_stops_after_three_failures(tmp_path):

@@ -183,6 +183,9 @@ def _llama_worker(rank, world, port, q):
     from ray_dynamic_batching_amd.parallel import collective as col
 
     torch.cuda.set_device(0)
+    import faulthandler
+
+    faulthandler.dump_traceback_later(120, exit=True)     # a stuck rank shows where, then exits
     _log(rank, "started")
     if world > 1:
         col.init_collective_group(world, rank, backend="gloo", group_name="tp")
@@ -240,6 +243,9 @@ def _replica_worker(rank, world, port, q, job_name, n_prompts):
     from ray_dynamic_batching_amd.runtime.tp_replica import TPReplica
 
     torch.cuda.set_device(0)
+    import faulthandler
+
+    faulthandler.dump_traceback_later(240, exit=True)
     _log(rank, "replica worker started")
     col.init_collective_group(world, rank, backend="gloo", group_name="tp")
     col.enable_xgmi("tp", max_elems=1 << 20, timeout_s=20.0)

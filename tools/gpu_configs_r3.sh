@@ -1,6 +1,7 @@
 # Round-3 evidence for BASELINE configs 2 / 3 / 4: TP=8 tests on one GPU, BERT bs16 and ResNet-50 bs32
 # tile tables, the ResNet-50 Poisson serving curve, and the conv kernels' counters.
 set -o pipefail
+bash tools/fresh.sh || exit 9
 mkdir -p gpurun_out/cfg
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 timeout -k 10 700 python -u -m pytest tests/test_tp8_gpu.py -x -v --timeout 600 --timeout-method thread -p no:cacheprovider -s -k "llama or replica" > gpurun_out/cfg/tp8.log 2>&1
