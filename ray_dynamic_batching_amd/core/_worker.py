@@ -20,6 +20,7 @@ from multiprocessing.connection import Listener
 
 TERMINATE = "__rdb_terminate__"
 PING = "__rdb_ping__"
+DAG_EXEC = "__rdb_dag_exec__"       # start a compiled-DAG execution loop (core/channel.py)
 
 
 def _reply(conn, lock, msg) -> None:
@@ -66,6 +67,15 @@ def serve_calls(instance, listener: Listener, max_concurrency: int, stop: thread
                     os._exit(0)
                 if method == PING:
                     _reply(conn, lock, (call_id, True, os.getpid()))
+                    continue
+                if method == DAG_EXEC:
+                    from .channel import start_exec_loop
+
+                    try:
+                        start_exec_loop(instance, args[0])
+                        _reply(conn, lock, (call_id, True, os.getpid()))
+                    except BaseException as e:  # noqa: BLE001
+                        _reply(conn, lock, (call_id, False, (RuntimeError(str(e)), traceback.format_exc())))
                     continue
                 pool.submit(run, conn, lock, call_id, method, args, kwargs)
         finally:

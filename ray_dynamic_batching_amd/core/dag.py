@@ -18,9 +18,12 @@ parallelism.  Here:
   the stages like microbatches in 1F1B.  ``teardown()`` waits for in-flight
   executions and rejects new ones.
 
-Values move actor -> driver -> actor over the core actor channels; GPU tensors
-between replicas move with ``parallel.collective`` send / recv (RCCL over
-xGMI), not through the DAG.
+Compiled DAGs move values over shared-memory channels (``core/channel.py``,
+reference ``experimental/channel/shared_memory_channel.py``): each edge is a
+native shm ring, each actor runs an execution loop over its nodes, and only
+the DAG's inputs and outputs touch the driver.  ``_channel="driver"`` keeps the
+interpreted path (values hop actor -> driver -> actor).  GPU tensors between
+replicas move with ``parallel.collective`` send / recv (RCCL over xGMI).
 """
 from __future__ import annotations
 
@@ -40,7 +43,14 @@ class DAGNode:
     def execute(self, *args, **kwargs):
         return _Schedule(self).run(args, kwargs, None)
 
-    def experimental_compile(self, _max_inflight_executions: int = 10, **_ignored) -> "CompiledDAG":
+    def experimental_compile(self, _max_inflight_executions: int = 10, _buffer_size_bytes: int = 1 << 20,
+                             _channel: str = "shm", **_ignored) -> "CompiledDAG":
+        """``_channel="shm"`` (default): every edge becomes a shared-memory
+        channel and each actor runs an execution loop (values never pass
+        through the driver); ``"driver"``: the interpreted schedule replayed
+        per execution (values hop through the driver)."""
+        if _channel == "shm":
+            return ChannelCompiledDAG(self, _max_inflight_executions, _buffer_size_bytes)
         return CompiledDAG(self, _max_inflight_executions)
 
 
@@ -236,3 +246,165 @@ class CompiledDAG:
         self._closed = True
         with self._cv:
             self._cv.wait_for(lambda: self._inflight == 0, timeout)
+
+
+class ChannelCompiledDAG:
+    """A compiled DAG on shared-memory channels (see module doc)."""
+
+    def __init__(self, root: DAGNode, max_inflight: int, buffer_size: int):
+        import collections
+        import uuid
+
+        from . import _local_actors
+        from ..runtime import job as rjob
+        from .channel import ChannelReader, ChannelWriter, start_exec_loop
+        from ._worker import DAG_EXEC
+
+        if max_inflight < 1:
+            raise ValueError("_max_inflight_executions must be >= 1")
+        sched = _Schedule(root)
+        if not any(isinstance(n, InputNode) for n in sched.order):
+            raise ValueError("a compiled DAG needs an InputNode")
+        nodes = [n for n in sched.order if isinstance(n, ClassMethodNode)]
+        if not nodes:
+            raise ValueError("a compiled DAG needs at least one actor method node")
+        outs = root.outputs if isinstance(root, MultiOutputNode) else [root]
+        if not all(isinstance(o, ClassMethodNode) for o in outs):
+            raise ValueError("compiled DAG outputs must be actor method nodes")
+        nq = [0]
+        producers: Dict[int, List[int]] = collections.defaultdict(list)
+        self._inputs: List[Tuple[int, DAGNode]] = []      # driver-written channels
+
+        def chan(a: DAGNode) -> Tuple[str, int]:
+            q = nq[0]
+            nq[0] += 1
+            if isinstance(a, (InputNode, InputAttributeNode)):
+                self._inputs.append((q, a))
+            elif isinstance(a, ClassMethodNode):
+                producers[id(a)].append(q)
+            else:
+                raise ValueError(f"unsupported DAG argument node {type(a).__name__}")
+            return ("chan", q)
+
+        specs = []
+        for n in nodes:
+            args = [chan(a) if isinstance(a, DAGNode) else ("const", a) for a in n.args]
+            kwargs = {k: (chan(a) if isinstance(a, DAGNode) else ("const", a)) for k, a in n.kwargs.items()}
+            specs.append((n, args, kwargs))
+        self._outputs = []
+        for o in outs:
+            q = nq[0]
+            nq[0] += 1
+            producers[id(o)].append(q)
+            self._outputs.append(q)
+        self.multi = isinstance(root, MultiOutputNode)
+        cap = 4
+        while cap < max_inflight + 2:
+            cap *= 2
+        self.job_name = rjob.unique_job_name("dag")
+        actors = {n.method._handle._actor_id: n.method._handle for n in nodes}
+        self.job = rjob.Job(self.job_name, create=True, n_replicas=1, n_queues=nq[0], n_clients=len(actors) + 2,
+                            req_capacity=cap, req_slot_bytes=buffer_size + 64, cmp_capacity=4, cmp_slot_bytes=64)
+        per_actor: Dict[str, List[dict]] = collections.defaultdict(list)
+        for n, args, kwargs in specs:
+            in_q = [a[1] for a in args if a[0] == "chan"] + [a[1] for a in kwargs.values() if a[0] == "chan"]
+            per_actor[n.method._handle._actor_id].append(dict(method=n.method._name, args=args, kwargs=kwargs,
+                                                             in_queues=in_q, out_queues=producers[id(n)]))
+        self._local_stops = []
+        try:
+            pending = []
+            for aid, ops in per_actor.items():
+                plan = dict(job=self.job_name, ops=ops)
+                if aid in _local_actors:
+                    self._local_stops.append(start_exec_loop(_local_actors[aid][0], plan))
+                else:
+                    pending.append(actors[aid]._call_now(DAG_EXEC, (plan,), {}))
+            for ref in pending:
+                ref._fut.result(60)
+        except BaseException:
+            self.job.close()
+            raise
+        self._client = rjob.Client(self.job)
+        self._writers = [(ChannelWriter(self.job, q, self._client), src) for q, src in self._inputs]
+        self._readers = [ChannelReader(self.job, q) for q in self._outputs]
+        self._slots = threading.BoundedSemaphore(max_inflight)
+        self._pending: "collections.deque" = collections.deque()
+        self._cv = threading.Condition()
+        self._stop = threading.Event()
+        self._closed = False
+        self._reader = threading.Thread(target=self._collect, daemon=True, name="rdb-dag-out")
+        self._reader.start()
+
+    @staticmethod
+    def _input_value(src: DAGNode, args, kwargs):
+        whole = args[0] if len(args) == 1 and not kwargs else _Args(args, kwargs)
+        if isinstance(src, InputNode):
+            return whole
+        if isinstance(whole, _Args):
+            return whole.args[src.key] if isinstance(src.key, int) else whole.kwargs[src.key]
+        return whole[src.key] if src.how == "item" else getattr(whole, src.key)
+
+    def execute(self, *args, **kwargs):
+        if self._closed:
+            raise RayError("this compiled DAG was torn down")
+        self._slots.acquire()
+        futs = [Future() for _ in self._readers]
+        with self._cv:
+            self._pending.append(futs)
+            self._cv.notify_all()
+        for w, src in self._writers:
+            try:
+                v = ("val", self._input_value(src, args, kwargs))
+            except Exception as e:  # noqa: BLE001
+                v = ("err", RayError(f"DAG input has no {getattr(src, 'key', '?')!r}: {e}"))
+            w.write(v[0], v[1], self._stop)
+        refs = [ObjectRef(f) for f in futs]
+        return refs if self.multi else refs[0]
+
+    def _collect(self) -> None:
+        while True:
+            with self._cv:
+                while not self._pending and not self._stop.is_set():
+                    self._cv.wait(0.1)
+                if not self._pending:
+                    return
+                futs = self._pending[0]
+            msgs = []
+            for r in self._readers:
+                m = r.read(self._stop)
+                if m is None:
+                    return
+                msgs.append(m)
+            with self._cv:
+                self._pending.popleft()
+            for f, (kind, val) in zip(futs, msgs):
+                if kind == "val":
+                    f.set_result(val)
+                elif kind == "err":
+                    f.set_exception(val)
+                else:
+                    f.set_exception(RayError("compiled DAG stopped"))
+            self._slots.release()
+
+    def teardown(self, timeout: Optional[float] = 30.0) -> None:
+        if self._closed:
+            return
+        self._closed = True
+        import time as _t
+
+        t_end = _t.monotonic() + (timeout or 30.0)
+        with self._cv:
+            while self._pending and _t.monotonic() < t_end:
+                self._cv.wait(0.05)
+        for w, _src in self._writers:
+            try:
+                w.write("stop", None, None, timeout_s=5.0)
+            except Exception:  # noqa: BLE001
+                pass
+        for r in self._readers:          # loops forward STOP to the outputs once they have drained
+            r.read(None, timeout_s=max(0.1, t_end - _t.monotonic()))
+        self._stop.set()
+        for s in self._local_stops:
+            s.set()
+        self._reader.join()          # it polls the stop flag: never unmap under a reading thread
+        self.job.close()
