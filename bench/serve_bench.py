@@ -43,6 +43,12 @@ def main(argv=None):
     from ray_dynamic_batching_amd.runtime.engine import EngineRunner, SessionSpec
 
     torch.cuda.set_device(0)
+    # replay the tile table shipped for this (model, max batch, depth) when there is one
+    # (ops/tuned/README.md); RDB_TUNE_FILE set by the caller wins
+    shipped = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "ray_dynamic_batching_amd",
+                           "ops", "tuned", f"mi355x_{a.model}_B{a.max_batch}_d{a.pipeline_depth}.json")
+    if a.backend == "hip" and "RDB_TUNE_FILE" not in os.environ and os.path.exists(shipped):
+        os.environ["RDB_TUNE_FILE"] = shipped
     m = models.create(a.model, device="cuda", backend=a.backend)
     in_bytes = int(np.prod(m.input_shape)) * torch.tensor([], dtype=m.input_dtype).element_size()
     name = rjob.unique_job_name("sbench")
@@ -84,6 +90,7 @@ def main(argv=None):
         runner.stop()
         j.close()
     out = {"model": a.model, "backend": a.backend, "max_batch": a.max_batch, "max_wait_ms": a.max_wait_ms,
+           "tile_table": os.path.basename(os.environ.get("RDB_TUNE_FILE", "")) or "tuned at start-up",
            "points": points}
     if a.json_out:
         with open(a.json_out, "w") as f:

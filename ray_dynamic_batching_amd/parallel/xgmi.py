@@ -91,16 +91,16 @@ class XgmiCommunicator:
         self._owns = owns
         self.calls = 0
         self.poisoned = False
-        # Store flavour of the fused-norm output: 0 plain, 1 nontemporal, 2 write-through (sc1).
-        # Write-through is the default: with plain (L2 write-back) stores a graph-replayed call
-        # left most of its norm rows unwritten as seen by a following device->host copy, on
-        # every XCD, while the bit-exact sum (uncached gather buffer) was fine; nontemporal
-        # stores failed the same way; write-through fixed it (tools/gpu_xgmi_diag.sh, the
-        # per-block launch records show every block ran with the right pointers).  The
-        # write-through store costs the same as a plain 16-B store (MI355X_MICROARCH.md).
+        # Store flavour of the fused-norm output: 0 plain (default), 1 nontemporal, 2
+        # write-through (sc1).  Plain stores keep the normalised rows in the XCD's L2
+        # for the GEMM that reads them next.  (Round 2 made sc1 the default after a
+        # graph-replay test read "unwritten" rows; tools/gpu_xgmi_cause*.sh showed the
+        # rows were unwritten because the two in-process ranks' streams shared one
+        # hardware queue and the barrier timed out -- every store flavour and both
+        # copy engines pass once the ranks run concurrently, tests/test_xgmi_gpu.py.)
         import os
 
-        self.norm_store = int(os.environ.get("RDB_XGMI_NORM_STORE", "2"))
+        self.norm_store = int(os.environ.get("RDB_XGMI_NORM_STORE", "0"))
         self.debug_ptr = 0          # set by enable_debug(): per-block launch-view records
 
     # -- construction ---------------------------------------------------------

@@ -39,10 +39,18 @@ _STREAMS = []
 
 
 def _streams(n):
-    """Ranks in one process need truly concurrent streams: the box has 4 HW
-    queues per process (GPU_MAX_HW_QUEUES), so create 2 once and reuse them."""
+    """Ranks in one process need truly concurrent streams.  Two streams of one
+    priority can share a hardware queue (the box has 4 per process,
+    GPU_MAX_HW_QUEUES, assigned round-robin -- which one depends on every
+    stream the process created before): rank 1's kernel then starts only after
+    rank 0's has timed out in its barrier (error 1, rows never written).  That
+    was the round-2 "unwritten fused-norm rows" finding: it followed the test
+    ORDER, not the store flavour or the copy engine (tools/gpu_xgmi_cause*.sh).
+    Streams of DIFFERENT priorities always get different hardware queues."""
+    if n > 2:
+        raise ValueError("in-process ranks: at most 2 (one stream per priority level)")
     while len(_STREAMS) < n:
-        _STREAMS.append(torch.cuda.Stream())
+        _STREAMS.append(torch.cuda.Stream(priority=-len(_STREAMS)))
     return _STREAMS[:n]
 
 
@@ -81,23 +89,24 @@ def test_xgmi_local_group_matches_fp32_sum(world, T, D, two_shot):
             c.close()
 
 
+@pytest.mark.parametrize("norm_store", [0, 1, 2])
 @pytest.mark.parametrize("prealloc", [False, True])
-def test_xgmi_local_group_graph_replay(prealloc):
+def test_xgmi_local_group_graph_replay(prealloc, norm_store):
     """The kernel keeps its epochs in device memory, so a captured call
     replays correctly (what the TP replica's per-bucket hipGraphs rely on).
 
-    Run after the ops kernel tests in the same process, this used to read most
-    of rank 0's fused-norm rows of the FIRST replay as never written (sentinel /
-    zeros) while the all-reduced sum was bit-exact.  The per-block launch
-    records (enable_debug) showed every block ran with the right pointers and
-    epoch; the norm output written through (sc1) instead of L2 write-back
-    stores fixed it, so that is the communicator's default (norm_store=2)."""
+    Every store flavour of the fused-norm output (plain -- the default --,
+    nontemporal, write-through) is checked; the ranks' streams have different
+    priorities so they run concurrently whatever ran before in this process
+    (see _streams: the round-2 "unwritten rows" were a barrier timeout of two
+    ranks sharing one hardware queue).  A barrier timeout fails with its cause."""
     from ray_dynamic_batching_amd.parallel.xgmi import XgmiCommunicator
 
     world, T, D, eps = 2, 64, 4096, 1e-5
     comms = XgmiCommunicator.local_group(world, max_elems=T * D, timeout_s=5.0)
     for c in comms:
         c.enable_debug()
+        c.norm_store = norm_store
     streams = _streams(world)
     xs, gamma = _inputs(world, T, D)
     dx = [x.cuda() for x in xs]
@@ -123,7 +132,7 @@ def test_xgmi_local_group_graph_replay(prealloc):
             torch.cuda.synchronize()
             ref_s, ref_h = _reference(xs, gamma, eps)
             for r in range(world):
-                assert comms[r].error() == 0
+                assert comms[r].error() == 0, "barrier timed out: the in-process ranks did not run concurrently"
                 assert torch.equal(outs[r][0].cpu(), ref_s)
                 h = outs[r][1].cpu().float()
                 bad = ((h - ref_h.float()).abs() > 2e-2 + 2e-2 * ref_h.float().abs()).any(1)

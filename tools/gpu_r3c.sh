@@ -1,0 +1,3 @@
+set -o pipefail
+bash tools/gpu_xgmi_cause2.sh
+bash tools/gpu_configs_r3.sh
