@@ -67,7 +67,28 @@ struct Session {
   int priority = 0;
   int64_t slo_ns = 0;
   bool drop_stale = false;
-  std::vector<double> est_ns;                        // per bucket service estimate
+  // per-bucket service estimates, written by the completer thread and read by
+  // the launcher: est_ns is the GPU time of a batch that ran ALONE (seeded by
+  // the latency replays, refined only by batches that overlapped no other
+  // batch) and drives duty-cycle charging / backfill; est_wall_ns is the EMA of
+  // the event-timed span under whatever overlap the compute streams had and
+  // drives stale dropping (when a request would actually complete)
+  std::unique_ptr<std::atomic<double>[]> est_ns, est_wall_ns;
+  size_t n_est = 0;
+  void reset_estimates(size_t n) {
+    n_est = n;
+    est_ns.reset(new std::atomic<double>[n]);
+    est_wall_ns.reset(new std::atomic<double>[n]);
+    for (size_t i = 0; i < n; ++i) {
+      est_ns[i].store(0.0, std::memory_order_relaxed);
+      est_wall_ns[i].store(0.0, std::memory_order_relaxed);
+    }
+  }
+  double est(int bi) const { return est_ns[bi].load(std::memory_order_relaxed); }
+  double est_wall(int bi) const {
+    const double w = est_wall_ns[bi].load(std::memory_order_relaxed);
+    return w > 0.0 ? w : est(bi);
+  }
   std::vector<std::vector<hipGraphExec_t>> graphs;   // [bucket][slot]
   std::vector<std::vector<uintptr_t>> out_dev;       // [bucket][slot]
   std::vector<uintptr_t> in_dev;                     // [slot]
@@ -105,6 +126,8 @@ struct InFlight {
   std::vector<uint64_t> req_pos;        // ring positions of the requests in batch order
   int64_t t_form_start = 0, t_launch = 0;
   bool gpu = false;
+  bool solo = false;     // no other GPU batch in flight when this one launched
+  uint64_t seq = 0;      // launch sequence number (launch_seq_ after this launch)
 };
 
 class Engine {
@@ -210,7 +233,7 @@ class Engine {
     s.priority = priority;
     s.slo_ns = (int64_t)(slo_ms * 1e6);
     s.drop_stale = drop_stale;
-    s.est_ns.assign(buckets.size(), 0.0);
+    s.reset_estimates(buckets.size());
     s.graphs.assign(buckets.size(), std::vector<hipGraphExec_t>(depth_, nullptr));
     s.out_dev.assign(buckets.size(), std::vector<uintptr_t>(depth_, 0));
     s.in_dev.assign(depth_, 0);
@@ -261,7 +284,7 @@ class Engine {
     s.priority = priority;
     s.slo_ns = (int64_t)(slo_ms * 1e6);
     s.drop_stale = drop_stale;
-    s.est_ns.assign(buckets.size(), 0.0);
+    s.reset_estimates(buckets.size());
     s.graphs.assign(buckets.size(), std::vector<hipGraphExec_t>(depth_, nullptr));
     s.out_dev.assign(buckets.size(), std::vector<uintptr_t>(depth_, 0));
     s.in_dev.assign(depth_, 0);
@@ -312,7 +335,17 @@ class Engine {
     s.graphs.at(bucket_idx).at(slot) = reinterpret_cast<hipGraphExec_t>(graph_exec);
     s.out_dev.at(bucket_idx).at(slot) = out_dev;
   }
-  void set_latency_estimate(int sid, int bucket_idx, double ms) { sess(sid).est_ns.at(bucket_idx) = ms * 1e6; }
+  void set_latency_estimate(int sid, int bucket_idx, double ms) {
+    Session& s = sess(sid);
+    if (bucket_idx < 0 || (size_t)bucket_idx >= s.n_est) throw std::out_of_range("bucket index");
+    s.est_ns[bucket_idx].store(ms * 1e6, std::memory_order_relaxed);
+  }
+  // (solo, wall) service estimates of one bucket in ms
+  std::pair<double, double> latency_estimate(int sid, int bucket_idx) {
+    Session& s = sess(sid);
+    if (bucket_idx < 0 || (size_t)bucket_idx >= s.n_est) throw std::out_of_range("bucket index");
+    return {s.est(bucket_idx) / 1e6, s.est_wall(bucket_idx) / 1e6};
+  }
   // Nexus duty cycle (policy 1): every `cycle_ms` each session may use `share_ms`
   // of GPU time (= occupancy x duty cycle); budgets reset at the cycle boundary.
   void set_duty_share(int sid, double ms) { sess(sid).duty_share_ns = (int64_t)(ms * 1e6); }
@@ -476,7 +509,7 @@ class Engine {
         if (!h) continue;
         const uint64_t depth = s.ring.h->head.load(std::memory_order_relaxed) - s.peek_pos;
         const int bi = bucket_for(s, (int)std::min<uint64_t>(depth, (uint64_t)s.max_batch));
-        if ((double)left < s.est_ns[bi]) continue;
+        if ((double)left < s.est(bi)) continue;
         const double key = (double)s.used_ns / (double)std::max<int64_t>(1, s.duty_share_ns) +
                            1e-12 * (double)(h->t_submit_ns & 0xFFFFFFF);  // tie-break: older head first
         if (key < best_key) {
@@ -599,7 +632,7 @@ class Engine {
           int64_t dl = h->deadline_ns;
           if (!dl && s.drop_stale && s.slo_ns) dl = h->t_submit_ns + s.slo_ns;
           if (dl) {
-            const double est = s.est_ns[bucket_for(s, std::min(s.max_batch, n + 1))];
+            const double est = s.est_wall(bucket_for(s, std::min(s.max_batch, n + 1)));
             if ((double)now_ns() + est > (double)dl) {
               write_completion(h, s.queue, ST_DROPPED_STALE, nullptr, 0, now_ns());
               dropped_.fetch_add(1, std::memory_order_relaxed);
@@ -656,7 +689,7 @@ class Engine {
                                    reinterpret_cast<void*>(s.out_dev[bi][slot]),
                                    (size_t)n * s.out_row_bytes, hipMemcpyDeviceToHost, cs));
           ENG_CHECK(hipEventRecord(ev_done_[slot], cs));
-          s.used_ns += (int64_t)s.est_ns[bi];
+          s.used_ns += (int64_t)s.est(bi);
           padded_.fetch_add(rows - n, std::memory_order_relaxed);
           roctxRangePop();
         }
@@ -664,6 +697,11 @@ class Engine {
         {
           std::lock_guard<std::mutex> lk(mu_);
           slot_busy_[slot] = true;
+          if (f.gpu) {
+            f.solo = gpu_inflight_ == 0;
+            f.seq = launch_seq_.fetch_add(1, std::memory_order_acq_rel) + 1;
+            ++gpu_inflight_;
+          }
           inflight_.push_back(std::move(f));
         }
         cv_.notify_all();
@@ -706,9 +744,18 @@ class Engine {
           if (hipEventElapsedTime(&ms, ev_start_[f.slot], ev_done_[f.slot]) == hipSuccess) {
             gpu_busy_ms_.store(gpu_busy_ms_.load() + ms);
             rs->busy_ns.fetch_add((uint64_t)(ms * 1e6), std::memory_order_relaxed);
-            // EMA of the service time of this bucket (drives stale dropping)
-            double& est = s.est_ns[f.bucket_idx];
-            est = est == 0.0 ? ms * 1e6 : 0.9 * est + 0.1 * ms * 1e6;
+            // EMAs of the service time of this bucket: the overlap-inflated
+            // span always, the solo estimate only from a batch that shared the
+            // GPU with no other batch from its launch to its completion
+            const double v = ms * 1e6;
+            std::atomic<double>& w = s.est_wall_ns[f.bucket_idx];
+            const double w0 = w.load(std::memory_order_relaxed);
+            w.store(w0 == 0.0 ? v : 0.9 * w0 + 0.1 * v, std::memory_order_relaxed);
+            const bool solo = f.solo && launch_seq_.load(std::memory_order_acquire) == f.seq;
+            std::atomic<double>& e = s.est_ns[f.bucket_idx];
+            const double e0 = e.load(std::memory_order_relaxed);
+            if (e0 == 0.0) e.store(v, std::memory_order_relaxed);
+            else if (solo) e.store(0.9 * e0 + 0.1 * v, std::memory_order_relaxed);
           }
           const char* out = reinterpret_cast<const char*>(s.host_out[f.slot]);
           const int64_t t_done = now_ns();
@@ -737,6 +784,7 @@ class Engine {
         {
           std::lock_guard<std::mutex> lk(mu_);
           slot_busy_[f.slot] = false;
+          if (f.gpu) --gpu_inflight_;
         }
         s.inflight.fetch_sub(1, std::memory_order_seq_cst);
         cv_.notify_all();
@@ -775,6 +823,8 @@ class Engine {
   std::mutex api_mu_;
   std::vector<bool> slot_busy_;
   std::deque<InFlight> inflight_;
+  int gpu_inflight_ = 0;                   // GPU batches launched and not yet completed (under mu_)
+  std::atomic<uint64_t> launch_seq_{0};    // GPU launches so far (solo detection)
   std::mutex mu_;
   std::condition_variable cv_;
   std::thread launcher_, completer_;
@@ -799,6 +849,7 @@ void register_engine(py::module_& m) {
       .def("set_input", &Engine::set_input)
       .def("set_graph", &Engine::set_graph)
       .def("set_latency_estimate", &Engine::set_latency_estimate)
+      .def("latency_estimate", &Engine::latency_estimate)
       .def("set_duty_share", &Engine::set_duty_share)
       .def("set_duty_cycle", &Engine::set_duty_cycle)
       .def("set_session_active", &Engine::set_session_active)

@@ -321,5 +321,13 @@ class EngineRunner:
     def stats(self):
         return self.engine.stats()
 
+    def latency_estimates(self, session: int = 0) -> dict:
+        """Per bucket size: (solo ms, overlapped-span ms).  The solo estimate
+        (latency replays, then batches that overlapped no other batch) charges
+        duty-cycle shares and gates backfill; the overlapped span EMA predicts
+        completion for stale-request dropping (engine.cpp Session::est_ns)."""
+        s = self.sessions[session]
+        return {b: tuple(self.engine.latency_estimate(s.sid, bi)) for bi, b in enumerate(s.buckets)}
+
     def error(self) -> str:
         return self.engine.error()

@@ -1,6 +1,7 @@
 """fp32_reference (models/reference.py) on CPU: the same weights upcast, the
 PyTorch path in fp32; cached kernel-layout weights dropped; the original
 model untouched."""
+import pytest
 import torch
 
 from ray_dynamic_batching_amd.models.reference import fp32_reference, rel_err
@@ -30,3 +31,16 @@ def test_fp32_reference_llama_cpu():
     h = r.hidden_states(ids)
     assert h.dtype == torch.float32
     assert rel_err(m.hidden_states(ids), h) < 5e-2
+
+
+def test_eager_reference_and_parity_bound_cpu():
+    from ray_dynamic_batching_amd.models.bert import BertConfig, BertForSequenceClassification
+    from ray_dynamic_batching_amd.models.reference import eager_reference, parity_bound
+
+    m = BertForSequenceClassification(BertConfig.tiny(seq_len=32), device="cpu", backend="torch", seed=2)
+    m._packed = "kernel-layout cache"
+    e = eager_reference(m)
+    assert e.backend == "torch" and e.dtype == torch.bfloat16 and e._packed is None and m._packed is not None
+    ids = m.example_input(4, seed=1)
+    assert torch.equal(e(ids), m(ids))                    # same dtype, same path: bit-identical
+    assert parity_bound(0.001) == 2e-2 and parity_bound(0.02) == pytest.approx(0.035)

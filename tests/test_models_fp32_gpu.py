@@ -7,7 +7,7 @@ percent fails it regardless of the logits' scale)."""
 import pytest
 import torch
 
-from ray_dynamic_batching_amd.models.reference import fp32_reference, rel_err
+from ray_dynamic_batching_amd.models.reference import eager_reference, fp32_reference, parity_bound, rel_err
 
 pytestmark = pytest.mark.gpu
 
@@ -27,7 +27,8 @@ def test_bert_hip_vs_fp32():
     y = m(ids)
     ref = fp32_reference(m)(ids)
     _nontrivial(ref)
-    assert rel_err(y, ref) <= BOUND, rel_err(y, ref)
+    bound = parity_bound(rel_err(eager_reference(m)(ids), ref))
+    assert rel_err(y, ref) <= bound, (rel_err(y, ref), bound)
 
 
 def test_bert_base_full_depth_hip_vs_fp32():
@@ -39,7 +40,8 @@ def test_bert_base_full_depth_hip_vs_fp32():
     y = m(ids)
     ref = fp32_reference(m)(ids)
     _nontrivial(ref)
-    assert rel_err(y, ref) <= BOUND, rel_err(y, ref)
+    bound = parity_bound(rel_err(eager_reference(m)(ids), ref))
+    assert rel_err(y, ref) <= bound, (rel_err(y, ref), bound)
 
 
 def test_resnet50_hip_vs_fp32():

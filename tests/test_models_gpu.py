@@ -218,6 +218,12 @@ def test_engine_concurrent_streams_match_single_stream():
         out = torch.stack([torch.tensor(struct.unpack("<2f", got[i])) for i in range(200)])
         assert torch.allclose(out, ref, atol=2e-2, rtol=2e-2), (out - ref).abs().max()
         assert runner.error() == ""
+        # service estimates: the solo one stays seeded from the latency replays
+        # (batches overlapped each other), the overlapped span was measured
+        est = runner.latency_estimates()
+        assert set(est) == set(runner.sessions[0].buckets)
+        solo, wall = est[8]
+        assert solo > 0 and wall > 0
     finally:
         runner.stop()
         j.close()
