@@ -21,6 +21,7 @@ from multiprocessing.connection import Listener
 TERMINATE = "__rdb_terminate__"
 PING = "__rdb_ping__"
 DAG_EXEC = "__rdb_dag_exec__"       # start a compiled-DAG execution loop (core/channel.py)
+DAG_SETUP = "__rdb_dag_setup__"     # allocate a compiled DAG's inbound tensor rings (core/channel.py)
 
 
 def _reply(conn, lock, msg) -> None:
@@ -67,6 +68,14 @@ def serve_calls(instance, listener: Listener, max_concurrency: int, stop: thread
                     os._exit(0)
                 if method == PING:
                     _reply(conn, lock, (call_id, True, os.getpid()))
+                    continue
+                if method == DAG_SETUP:
+                    from .channel import create_rings
+
+                    try:
+                        _reply(conn, lock, (call_id, True, create_rings(*args)))
+                    except BaseException as e:  # noqa: BLE001
+                        _reply(conn, lock, (call_id, False, (RuntimeError(str(e)), traceback.format_exc())))
                     continue
                 if method == DAG_EXEC:
                     from .channel import start_exec_loop

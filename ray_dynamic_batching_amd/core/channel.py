@@ -10,8 +10,19 @@ Here a channel is one request ring of a native job segment
 (``runtime/csrc/shm.h``: MPSC ring, seq-numbered slots, futex doorbell); the
 writer is a native ``Client`` (``submit``), the reader a native ``Consumer``
 (``pop``).  Values are cloudpickled into the slot (``buffer_size_bytes`` per
-value); GPU tensors between replicas travel with ``parallel.collective`` (RCCL
-over xGMI), not through a channel.
+value).
+
+Tensor edges (reference ``experimental/channel/torch_tensor_type.py``,
+``torch_tensor_nccl_channel.py``): a node marked
+``.with_tensor_transport()`` / ``.with_type_hint(TorchTensorType())`` ships
+the torch tensors inside its values through a ``TensorRing`` owned by the
+channel's READER -- device memory exported once with HIP IPC for GPU tensors
+(the writer's copy goes HBM -> HBM, over xGMI when the reader sits on a peer
+GPU), a POSIX shared-memory segment for host tensors -- and only a small
+descriptor (slot offset, dtype, shape) travels through the shm ring.  A ring
+has ``ring capacity + 2`` slots: at most ``capacity`` messages are queued, one
+more is being cloned out by the reader and one is being written, so a slot is
+never overwritten while it is still read.
 """
 from __future__ import annotations
 
@@ -21,6 +32,241 @@ import traceback
 from typing import Any, Dict, List, Optional, Tuple
 
 STOP = ("stop",)
+_ALIGN = 256                          # tensor placement inside a ring slot
+
+
+class TorchTensorType:
+    """Type hint of a DAG edge whose values carry torch tensors (reference
+    ``ray.experimental.channel.torch_tensor_type.TorchTensorType``).
+    ``transport``: "auto" / "device" / "nccl" -- GPU tensors through the
+    reader's device ring (HIP IPC; xGMI between GPUs), host tensors through a
+    shared-memory ring; "shm" -- the same, host tensors only (GPU tensors are
+    pickled inline)."""
+
+    def __init__(self, transport: str = "auto", _static_shape: bool = False, _direct_return: bool = False):
+        if transport not in ("auto", "device", "nccl", "shm"):
+            raise ValueError(f"unknown tensor transport {transport!r}")
+        self.transport = transport
+
+    def __repr__(self):
+        return f"TorchTensorType(transport={self.transport!r})"
+
+
+class _TRef:
+    """Descriptor of a tensor placed in a ring slot."""
+    __slots__ = ("dev", "off", "nbytes", "dtype", "shape")
+
+    def __init__(self, dev, off, nbytes, dtype, shape):
+        self.dev, self.off, self.nbytes, self.dtype, self.shape = dev, off, nbytes, dtype, shape
+
+    def __reduce__(self):
+        return (_TRef, (self.dev, self.off, self.nbytes, self.dtype, self.shape))
+
+
+class _PtrArray:
+    def __init__(self, ptr: int, n: int):
+        self.__cuda_array_interface__ = {"shape": (n,), "typestr": "|u1", "data": (ptr, False), "version": 3,
+                                         "strides": None}
+
+
+_RINGS: Dict[Tuple[str, int, str], "TensorRing"] = {}     # this process's rings by (job, queue, dev)
+_RING_LOCK = threading.Lock()
+
+
+class TensorRing:
+    """``slots`` x ``slot_bytes`` staging buffer for one channel's tensors.
+    ``dev="cuda"``: device memory of the creating process's current GPU
+    (``xgmi_alloc_uncached``, exported with hipIpcGetMemHandle); ``"cpu"``: a
+    POSIX shared-memory segment.  Created by the reader, attached by the
+    writer from ``export()``."""
+
+    def __init__(self, job: str, queue: int, dev: str, slots: int, slot_bytes: int, _attach: Optional[dict] = None):
+        import os
+
+        import torch
+
+        self.job, self.queue, self.dev = job, queue, dev
+        self.slots, self.slot_bytes = int(slots), int(slot_bytes)
+        n = self.slots * self.slot_bytes
+        self._shm = None
+        self._ptr = 0
+        self._owner = _attach is None
+        self.pid = os.getpid() if _attach is None else _attach["pid"]
+        if dev == "cpu":
+            from multiprocessing import shared_memory
+
+            if _attach is None:
+                self._shm = shared_memory.SharedMemory(create=True, size=n)
+            else:
+                self._shm = shared_memory.SharedMemory(name=_attach["name"])
+                _untrack(self._shm)
+            self.buf = torch.frombuffer(self._shm.buf, dtype=torch.uint8, count=n)
+        else:
+            from .. import ops
+
+            o = ops._ops()
+            if _attach is None:
+                self._ptr = o.xgmi_alloc_uncached(n)
+                self._handle = o.xgmi_ipc_handle(self._ptr)
+            else:
+                self._ptr = o.xgmi_ipc_open(_attach["handle"])
+            self.buf = torch.as_tensor(_PtrArray(self._ptr, n), device=torch.device("cuda", torch.cuda.current_device()))
+
+    def export(self) -> dict:
+        d = dict(job=self.job, queue=self.queue, dev=self.dev, slots=self.slots, slot_bytes=self.slot_bytes,
+                 pid=self.pid)
+        if self.dev == "cpu":
+            d["name"] = self._shm.name
+        else:
+            d["handle"] = self._handle
+        return d
+
+    @staticmethod
+    def attach(desc: dict) -> "TensorRing":
+        import os
+
+        key = (desc["job"], desc["queue"], desc["dev"])
+        if desc["pid"] == os.getpid():                  # same process (local-mode actor, driver)
+            with _RING_LOCK:
+                return _RINGS[key]
+        return TensorRing(desc["job"], desc["queue"], desc["dev"], desc["slots"], desc["slot_bytes"], _attach=desc)
+
+    def slot(self, seq: int):
+        base = (seq % self.slots) * self.slot_bytes
+        return self.buf[base:base + self.slot_bytes]
+
+    def close(self) -> None:
+        self.buf = None
+        if self._shm is not None:
+            try:
+                self._shm.close()
+                if self._owner:
+                    self._shm.unlink()
+            except (OSError, BufferError):
+                pass
+            self._shm = None
+        if self._ptr:
+            from .. import ops
+
+            o = ops._ops()
+            try:
+                if self._owner:
+                    import torch
+
+                    torch.cuda.synchronize()
+                    o.xgmi_free(self._ptr)
+                else:
+                    o.xgmi_ipc_close(self._ptr)
+            except Exception:  # noqa: BLE001 - teardown
+                pass
+            self._ptr = 0
+
+
+def _untrack(shm) -> None:
+    """An attached segment is the creator's to unlink: keep this process's
+    resource tracker from unlinking it at exit."""
+    try:
+        from multiprocessing import resource_tracker
+
+        resource_tracker.unregister(shm._name, "shared_memory")   # noqa: SLF001
+    except Exception:  # noqa: BLE001
+        pass
+
+
+def create_rings(job: str, specs: List[Tuple[int, int, int]], devs: Tuple[str, ...]) -> Dict[int, Dict[str, dict]]:
+    """Reader side: allocate the rings of this process's inbound tensor
+    channels; ``specs`` = [(queue, slots, slot_bytes)]. Returns
+    {queue: {dev: export}}."""
+    import torch
+
+    out: Dict[int, Dict[str, dict]] = {}
+    for q, slots, nbytes in specs:
+        out[q] = {}
+        for dev in devs:
+            if dev == "cuda" and not torch.cuda.is_available():
+                continue
+            r = TensorRing(job, q, dev, slots, nbytes)
+            with _RING_LOCK:
+                _RINGS[(job, q, dev)] = r
+            out[q][dev] = r.export()
+    return out
+
+
+def release_rings(job: str, queues: Optional[List[int]] = None) -> None:
+    """Free this process's rings of ``job`` (only those of ``queues`` if given)."""
+    with _RING_LOCK:
+        keys = [k for k in _RINGS if k[0] == job and (queues is None or k[1] in queues)]
+        rings = [_RINGS.pop(k) for k in keys]
+    for r in rings:
+        r.close()
+
+
+def _walk(v, fn):
+    """Rebuild ``v`` with ``fn`` applied to every leaf of lists / tuples / dicts."""
+    if isinstance(v, list):
+        return [_walk(x, fn) for x in v]
+    if isinstance(v, tuple) and type(v) is tuple:
+        return tuple(_walk(x, fn) for x in v)
+    if isinstance(v, dict) and type(v) is dict:
+        return {k: _walk(x, fn) for k, x in v.items()}
+    return fn(v)
+
+
+def encode_tensors(value, rings: Dict[str, "TensorRing"], seq: int):
+    """Writer side: copy every tensor of ``value`` whose device has a ring into
+    slot ``seq`` of that ring and replace it with a descriptor."""
+    import torch
+
+    used = {d: 0 for d in rings}
+    sync = [False]
+
+    def put(x):
+        if not isinstance(x, torch.Tensor):
+            return x
+        dev = "cuda" if x.is_cuda else "cpu"
+        ring = rings.get(dev)
+        if ring is None:
+            return x
+        nbytes = x.numel() * x.element_size()
+        off = used[dev]
+        if off + nbytes > ring.slot_bytes:
+            raise ValueError(f"tensors of {off + nbytes} bytes exceed the channel's {ring.slot_bytes}-byte slot "
+                             "(compile with a larger _buffer_size_bytes)")
+        used[dev] = (off + nbytes + _ALIGN - 1) // _ALIGN * _ALIGN
+        if nbytes:
+            src = x.detach().contiguous().reshape(-1).view(torch.uint8)
+            ring.slot(seq)[off:off + nbytes].copy_(src)
+            sync[0] |= dev == "cuda"
+        return _TRef(dev, off, nbytes, x.dtype, tuple(x.shape))
+
+    out = _walk(value, put)
+    if sync[0]:
+        torch.cuda.current_stream().synchronize()     # the bytes land before the descriptor is sent
+    return out
+
+
+def decode_tensors(value, rings: Dict[str, "TensorRing"], seq: int):
+    """Reader side: materialise the descriptors of slot ``seq`` as tensors
+    owned by this process (cloned out of the ring before the slot is reused)."""
+    import torch
+
+    sync = [False]
+
+    def get(x):
+        if not isinstance(x, _TRef):
+            return x
+        ring = rings[x.dev]
+        if x.nbytes == 0:
+            t = torch.empty(x.shape, dtype=x.dtype, device=ring.buf.device)
+        else:
+            t = ring.slot(seq)[x.off:x.off + x.nbytes].view(x.dtype).view(x.shape).clone()
+        sync[0] |= x.dev == "cuda"
+        return t
+
+    out = _walk(value, get)
+    if sync[0]:
+        torch.cuda.current_stream().synchronize()     # cloned out before the next message frees the slot
+    return out
 
 
 def _pack(kind: str, value: Any = None) -> bytes:
@@ -36,12 +282,23 @@ def _unpack(b: bytes):
 
 
 class ChannelWriter:
-    def __init__(self, job, queue: int, client):
+    def __init__(self, job, queue: int, client, rings: Optional[Dict[str, dict]] = None):
         self.job, self.queue, self.client = job, queue, client
         self.client_max = int(job.info()["req_payload_bytes"])
+        self.rings = {d: TensorRing.attach(desc) for d, desc in (rings or {}).items()}
+        self.seq = 0
 
     def write(self, kind: str, value: Any = None, stop: Optional[threading.Event] = None,
               timeout_s: float = 60.0) -> None:
+        seq = self.seq
+        self.seq += 1                     # every message takes a slot number (reader counts the same way)
+        if self.rings and kind == "val":
+            try:
+                value = encode_tensors(value, self.rings, seq)
+            except ValueError as e:
+                from . import RayError
+
+                kind, value = "err", RayError(str(e)[:512])
         data = _pack(kind, value)
         if kind == "err" and len(data) > self.client_max:
             from . import RayError
@@ -63,11 +320,14 @@ class ChannelWriter:
 
 
 class ChannelReader:
-    def __init__(self, job, queue: int):
+    def __init__(self, job, queue: int, job_name: str = ""):
         from ..runtime import job as rjob
 
         self.queue = queue
         self.cons = rjob.Consumer(job, [queue])
+        with _RING_LOCK:
+            self.rings = {k[2]: r for k, r in _RINGS.items() if k[0] == job_name and k[1] == queue}
+        self.seq = 0
 
     def read(self, stop: Optional[threading.Event] = None, timeout_s: Optional[float] = None):
         """(kind, value) of the next message; None on stop / timeout."""
@@ -75,7 +335,12 @@ class ChannelReader:
         while True:
             got = self.cons.pop(1, 50_000_000)
             if got:
-                return _unpack(got[0][6])
+                seq = self.seq
+                self.seq += 1
+                kind, value = _unpack(got[0][6])
+                if self.rings and kind == "val":
+                    value = decode_tensors(value, self.rings, seq)
+                return kind, value
             if (stop is not None and stop.is_set()) or (t_end is not None and time.monotonic() > t_end):
                 return None
 
@@ -89,10 +354,11 @@ def exec_loop(instance, plan: Dict[str, Any], stop: threading.Event) -> None:
 
     job = rjob.Job(plan["job"], create=False)
     client = rjob.Client(job)
+    rings = plan.get("rings", {})
     ops = []
     for op in plan["ops"]:
-        readers = {q: ChannelReader(job, q) for q in op["in_queues"]}
-        writers = [ChannelWriter(job, q, client) for q in op["out_queues"]]
+        readers = {q: ChannelReader(job, q, plan["job"]) for q in op["in_queues"]}
+        writers = [ChannelWriter(job, q, client, rings.get(q)) for q in op["out_queues"]]
         ops.append((op, readers, writers))
     try:
         while not stop.is_set():
@@ -136,7 +402,19 @@ def exec_loop(instance, plan: Dict[str, Any], stop: threading.Event) -> None:
 
                         w.write("err", RayError(str(e)[:512]), stop)
     finally:
+        for _op, _r, writers in ops:
+            for w in writers:
+                for r in w.rings.values():
+                    if not r._owner and r.pid != _getpid():
+                        r.close()
+        release_rings(plan["job"], [q for op, _r, _w in ops for q in op["in_queues"]])
         job.close()
+
+
+def _getpid() -> int:
+    import os
+
+    return os.getpid()
 
 
 async def _await(aw):

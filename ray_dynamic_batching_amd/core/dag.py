@@ -22,8 +22,13 @@ Compiled DAGs move values over shared-memory channels (``core/channel.py``,
 reference ``experimental/channel/shared_memory_channel.py``): each edge is a
 native shm ring, each actor runs an execution loop over its nodes, and only
 the DAG's inputs and outputs touch the driver.  ``_channel="driver"`` keeps the
-interpreted path (values hop actor -> driver -> actor).  GPU tensors between
-replicas move with ``parallel.collective`` send / recv (RCCL over xGMI).
+interpreted path (values hop actor -> driver -> actor).  A node marked
+``.with_tensor_transport()`` (or ``.with_type_hint(TorchTensorType())``,
+reference ``dag_node.py`` ``with_tensor_transport`` / ``with_type_hint``)
+sends the torch tensors of its values through the reader's staging ring --
+GPU memory exported with HIP IPC (device-to-device copies, over xGMI between
+GPUs), shared memory for host tensors -- with only descriptors in the shm
+ring (``core/channel.py`` ``TensorRing``).
 """
 from __future__ import annotations
 
@@ -32,13 +37,30 @@ from concurrent.futures import Future
 from typing import Any, Dict, List, Optional, Sequence, Tuple
 
 from . import ObjectRef, RayError, _ActorMethod
+from .channel import TorchTensorType
 
-__all__ = ["DAGNode", "InputNode", "InputAttributeNode", "ClassMethodNode", "MultiOutputNode", "CompiledDAG"]
+__all__ = ["DAGNode", "InputNode", "InputAttributeNode", "ClassMethodNode", "MultiOutputNode", "CompiledDAG",
+           "TorchTensorType"]
 
 
 class DAGNode:
+    _type_hint: Optional[TorchTensorType] = None
+
     def _deps(self) -> List["DAGNode"]:
         return []
+
+    def with_tensor_transport(self, transport: str = "auto", _static_shape: bool = False,
+                              _direct_return: bool = False) -> "DAGNode":
+        """Ship the torch tensors of this node's outputs through staging rings
+        (compiled DAGs; see core/channel.py).  Returns the node."""
+        self._type_hint = TorchTensorType(transport, _static_shape, _direct_return)
+        return self
+
+    def with_type_hint(self, hint) -> "DAGNode":
+        if hint is not None and not isinstance(hint, TorchTensorType):
+            raise TypeError("with_type_hint expects a TorchTensorType")
+        self._type_hint = hint
+        return self
 
     def execute(self, *args, **kwargs):
         return _Schedule(self).run(args, kwargs, None)
@@ -274,22 +296,33 @@ class ChannelCompiledDAG:
         nq = [0]
         producers: Dict[int, List[int]] = collections.defaultdict(list)
         self._inputs: List[Tuple[int, DAGNode]] = []      # driver-written channels
+        # tensor channels: queue -> (reader actor id or None = driver, ring devices)
+        tensor_q: Dict[int, Tuple[Optional[str], Tuple[str, ...]]] = {}
 
-        def chan(a: DAGNode) -> Tuple[str, int]:
+        def devs_of(a: DAGNode) -> Optional[Tuple[str, ...]]:
+            h = getattr(a, "_type_hint", None)
+            if h is None:
+                return None
+            return ("cpu",) if h.transport == "shm" else ("cpu", "cuda")
+
+        def chan(a: DAGNode, reader: Optional[str]) -> Tuple[str, int]:
             q = nq[0]
             nq[0] += 1
             if isinstance(a, (InputNode, InputAttributeNode)):
                 self._inputs.append((q, a))
             elif isinstance(a, ClassMethodNode):
                 producers[id(a)].append(q)
+                if devs_of(a):
+                    tensor_q[q] = (reader, devs_of(a))
             else:
                 raise ValueError(f"unsupported DAG argument node {type(a).__name__}")
             return ("chan", q)
 
         specs = []
         for n in nodes:
-            args = [chan(a) if isinstance(a, DAGNode) else ("const", a) for a in n.args]
-            kwargs = {k: (chan(a) if isinstance(a, DAGNode) else ("const", a)) for k, a in n.kwargs.items()}
+            rd = n.method._handle._actor_id
+            args = [chan(a, rd) if isinstance(a, DAGNode) else ("const", a) for a in n.args]
+            kwargs = {k: (chan(a, rd) if isinstance(a, DAGNode) else ("const", a)) for k, a in n.kwargs.items()}
             specs.append((n, args, kwargs))
         self._outputs = []
         for o in outs:
@@ -297,6 +330,8 @@ class ChannelCompiledDAG:
             nq[0] += 1
             producers[id(o)].append(q)
             self._outputs.append(q)
+            if devs_of(o):
+                tensor_q[q] = (None, devs_of(o))
         self.multi = isinstance(root, MultiOutputNode)
         cap = 4
         while cap < max_inflight + 2:
@@ -312,9 +347,22 @@ class ChannelCompiledDAG:
                                                              in_queues=in_q, out_queues=producers[id(n)]))
         self._local_stops = []
         try:
+            # tensor rings: allocated by each tensor channel's reader, attached by its writer
+            from .channel import create_rings
+            from ._worker import DAG_SETUP
+
+            slots = cap + 2
+            rings: Dict[int, Dict[str, dict]] = {}
+            for q, (rd, devs) in tensor_q.items():
+                spec = (self.job_name, [(q, slots, buffer_size)], devs)
+                if rd is None or rd in _local_actors:
+                    rings.update(create_rings(*spec))
+                else:
+                    rings.update(actors[rd]._call_now(DAG_SETUP, spec, {})._fut.result(60))
             pending = []
             for aid, ops in per_actor.items():
-                plan = dict(job=self.job_name, ops=ops)
+                outq = [q for op in ops for q in op["out_queues"]]
+                plan = dict(job=self.job_name, ops=ops, rings={q: rings[q] for q in outq if q in rings})
                 if aid in _local_actors:
                     self._local_stops.append(start_exec_loop(_local_actors[aid][0], plan))
                 else:
@@ -322,11 +370,14 @@ class ChannelCompiledDAG:
             for ref in pending:
                 ref._fut.result(60)
         except BaseException:
+            from .channel import release_rings
+
+            release_rings(self.job_name)
             self.job.close()
             raise
         self._client = rjob.Client(self.job)
         self._writers = [(ChannelWriter(self.job, q, self._client), src) for q, src in self._inputs]
-        self._readers = [ChannelReader(self.job, q) for q in self._outputs]
+        self._readers = [ChannelReader(self.job, q, self.job_name) for q in self._outputs]
         self._slots = threading.BoundedSemaphore(max_inflight)
         self._pending: "collections.deque" = collections.deque()
         self._cv = threading.Condition()
@@ -407,4 +458,7 @@ class ChannelCompiledDAG:
         for s in self._local_stops:
             s.set()
         self._reader.join()          # it polls the stop flag: never unmap under a reading thread
+        from .channel import release_rings
+
+        release_rings(self.job_name, list(self._outputs))
         self.job.close()

@@ -148,3 +148,79 @@ def test_compiled_dag_shm_channels_actor_to_actor(rt):
     drv = big.experimental_compile(_channel="driver")
     assert ray.get(drv.execute(4), timeout=30) == 6.0
     drv.teardown()
+
+
+class TensorStage:
+    def make(self, n):
+        import torch
+
+        return {"x": torch.arange(n, dtype=torch.float64), "meta": ("n", n), "ids": [torch.ones(3, dtype=torch.int64)]}
+
+    def total(self, d, scale=1.0):
+        assert d["meta"] == ("n", d["x"].numel())
+        return (d["x"] * scale).sum() + d["ids"][0].sum()
+
+    def big(self, n):
+        import torch
+
+        return torch.zeros(n, dtype=torch.float64)
+
+
+def test_compiled_dag_tensor_transport_host_ring(rt):
+    """``with_tensor_transport()``: the tensors of a node's values travel through
+    the reader's staging ring (here host shared memory: CPU tensors) and only
+    descriptors cross the shm ring (nested containers, mixed tensors and
+    plain values, an actor -> actor edge and an actor -> driver edge)."""
+    import torch
+
+    from ray_dynamic_batching_amd.core.dag import TorchTensorType
+
+    A = ray.remote(num_gpus=1)(TensorStage)
+    a, b = A.remote(), A.remote()
+    n = 24 * 1024                                       # 192 KB of tensor per value
+    with InputNode() as inp:
+        made = a.make.bind(inp).with_tensor_transport()
+        out = b.total.bind(made, scale=2.0).with_type_hint(TorchTensorType(transport="shm"))
+    cd = out.experimental_compile(_max_inflight_executions=3, _buffer_size_bytes=256 * 1024)
+    refs = [cd.execute(n + i) for i in range(8)]
+    for i, r in enumerate(refs):
+        got = ray.get(r, timeout=60)
+        assert isinstance(got, torch.Tensor) and float(got) == 2.0 * sum(range(n + i)) + 3
+    cd.teardown()
+    # a tensor larger than a ring slot fails that execution, loudly, and the next ones still run
+    with InputNode() as inp:
+        big = b.total.bind(a.make.bind(inp).with_tensor_transport())
+    small = big.experimental_compile(_max_inflight_executions=1, _buffer_size_bytes=64 * 1024)
+    with pytest.raises(Exception, match="slot|buffer"):
+        ray.get(small.execute(32 * 1024), timeout=30)
+    assert float(ray.get(small.execute(10), timeout=30)) == 45.0 + 3
+    small.teardown(timeout=5)
+    with pytest.raises(ValueError):
+        TorchTensorType(transport="carrier-pigeon")
+
+
+def test_tensor_ring_slot_reuse_protocol():
+    """Ring slots are indexed by message sequence number on both sides; a
+    value's tensors are cloned out, so a later write into the same slot does
+    not change a value already read."""
+    import torch
+
+    from ray_dynamic_batching_amd.core.channel import (TensorRing, _TRef, create_rings, decode_tensors,
+                                                       encode_tensors, release_rings)
+
+    job = "t" + uuid.uuid4().hex[:8]
+    exp = create_rings(job, [(0, 3, 4096)], ("cpu",))
+    w = {"cpu": TensorRing.attach(exp[0]["cpu"])}
+    r = {"cpu": w["cpu"]}
+    try:
+        enc = encode_tensors([torch.full((4,), 7.0), 5, torch.empty(0)], w, seq=4)
+        assert isinstance(enc[0], _TRef) and enc[1] == 5 and enc[2].nbytes == 0
+        import cloudpickle
+
+        assert len(cloudpickle.dumps(encode_tensors(torch.zeros(1000), w, seq=0))) < 300   # descriptor only
+        got = decode_tensors(enc, r, seq=4)
+        encode_tensors([torch.full((4,), -1.0)], w, seq=7)        # 7 % 3 == 4 % 3: same slot, rewritten
+        assert got[0].tolist() == [7.0] * 4 and got[2].numel() == 0
+        assert decode_tensors(enc, r, seq=7)[0].tolist() == [-1.0] * 4
+    finally:
+        release_rings(job)
