@@ -227,17 +227,20 @@ class BertForSequenceClassification:
         c = self.cfg
         B, S = ids.shape
         D, H = c.hidden, c.heads
-        lens = ops.seq_lens(ids, c.pad_token_id)
+        fuse = self.fuse_qkv_attn and ops.qkv_attention_supported(S, H, D // H, D)
+        # the fused kernel counts each sequence's key length from the ids itself
+        kid = (ids.contiguous(), c.pad_token_id) if fuse and ids.dtype == torch.int32 else None
+        lens = None if kid is not None else ops.seq_lens(ids, c.pad_token_id)
         n = len(self.layers)
         lnout = self.fuse_residual_ln and self.dtype == torch.bfloat16 and D % 8 == 0
         # row-panel LayerNorm workspaces, 2 per LNOUT GEMM: zeroed by the embedding kernel
         ws = torch.empty(4 * n, B * S, 2, device=ids.device, dtype=torch.float32) if lnout else None
         h = ops.embed_ln(ids, self.word, self.pos, self.typ, self.emb_g, self.emb_b, c.eps, zero_stats=ws)
-        fuse = self.fuse_qkv_attn and ops.qkv_attention_supported(S, H, D // H, D)
         packed = self._packed_qkv() if fuse else None
         for i, L in enumerate(self.layers):
             if fuse:   # one kernel: projection tile of (sequence, head) -> attention in LDS
-                ctx = ops.qkv_attention(h.reshape(B * S, D), packed[i][0], packed[i][1], B, S, H, lens=lens)
+                ctx = ops.qkv_attention(h.reshape(B * S, D), packed[i][0], packed[i][1], B, S, H, lens=lens,
+                                        key_ids=kid)
             else:
                 qkv = ops.linear(h, L["w_qkv"], L["b_qkv"])
                 ctx = ops.attention(qkv, B, S, H, H, D // H, lens=lens)

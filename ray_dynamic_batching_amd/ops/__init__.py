@@ -610,11 +610,15 @@ def qkv_attention_supported(S: int, H: int, D: int, K: int) -> bool:
 def qkv_attention(x: torch.Tensor, w_packed: torch.Tensor, b_packed: Optional[torch.Tensor], B: int, S: int, H: int,
                   lens: Optional[torch.Tensor] = None, scale: Optional[float] = None,
                   out: Optional[torch.Tensor] = None, cfg: int = -1, lna: Optional[tuple] = None,
-                  stats_out: Optional[torch.Tensor] = None) -> torch.Tensor:
+                  stats_out: Optional[torch.Tensor] = None, key_ids: Optional[tuple] = None) -> torch.Tensor:
     """Fused QKV projection + bidirectional attention (qkv_attention.hip):
     ctx [B*S, H*64] = MHA(x @ W^T + b) for S <= 128, head dim 64, with the
     projection weight in ``pack_qkv_heads`` layout.  The [B*S, 3*H*64] QKV
     activation is never materialised.
+
+    Key lengths: ``lens`` (int32 [B], e.g. ``seq_lens``) or ``key_ids=(ids,
+    pad_id)`` -- the kernel counts each sequence's non-pad tokens itself
+    (right padding, as ``seq_lens``), so no lengths kernel runs.
 
     ``lna=(colsum, bias_f32, eps)`` (packed order, f32): x holds RAW rows whose
     LayerNorm is folded into ``w_packed`` (``fold_ln_weights`` then packing);
@@ -645,13 +649,19 @@ def qkv_attention(x: torch.Tensor, w_packed: torch.Tensor, b_packed: Optional[to
     _check(x.stride(0) % 8 == 0 and _aligned(x) and _aligned(w_packed), "qkv_attention: alignment")
     if lens is not None:
         _check(lens.dtype == torch.int32 and lens.numel() == B and lens.is_cuda, "qkv_attention: lens must be int32 [B]")
+    kid, pad = None, 0
+    if key_ids is not None:
+        kid, pad = key_ids
+        _check(lens is None, "qkv_attention: pass lens or key_ids, not both")
+        _check(kid.dtype == torch.int32 and kid.is_cuda and kid.is_contiguous() and tuple(kid.shape) == (B, S),
+               "qkv_attention: key_ids must be contiguous int32 [B, S] on the GPU")
     if out is None:
         out = torch.empty(B * S, H * 64, device=x.device, dtype=x.dtype)
     _check(out.is_contiguous() and out.shape == (B * S, H * 64) and _aligned(out), "qkv_attention: bad out")
     scale = 1.0 / 8.0 if scale is None else scale
     args = (DTYPE_CODE[x.dtype], x.data_ptr(), x.stride(0), w_packed.data_ptr(), _ptr(b_packed), B, S, H, K,
             _ptr(lens), out.data_ptr(), H * 64, float(scale))
-    extra = (_ptr(cs), _ptr(bf), _ptr(stats_out), float(eps))
+    extra = (_ptr(cs), _ptr(bf), _ptr(stats_out), float(eps), _ptr(kid), int(pad))
     fn = _ops().qkv_attn_fwd
     if cfg < 0:
         key = ("qkv_attn", x.dtype, B, S, H, K, x.stride(0), lna is not None)

@@ -29,7 +29,7 @@ void attn_fwd(int dtype, uintptr_t qkv, int ld_qkv, int q_off, int k_off, int v_
               uintptr_t stream);
 void qkv_attn_fwd(int dtype, uintptr_t X, int ldx, uintptr_t Wp, uintptr_t bp, int B, int S, int H, int hidden,
                   uintptr_t lens, uintptr_t out, int ld_out, float scale, int cfg, uintptr_t stream,
-                  uintptr_t colsum, uintptr_t bias_f, uintptr_t stats_out, float eps);
+                  uintptr_t colsum, uintptr_t bias_f, uintptr_t stats_out, float eps, uintptr_t key_ids, int pad);
 void softmax_topk(uintptr_t x, int rows, int C, int k, uintptr_t probs, uintptr_t idx, uintptr_t stream);
 void rope(uintptr_t qkv, int ld, int q_off, int k_off, int H, int Hkv, int D, int S, uintptr_t cos_t,
           uintptr_t sin_t, int T, int pos_offset, uintptr_t stream);
@@ -82,8 +82,8 @@ PYBIND11_MODULE(_rdb_ops, m) {
   m.def("qkv_attn_fwd", &rdb::qkv_attn_fwd, py::arg("dtype"), py::arg("X"), py::arg("ldx"), py::arg("Wp"),
         py::arg("bp"), py::arg("B"), py::arg("S"), py::arg("H"), py::arg("hidden"), py::arg("lens"), py::arg("out"),
         py::arg("ld_out"), py::arg("scale"), py::arg("cfg"), py::arg("stream"), py::arg("colsum") = 0,
-        py::arg("bias_f") = 0, py::arg("stats_out") = 0, py::arg("eps") = 0.0f,
-        py::call_guard<py::gil_scoped_release>());
+        py::arg("bias_f") = 0, py::arg("stats_out") = 0, py::arg("eps") = 0.0f, py::arg("key_ids") = 0,
+        py::arg("pad") = 0, py::call_guard<py::gil_scoped_release>());
   m.def("softmax_topk", &rdb::softmax_topk, py::call_guard<py::gil_scoped_release>());
   m.def("rope", &rdb::rope, py::call_guard<py::gil_scoped_release>());
   m.def("gather_rows", &rdb::gather_rows, py::call_guard<py::gil_scoped_release>());

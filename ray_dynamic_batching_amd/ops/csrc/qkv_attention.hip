@@ -46,7 +46,8 @@ struct QkvLn {
 template <typename T, int NW, int STAGES, bool LNA, int WGM_ = (NW == 8 ? 4 : 2)>
 __global__ void __launch_bounds__(64 * NW, NW == 8 && STAGES == 3 ? 1 : 2)
 qkv_attn_kernel(DenseParams ap, const T* __restrict__ W, const T* __restrict__ bias, int S, int H,
-                const int* __restrict__ lens, T* __restrict__ out, int ld_out, float scale_log2e, QkvLn ln) {
+                const int* __restrict__ lens, T* __restrict__ out, int ld_out, float scale_log2e, QkvLn ln,
+                const int* __restrict__ kids, int pad) {
   constexpr int BM = 128, BN = 192, BK = 64, D = 64;
   constexpr int WGM = WGM_, WGN = NW / WGM_;
   constexpr int NT = 64 * NW;
@@ -129,8 +130,11 @@ qkv_attn_kernel(DenseParams ap, const T* __restrict__ W, const T* __restrict__ b
     }
   };
 
-  // key length of this sequence: fetched before the main loop, used after it
+  // key length of this sequence: fetched before the main loop, used after it --
+  // either a precomputed lens[b] or, with kids (the [B, S] token ids), counted
+  // here from the ids (non-pad tokens, right padding): no separate lengths kernel
   int kv_len = lens ? lens[b] : S;
+  const int kid = (kids != nullptr && tid < S) ? kids[(size_t)b * S + tid] : pad;
   const int nk = (K + BK - 1) / BK;
   if constexpr (STAGES == 2) {
     stage(0, 0);
@@ -159,6 +163,15 @@ qkv_attn_kernel(DenseParams ap, const T* __restrict__ W, const T* __restrict__ b
       buf = buf == 2 ? 0 : buf + 1;
     }
     __syncthreads();
+  }
+  if (kids != nullptr) {
+    __shared__ int s_cnt[NW];
+    const unsigned long long bal = __ballot(kid != pad);
+    if (lane == 0) s_cnt[wid] = __popcll(bal);
+    __syncthreads();
+    kv_len = 0;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) kv_len += s_cnt[w];
   }
   kv_len = kv_len < S ? (kv_len < 1 ? 1 : kv_len) : S;
   // LNA: per-row (mean, rstd) of this lane's rows; head 0 publishes the sums
@@ -314,24 +327,25 @@ constexpr int kNumQkvAttnCfgs = 4;
 
 template <typename T, bool LNA>
 static void launch_qkv_attn(int cfg, const DenseParams& p, const T* W, const T* bias, int B, int S, int H,
-                            const int* lens, T* out, int ld_out, float sl2e, const QkvLn& ln, hipStream_t s) {
+                            const int* lens, T* out, int ld_out, float sl2e, const QkvLn& ln, hipStream_t s,
+                            const int* kids, int pad) {
   const dim3 grid(B * H);
   switch (cfg) {
     case 0:
       hipLaunchKernelGGL((qkv_attn_kernel<T, 8, 3, LNA>), grid, dim3(512), 0, s, p, W, bias, S, H, lens, out, ld_out,
-                         sl2e, ln);
+                         sl2e, ln, kids, pad);
       break;
     case 1:
       hipLaunchKernelGGL((qkv_attn_kernel<T, 8, 2, LNA>), grid, dim3(512), 0, s, p, W, bias, S, H, lens, out, ld_out,
-                         sl2e, ln);
+                         sl2e, ln, kids, pad);
       break;
     case 3:
       hipLaunchKernelGGL((qkv_attn_kernel<T, 8, 2, LNA, 2>), grid, dim3(512), 0, s, p, W, bias, S, H, lens, out,
-                         ld_out, sl2e, ln);
+                         ld_out, sl2e, ln, kids, pad);
       break;
     default:
       hipLaunchKernelGGL((qkv_attn_kernel<T, 4, 2, LNA>), grid, dim3(256), 0, s, p, W, bias, S, H, lens, out, ld_out,
-                         sl2e, ln);
+                         sl2e, ln, kids, pad);
       break;
   }
 }
@@ -342,13 +356,15 @@ static void launch_qkv_attn(int cfg, const DenseParams& p, const T* W, const T* 
 // are f32 [H*192] (packed order), stats_out (optional) f32 [B*S, 2].
 void qkv_attn_fwd(int dtype, uintptr_t X, int ldx, uintptr_t Wp, uintptr_t bp, int B, int S, int H, int hidden,
                   uintptr_t lens, uintptr_t out, int ld_out, float scale, int cfg, uintptr_t stream,
-                  uintptr_t colsum, uintptr_t bias_f, uintptr_t stats_out, float eps) {
+                  uintptr_t colsum, uintptr_t bias_f, uintptr_t stats_out, float eps, uintptr_t key_ids, int pad) {
   if (S < 1 || S > 128) throw std::invalid_argument("qkv_attn: 1 <= S <= 128");
   if (hidden % 8 || ldx % 8 || ld_out % 4) throw std::invalid_argument("qkv_attn: hidden / ldx % 8, ld_out % 4");
   const bool lna = colsum != 0;
   if ((X | Wp | out) & 15 || (!lna && (bp & 7)) || (lna && ((colsum | bias_f) & 15 || !bias_f)) || stats_out & 7)
     throw std::invalid_argument("qkv_attn: alignment / folded-LayerNorm operands");
   if (cfg < 0 || cfg >= kNumQkvAttnCfgs) cfg = 1;
+  if (key_ids && lens) throw std::invalid_argument("qkv_attn: pass lens or key_ids, not both");
+  if (key_ids & 3) throw std::invalid_argument("qkv_attn: key_ids must be int32-aligned");
   if (B <= 0 || H <= 0) return;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const DenseParams p{reinterpret_cast<const void*>(X), ldx, B * S, hidden};
@@ -357,7 +373,8 @@ void qkv_attn_fwd(int dtype, uintptr_t X, int ldx, uintptr_t Wp, uintptr_t bp, i
                  reinterpret_cast<float*>(stats_out), 1.0f / hidden, eps};
 #define RDB_QA(T, L)                                                                                            \
   launch_qkv_attn<T, L>(cfg, p, reinterpret_cast<const T*>(Wp), reinterpret_cast<const T*>(bp), B, S, H,        \
-                        reinterpret_cast<const int*>(lens), reinterpret_cast<T*>(out), ld_out, sl2e, ln, s)
+                        reinterpret_cast<const int*>(lens), reinterpret_cast<T*>(out), ld_out, sl2e, ln, s,   \
+                        reinterpret_cast<const int*>(key_ids), pad)
   if (dtype == 0) {
     if (lna) RDB_QA(bf16, true); else RDB_QA(bf16, false);
   } else if (dtype == 1) {

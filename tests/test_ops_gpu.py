@@ -154,6 +154,13 @@ def test_qkv_attention(B, S, H, K, cfg, dtype):
         y = ops.qkv_attention(x, wp, bp, B, S, H, lens=ln, cfg=cfg)
         ref = ops.qkv_attention_ref(x, w, b, B, S, H, lens=ln)
         _close(y, ref, 2e-2, 2e-2)
+    # key lengths counted in-kernel from right-padded token ids (pad id 7): same result, bit for bit
+    ids = torch.randint(8, 1000, (B, S), device="cuda", dtype=torch.int32)
+    for i in range(B):
+        ids[i, int(lens[i]):] = 7
+    y_ids = ops.qkv_attention(x, wp, bp, B, S, H, cfg=cfg, key_ids=(ids, 7))
+    assert torch.equal(ops.seq_lens(ids, 7), lens.clamp(min=1))
+    assert torch.equal(y_ids, ops.qkv_attention(x, wp, bp, B, S, H, lens=lens, cfg=cfg))
 
 
 def test_qkv_attention_matches_two_kernel_path():
