@@ -229,7 +229,8 @@ class BertForSequenceClassification:
         D, H = c.hidden, c.heads
         fuse = self.fuse_qkv_attn and ops.qkv_attention_supported(S, H, D // H, D)
         # the fused kernel counts each sequence's key length from the ids itself
-        kid = (ids.contiguous(), c.pad_token_id) if fuse and ids.dtype == torch.int32 else None
+        kid = ((ids.contiguous(), c.pad_token_id) if fuse and ids.dtype == torch.int32
+               and os.environ.get("RDB_BERT_KEY_IDS", "1") != "0" else None)
         lens = None if kid is not None else ops.seq_lens(ids, c.pad_token_id)
         n = len(self.layers)
         lnout = self.fuse_residual_ln and self.dtype == torch.bfloat16 and D % 8 == 0

@@ -23,7 +23,6 @@
 namespace rdb {
 
 constexpr int kSkWaves = 8;
-constexpr int kSkUnroll = 4;  // K-steps (of 32) issued ahead per wave
 
 template <typename T> struct SkMfma;
 template <> struct SkMfma<bf16> {
@@ -65,8 +64,13 @@ __device__ __forceinline__ float sk_act(int act, float x) {
   }
 }
 
-// MT = number of 16-row M tiles (M <= 16 * MT).
-template <typename T, typename OutT, int MT>
+// MT = number of 16-row M tiles (M <= 16 * MT); U = K-steps (of 32) whose
+// loads a wave issues together before their MFMAs.  The launcher picks U >=
+// the wave's step count whenever the registers allow, so all of a wave's W / A
+// loads are in flight at once: one memory latency per wave instead of one per
+// step (at K = 768 a wave owns 3 steps, at K = 3072 12).  The epilogue's bias
+// and residual are fetched before the main loop, under it.
+template <typename T, typename OutT, int MT, int U>
 __global__ void __launch_bounds__(kSkWaves * 64)
 skinny_gemm_kernel(const T* __restrict__ A, int lda, const T* __restrict__ W, int ldw, OutT* __restrict__ C, int ldc,
                    const T* __restrict__ bias, const T* __restrict__ R, int ldr, int M, int N, int K, float alpha,
@@ -76,6 +80,20 @@ skinny_gemm_kernel(const T* __restrict__ A, int lda, const T* __restrict__ W, in
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int n0 = blockIdx.x * 16;
   const int fr = lane & 15, fg = lane >> 4;
+
+  // epilogue operands of the finishing waves (wave t < MT finishes M tile t)
+  const int m_ep = wid * 16 + fr, n_ep = n0 + fg * 4;
+  const int valid = N - n_ep < 4 ? N - n_ep : 4;
+  float bv[4] = {0.f, 0.f, 0.f, 0.f}, rv[4] = {0.f, 0.f, 0.f, 0.f};
+  if (wid < MT && m_ep < M && n_ep < N) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      if (e < valid) {
+        if (bias) bv[e] = (float)bias[n_ep + e];
+        if (R) rv[e] = (float)R[(size_t)m_ep * ldr + n_ep + e];
+      }
+    }
+  }
 
   // this wave's K range, in whole 32-deep steps
   const int steps = K / 32;
@@ -93,25 +111,21 @@ skinny_gemm_kernel(const T* __restrict__ A, int lda, const T* __restrict__ W, in
 #pragma unroll
   for (int t = 0; t < MT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  int s = s0;
-  for (; s + kSkUnroll <= s1; s += kSkUnroll) {
-    frag wf[kSkUnroll], af[kSkUnroll][MT];
+  for (int s = s0; s < s1; s += U) {
+    frag wf[U], af[U][MT];
 #pragma unroll
-    for (int u = 0; u < kSkUnroll; ++u) {
-      wf[u] = *reinterpret_cast<const frag*>(wrow + (s + u) * 32);
+    for (int u = 0; u < U; ++u) {
+      if (s + u < s1) {                       // wave-uniform
+        wf[u] = *reinterpret_cast<const frag*>(wrow + (s + u) * 32);
 #pragma unroll
-      for (int t = 0; t < MT; ++t) af[u][t] = *reinterpret_cast<const frag*>(arow[t] + (s + u) * 32);
+        for (int t = 0; t < MT; ++t) af[u][t] = *reinterpret_cast<const frag*>(arow[t] + (s + u) * 32);
+      }
     }
 #pragma unroll
-    for (int u = 0; u < kSkUnroll; ++u)
+    for (int u = 0; u < U; ++u)
+      if (s + u < s1)
 #pragma unroll
-      for (int t = 0; t < MT; ++t) acc[t] = SkMfma<T>::mma(wf[u], af[u][t], acc[t]);
-  }
-  for (; s < s1; ++s) {
-    const frag wf = *reinterpret_cast<const frag*>(wrow + s * 32);
-#pragma unroll
-    for (int t = 0; t < MT; ++t)
-      acc[t] = SkMfma<T>::mma(wf, *reinterpret_cast<const frag*>(arow[t] + s * 32), acc[t]);
+        for (int t = 0; t < MT; ++t) acc[t] = SkMfma<T>::mma(wf[u], af[u][t], acc[t]);
   }
 
 #pragma unroll
@@ -123,35 +137,36 @@ skinny_gemm_kernel(const T* __restrict__ A, int lda, const T* __restrict__ W, in
   f32x4 v = red[0][t][lane];
 #pragma unroll
   for (int w = 1; w < kSkWaves; ++w) v += red[w][t][lane];
-  const int m = t * 16 + fr;
-  const int n = n0 + fg * 4;
-  if (m >= M || n >= N) return;
-  const int valid = min(4, N - n);
+  if (m_ep >= M || n_ep >= N) return;
   float y[4];
 #pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    float x = alpha * v[e];
-    if (e < valid) {
-      if (bias) x += (float)bias[n + e];
-      if (R) x += (float)R[(size_t)m * ldr + n + e];
-    }
-    y[e] = sk_act(act, x);
-  }
-  sk_store<OutT>(C + (size_t)m * ldc + n, y, (valid == 4 && (ldc & 3) == 0) ? 4 : valid);
+  for (int e = 0; e < 4; ++e) y[e] = sk_act(act, alpha * v[e] + bv[e] + rv[e]);
+  sk_store<OutT>(C + (size_t)m_ep * ldc + n_ep, y, (valid == 4 && (ldc & 3) == 0) ? 4 : valid);
+}
+
+template <typename T, typename OutT, int MT>
+static void launch_sk_mt(const T* A, int lda, const T* W, int ldw, OutT* C, int ldc, const T* bias, const T* R,
+                         int ldr, int M, int N, int K, float alpha, int act, hipStream_t s) {
+  const dim3 grid((N + 15) / 16), block(kSkWaves * 64);
+  const int per = (K / 32 + kSkWaves - 1) / kSkWaves;
+  // all of a wave's steps in flight at once while (MT + 1) * U frags fit ~200 VGPRs
+  constexpr int UMAX = (MT + 1) * 16 * 4 <= 200 ? 16 : 8;
+#define RDB_SKU(U_) hipLaunchKernelGGL((skinny_gemm_kernel<T, OutT, MT, U_>), grid, block, 0, s, A, lda, W, ldw, C, \
+                                       ldc, bias, R, ldr, M, N, K, alpha, act)
+  if (per <= 4) RDB_SKU(4);
+  else if (per <= 8 || UMAX == 8) RDB_SKU(8);
+  else RDB_SKU(UMAX);
+#undef RDB_SKU
 }
 
 template <typename T, typename OutT>
 static void launch_sk(const T* A, int lda, const T* W, int ldw, OutT* C, int ldc, const T* bias, const T* R, int ldr,
                       int M, int N, int K, float alpha, int act, hipStream_t s) {
-  const dim3 grid((N + 15) / 16), block(kSkWaves * 64);
   const int mt = (M + 15) / 16;
-#define RDB_SK(MT_) hipLaunchKernelGGL((skinny_gemm_kernel<T, OutT, MT_>), grid, block, 0, s, A, lda, W, ldw, C, ldc, \
-                                       bias, R, ldr, M, N, K, alpha, act)
-  if (mt == 1) RDB_SK(1);
-  else if (mt == 2) RDB_SK(2);
-  else if (mt == 3) RDB_SK(3);
-  else RDB_SK(4);
-#undef RDB_SK
+  if (mt == 1) launch_sk_mt<T, OutT, 1>(A, lda, W, ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act, s);
+  else if (mt == 2) launch_sk_mt<T, OutT, 2>(A, lda, W, ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act, s);
+  else if (mt == 3) launch_sk_mt<T, OutT, 3>(A, lda, W, ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act, s);
+  else launch_sk_mt<T, OutT, 4>(A, lda, W, ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act, s);
 }
 
 bool skinny_gemm_ok(int M, int N, int K, int lda, int ldw, int act, uintptr_t A, uintptr_t W) {

@@ -280,6 +280,72 @@ static void launch_norm(dim3 grid, hipStream_t s, uintptr_t x, uintptr_t res, ui
 #undef RDB_CASE
 }
 
+// Half-wave-per-token form of embed_ln_kernel (16-B accesses, 8 tokens per
+// block; norm16_kernel's layout): half the memory instructions of the 8-B form
+// and the row reductions stay inside the half wave.
+template <typename T, int NV>
+__global__ void __launch_bounds__(256)
+embed16_kernel(const int* __restrict__ ids, const int* __restrict__ types, const T* __restrict__ word,
+               const T* __restrict__ pos, const T* __restrict__ typ, const T* __restrict__ gamma,
+               const T* __restrict__ beta, T* __restrict__ y, int tokens, int S, int D, int vocab, float eps,
+               float2* __restrict__ zst, int zn, int zstride) {
+  const int hl = threadIdx.x & 31;
+  const int t = blockIdx.x * 8 + (threadIdx.x >> 5);
+  if (t >= tokens) return;      // whole half waves only: the xor-16..1 reductions stay inside a half
+  for (int k = hl; k < zn; k += 32) zst[(size_t)k * zstride + t] = float2{0.f, 0.f};
+  int id = ids[t];
+  id = id < 0 ? 0 : (id >= vocab ? vocab - 1 : id);
+  const int tt = types ? types[t] : 0;
+  const int p = t % S;
+  float v[NV][8];
+  float sm = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = i * 256 + hl * 8;
+    float a[8], b[8], d[8];
+    load8(word + (size_t)id * D + c, a);
+    load8(pos + (size_t)p * D + c, b);
+    load8(typ + (size_t)tt * D + c, d);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { v[i][e] = a[e] + b[e] + d[e]; sm += v[i][e]; }
+  }
+  const float mean = half_sum(sm) / D;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { const float dd = v[i][e] - mean; q += dd * dd; }
+  const float rstd = rsqrtf(half_sum(q) / D + eps);
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = i * 256 + hl * 8;
+    float g[8], b[8], o[8];
+    load8(gamma + c, g);
+    load8(beta + c, b);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = (v[i][e] - mean) * rstd * g[e] + b[e];
+    st8(y + (size_t)t * D + c, o);
+  }
+}
+
+template <typename T>
+static bool launch_embed16(hipStream_t s, uintptr_t ids, uintptr_t types, uintptr_t word, uintptr_t pos,
+                           uintptr_t typ, uintptr_t gamma, uintptr_t beta, uintptr_t y, int tokens, int S, int D,
+                           int vocab, float eps, uintptr_t zst, int zn, int zstride) {
+  if ((word | pos | typ | gamma | beta | y) & 15) return false;
+  const dim3 grid((tokens + 7) / 8);
+#define RDB_E16(NV)                                                                                          \
+  if (D == 256 * NV) {                                                                                       \
+    hipLaunchKernelGGL((embed16_kernel<T, NV>), grid, dim3(256), 0, s, (const int*)ids, (const int*)types,   \
+                       (const T*)word, (const T*)pos, (const T*)typ, (const T*)gamma, (const T*)beta, (T*)y, \
+                       tokens, S, D, vocab, eps, (float2*)zst, zn, zstride);                                 \
+    return true;                                                                                             \
+  }
+  RDB_E16(1) RDB_E16(2) RDB_E16(3) RDB_E16(4) RDB_E16(8) RDB_E16(16)
+#undef RDB_E16
+  return false;
+}
+
 template <typename T>
 static void launch_embed(dim3 grid, hipStream_t s, uintptr_t ids, uintptr_t types, uintptr_t word,
                          uintptr_t pos, uintptr_t typ, uintptr_t gamma, uintptr_t beta, uintptr_t y,
@@ -354,6 +420,17 @@ void embed_ln_fwd(int dtype, uintptr_t ids, uintptr_t types, uintptr_t word, uin
   if (!zero_stats) zn = 0;
   if (tokens <= 0) return;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  static const bool e16_env = [] { const char* e = getenv("RDB_EMBED16"); return !(e && e[0] == '0'); }();
+  if (e16_env && dtype <= 1) {
+    const bool ok = dtype == 0 ? launch_embed16<bf16>(s, ids, types, word, pos, typ, gamma, beta, y, tokens, S, D, vocab,
+                                                      eps, zero_stats, zn, zstride)
+                               : launch_embed16<f16>(s, ids, types, word, pos, typ, gamma, beta, y, tokens, S, D, vocab,
+                                                     eps, zero_stats, zn, zstride);
+    if (ok) {
+      RDB_HIP_CHECK(hipGetLastError());
+      return;
+    }
+  }
   dim3 grid((tokens + 3) / 4);
   if (dtype == 0)
     launch_embed<bf16>(grid, s, ids, types, word, pos, typ, gamma, beta, y, tokens, S, D, vocab, eps, zero_stats, zn, zstride);

@@ -101,6 +101,16 @@ def test_embed_ln():
     b = torch.randn(D, device="cuda", dtype=torch.bfloat16)
     ids = torch.randint(0, V, (4, S), device="cuda", dtype=torch.int32)
     _close(ops.embed_ln(ids, word, pos, typ, g, b), ops.embed_ln_ref(ids, word, pos, typ, g, b), 3e-2, 2e-2)
+    # token types, an odd token count (partial last block), both kernel forms: the 16-B
+    # half-wave one (aligned tables) and the 8-B one (a table 8-B but not 16-B aligned)
+    ids = torch.randint(0, V, (3, 37), device="cuda", dtype=torch.int32)
+    types = torch.randint(0, 2, (3, 37), device="cuda", dtype=torch.int32)
+    ref = ops.embed_ln_ref(ids, word, pos, typ, g, b, types=types)
+    _close(ops.embed_ln(ids, word, pos, typ, g, b, types=types), ref, 3e-2, 2e-2)
+    pos8 = torch.empty(512 * D + 4, device="cuda", dtype=torch.bfloat16)[4:].view(512, D)
+    pos8.copy_(pos)
+    assert pos8.data_ptr() % 16 == 8
+    _close(ops.embed_ln(ids, word, pos8, typ, g, b, types=types), ref, 3e-2, 2e-2)
 
 
 @pytest.mark.parametrize("B,S,H,Hkv,D,causal,use_lens", [
