@@ -579,7 +579,7 @@ def attention(qkv: torch.Tensor, B: int, S: int, H: int, Hkv: int, D: int, lens:
     return out
 
 
-NUM_QKV_ATTN_CFGS = 4   # qkv_attention.hip: 8 waves (4x2) x 3 stages, 8 (4x2) x 2, 4 x 2, 8 (2x4) x 2
+NUM_QKV_ATTN_CFGS = 5   # qkv_attention.hip: 8 waves (4x2) x 3 stages, 8 (4x2) x 2, 4 x 2, 8 (2x4) x 2, two sequences per block (S == 128)
 QKV_ATTN_MAX_S = 128
 
 

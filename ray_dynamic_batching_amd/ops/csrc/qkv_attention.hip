@@ -43,12 +43,18 @@ struct QkvLn {
   float inv_d, eps;
 };
 
-template <typename T, int NW, int STAGES, bool LNA, int WGM_ = (NW == 8 ? 4 : 2)>
-__global__ void __launch_bounds__(64 * NW, NW == 8 && STAGES == 3 ? 1 : 2)
+// SEQ = 2 (S == 128 only): one block = TWO consecutive sequences of one head, a
+// 256 x 192 projection tile -- the head's W tile (192 x hidden) is staged once
+// for two sequences, 30 % fewer bytes per FLOP through the per-CU L2 -> LDS
+// path that bounds the projection; B*H/2 blocks.  Waves 0..3 then run the
+// attention of the first sequence, 4..7 of the second.
+template <typename T, int NW, int STAGES, bool LNA, int WGM_ = (NW == 8 ? 4 : 2), int SEQ = 1>
+__global__ void __launch_bounds__(64 * NW, NW == 8 && (STAGES == 3 || SEQ == 2) ? 1 : 2)
 qkv_attn_kernel(DenseParams ap, const T* __restrict__ W, const T* __restrict__ bias, int S, int H,
                 const int* __restrict__ lens, T* __restrict__ out, int ld_out, float scale_log2e, QkvLn ln,
                 const int* __restrict__ kids, int pad) {
-  constexpr int BM = 128, BN = 192, BK = 64, D = 64;
+  constexpr int BM = 128 * SEQ, BN = 192, BK = 64, D = 64;
+  static_assert(SEQ == 1 || (SEQ == 2 && NW == 8), "two sequences per block: 8 waves");
   constexpr int WGM = WGM_, WGN = NW / WGM_;
   constexpr int NT = 64 * NW;
   constexpr int WM = BM / WGM, WN = BN / WGN;       // 32|64 x 96
@@ -70,8 +76,8 @@ qkv_attn_kernel(DenseParams ap, const T* __restrict__ W, const T* __restrict__ b
   const int wm = wid / WGN, wn = wid % WGN;
   const int fr = lane & 15, fg = lane >> 4;
   const int t = xcd_remap(blockIdx.x, gridDim.x);
-  const int b = t / H, h = t - b * H;
-  const int m0 = b * S, n0 = h * BN;
+  const int b = t / H, h = t - b * H;            // b: the block's first sequence / SEQ
+  const int m0 = b * SEQ * S, n0 = h * BN;
   const int K = ap.K;
 
   // ---- 1. projection main loop (gemm_core.h's, fixed 128 x 192 tile) ----
@@ -133,8 +139,13 @@ qkv_attn_kernel(DenseParams ap, const T* __restrict__ W, const T* __restrict__ b
   // key length of this sequence: fetched before the main loop, used after it --
   // either a precomputed lens[b] or, with kids (the [B, S] token ids), counted
   // here from the ids (non-pad tokens, right padding): no separate lengths kernel
-  int kv_len = lens ? lens[b] : S;
-  const int kid = (kids != nullptr && tid < S) ? kids[(size_t)b * S + tid] : pad;
+  // (SEQ = 2: S == 128, tokens [128*sq, 128*sq + 128) of the tile are sequence b*2 + sq;
+  // wave w's attention queries lie in sequence w / 4)
+  const int nseq = ap.M / S;
+  const int my_seq = SEQ == 1 ? 0 : wid / (NW / SEQ);
+  const int gseq = b * SEQ + my_seq < nseq ? b * SEQ + my_seq : nseq - 1;
+  int kv_len = lens ? lens[gseq] : S;
+  const int kid = (kids != nullptr && tid < SEQ * S && b * SEQ + tid / S < nseq) ? kids[(size_t)b * SEQ * S + tid] : pad;
   const int nk = (K + BK - 1) / BK;
   if constexpr (STAGES == 2) {
     stage(0, 0);
@@ -170,8 +181,12 @@ qkv_attn_kernel(DenseParams ap, const T* __restrict__ W, const T* __restrict__ b
     if (lane == 0) s_cnt[wid] = __popcll(bal);
     __syncthreads();
     kv_len = 0;
+    if constexpr (SEQ == 1) {
 #pragma unroll
-    for (int w = 0; w < NW; ++w) kv_len += s_cnt[w];
+      for (int w = 0; w < NW; ++w) kv_len += s_cnt[w];
+    } else {                  // ids of sequence sq were read by waves 2*sq, 2*sq + 1 (S == 128)
+      kv_len = s_cnt[2 * my_seq] + s_cnt[2 * my_seq + 1];
+    }
   }
   kv_len = kv_len < S ? (kv_len < 1 ? 1 : kv_len) : S;
   // LNA: per-row (mean, rstd) of this lane's rows; head 0 publishes the sums
@@ -186,7 +201,7 @@ qkv_attn_kernel(DenseParams ap, const T* __restrict__ W, const T* __restrict__ b
       q += __shfl_xor(q, 32, 64);
       ln_row_stats(float2{a, q}, ln.inv_d, ln.eps, mu[j], rs[j]);
       const int tok = wm * WM + j * 16 + fr;
-      if (ln.stats_out != nullptr && h == 0 && wn == 0 && fg == 0 && tok < S && m0 + tok < ap.M)
+      if (ln.stats_out != nullptr && h == 0 && wn == 0 && fg == 0 && tok % 128 < S && m0 + tok < ap.M)
         *reinterpret_cast<float2*>(ln.stats_out + (size_t)(m0 + tok) * 2) = float2{a, q};
     }
   }
@@ -230,7 +245,8 @@ qkv_attn_kernel(DenseParams ap, const T* __restrict__ W, const T* __restrict__ b
   __syncthreads();
 
   // ---- 3. attention: wave w owns queries [w*16*QT, (w+1)*16*QT) ----
-  const int q0 = wid * 16 * QT;
+  const int q0 = wid * 16 * QT;                      // token index in the tile
+  const int kbase = my_seq * 128;                    // this wave's sequence's keys in the tile
   frag qf[QT][2];
 #pragma unroll
   for (int qt = 0; qt < QT; ++qt)
@@ -245,13 +261,13 @@ qkv_attn_kernel(DenseParams ap, const T* __restrict__ W, const T* __restrict__ b
     for (int qt = 0; qt < QT; ++qt) s[kt][qt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      const frag kf = *reinterpret_cast<const frag*>(Ks + swz_off(kt * 16 + fr, ks * 4 + fg));
+      const frag kf = *reinterpret_cast<const frag*>(Ks + swz_off(kbase + kt * 16 + fr, ks * 4 + fg));
 #pragma unroll
       for (int qt = 0; qt < QT; ++qt) s[kt][qt] = MfmaOp<T>::mma(kf, qf[qt][ks], s[kt][qt]);
     }
   }
   float l_run[QT];
-  const bool need_mask = kv_len < BM;
+  const bool need_mask = kv_len < 128;
 #pragma unroll
   for (int qt = 0; qt < QT; ++qt) {
     float mx = -INFINITY;
@@ -294,7 +310,7 @@ qkv_attn_kernel(DenseParams ap, const T* __restrict__ W, const T* __restrict__ b
       }
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) {
-      const T* vr = Vt + (dt * 16 + fr) * VT_LD + c * 32 + fg * 4;
+      const T* vr = Vt + (dt * 16 + fr) * VT_LD + kbase + c * 32 + fg * 4;
       const frag4 lo = *reinterpret_cast<const frag4*>(vr);
       const frag4 hi = *reinterpret_cast<const frag4*>(vr + 16);
       const frag vf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
@@ -310,7 +326,7 @@ qkv_attn_kernel(DenseParams ap, const T* __restrict__ W, const T* __restrict__ b
     l += __shfl_xor(l, 32, 64);
     const float inv = 1.f / l;
     const int q = q0 + qt * 16 + fr;
-    if (q >= S) continue;
+    if (q - kbase >= S || m0 + q >= ap.M) continue;
     T* op = out + (size_t)(m0 + q) * ld_out + h * D;
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) {
@@ -322,8 +338,9 @@ qkv_attn_kernel(DenseParams ap, const T* __restrict__ W, const T* __restrict__ b
 }
 
 // cfg: 0 = 8 waves (4x2) / 3 stages (1 block per CU), 1 = 8 waves (4x2) / 2 stages, 2 = 4 waves / 2 stages,
-//      3 = 8 waves (2x4: 64x48 wave tiles, fewer LDS fragment reads per MFMA) / 2 stages
-constexpr int kNumQkvAttnCfgs = 4;
+//      3 = 8 waves (2x4: 64x48 wave tiles, fewer LDS fragment reads per MFMA) / 2 stages,
+//      4 = two sequences per block (256 x 192 tile, 8 waves 4x2, 2 stages; S == 128 only, else cfg 3)
+constexpr int kNumQkvAttnCfgs = 5;
 
 template <typename T, bool LNA>
 static void launch_qkv_attn(int cfg, const DenseParams& p, const T* W, const T* bias, int B, int S, int H,
@@ -342,6 +359,10 @@ static void launch_qkv_attn(int cfg, const DenseParams& p, const T* W, const T* 
     case 3:
       hipLaunchKernelGGL((qkv_attn_kernel<T, 8, 2, LNA, 2>), grid, dim3(512), 0, s, p, W, bias, S, H, lens, out,
                          ld_out, sl2e, ln, kids, pad);
+      break;
+    case 4:   // two sequences per block (S == 128, host-checked)
+      hipLaunchKernelGGL((qkv_attn_kernel<T, 8, 2, LNA, 4, 2>), dim3((B + 1) / 2 * H), dim3(512), 0, s, p, W, bias, S,
+                         H, lens, out, ld_out, sl2e, ln, kids, pad);
       break;
     default:
       hipLaunchKernelGGL((qkv_attn_kernel<T, 4, 2, LNA>), grid, dim3(256), 0, s, p, W, bias, S, H, lens, out, ld_out,
@@ -363,6 +384,7 @@ void qkv_attn_fwd(int dtype, uintptr_t X, int ldx, uintptr_t Wp, uintptr_t bp, i
   if ((X | Wp | out) & 15 || (!lna && (bp & 7)) || (lna && ((colsum | bias_f) & 15 || !bias_f)) || stats_out & 7)
     throw std::invalid_argument("qkv_attn: alignment / folded-LayerNorm operands");
   if (cfg < 0 || cfg >= kNumQkvAttnCfgs) cfg = 1;
+  if (cfg == 4 && S != 128) cfg = 3;
   if (key_ids && lens) throw std::invalid_argument("qkv_attn: pass lens or key_ids, not both");
   if (key_ids & 3) throw std::invalid_argument("qkv_attn: key_ids must be int32-aligned");
   if (B <= 0 || H <= 0) return;

@@ -145,8 +145,9 @@ def test_attention_spike_rescale():
     _close(ops.attention(qkv, B, S, H, H, D), ops.attention_ref(qkv, B, S, H, H, D), 2e-2, 2e-2)
 
 
-@pytest.mark.parametrize("B,S,H,K", [(4, 128, 12, 768), (3, 100, 4, 256), (2, 64, 2, 136), (1, 1, 1, 64)])
-@pytest.mark.parametrize("cfg", [0, 1, 2, 3])
+@pytest.mark.parametrize("B,S,H,K", [(4, 128, 12, 768), (5, 128, 2, 256), (3, 100, 4, 256), (2, 64, 2, 136),
+                                     (1, 1, 1, 64)])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4])
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
 def test_qkv_attention(B, S, H, K, cfg, dtype):
     """Fused projection + attention (qkv_attention.hip) == GEMM -> attention in fp32,
@@ -478,7 +479,7 @@ def test_linear_ln_self_stats_and_lnr_only_all_tiles(cfg):
     _close(y2, ops.linear_ln_ref(h, w3, b3, residual=x, ln_res=(g, be)), 3e-2, 3e-2)
 
 
-@pytest.mark.parametrize("cfg", [0, 1, 2, 3])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4])
 def test_qkv_attention_folded_layernorm(cfg):
     """Fused projection+attention on RAW rows with the LayerNorm folded into the
     packed weight == LayerNorm -> unfused reference; the statistics it
