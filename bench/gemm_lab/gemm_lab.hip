@@ -52,10 +52,10 @@ __global__ void fill_rand(bf16* p, size_t n, uint32_t seed, float scale) {
 struct Shape { int M, N, K; const char* name; };
 struct Variant { std::string name; std::function<void(const bf16*, const bf16*, const bf16*, bf16*, int, int, int, hipStream_t)> run; };
 
-template <int NW, int BM, int BN, int GM, int GN, int S, int BK = 64>
+template <int NW, int BM, int BN, int GM, int GN, int S, int BK = 64, int OCC = 2>
 Variant pp(const char* nm) {
   return {nm, [](const bf16* A, const bf16* W, const bf16* b, bf16* C, int M, int N, int K, hipStream_t s) {
-            launch_gemm_pp<bf16, bf16, NW, BM, BN, GM, GN, S, BK>(A, K, W, K, C, N, b, nullptr, 0, M, N, K, 1.f,
+            launch_gemm_pp<bf16, bf16, NW, BM, BN, GM, GN, S, BK, OCC>(A, K, W, K, C, N, b, nullptr, 0, M, N, K, 1.f,
                                                                    ACT_NONE, s);
           }};
 }
@@ -97,7 +97,18 @@ int main(int argc, char** argv) {
                                {4096, 768, 3072, "bert.ffn2"},
                                {4096, 4096, 4096, "sq4096"}};
   std::vector<Variant> vs = {
-#ifdef LAB_FAST
+#if defined(LAB_SET_OCC)
+      // occupancy: one 8-wave block per CU (OCC 2) vs two co-resident blocks (OCC 4, LDS <= 80 KiB)
+      pp<8, 256, 128, 2, 2, 3, 64, 2>("pp8 256x128 bk64 s3"),
+      pp<8, 256, 128, 2, 2, 3, 32, 4>("pp8 256x128 bk32 s3 occ4"),
+      pp<8, 256, 128, 2, 2, 4, 32, 2>("pp8 256x128 bk32 s4"),
+      pp<8, 128, 128, 2, 2, 4, 32, 4>("pp8 128x128 bk32 s4 occ4"),
+      pp<8, 128, 256, 1, 4, 3, 32, 4>("pp8 128x256 bk32 s3 occ4"),
+      pp<8, 256, 256, 2, 2, 4, 32, 2>("pp8 256x256 bk32 s4"),
+      pp<4, 128, 128, 1, 2, 4, 32, 2>("pp4 128x128 bk32 s4"),
+      pp<4, 128, 128, 1, 2, 3, 32, 3>("pp4 128x128 bk32 s3 occ3"),
+      core(10), core(9),
+#elif defined(LAB_FAST)
       LAB_FAST
 #else
       pp<8, 256, 128, 2, 2, 3>("pp8 256x128 2x2 s3"),

@@ -82,6 +82,14 @@ class BertForSequenceClassification:
         # critical path) costs more than the LayerNorm kernel it removes
         # (+11 us vs -5 us per GEMM, profiles/ab_r2.json) -- off by default
         self.fuse_residual_ln = os.environ.get("RDB_BERT_LNOUT", "0") == "1"
+        # RDB_BERT_ROWLN: o-proj -> LN1 ("o"), FFN-down -> LN2 ("d") or both ("1")
+        # on the full-row GEMM + LayerNorm kernel (ops.linear_rowln: 64-row blocks
+        # own whole 768-wide rows, statistics block-local) for batches of at
+        # least RDB_BERT_ROWLN_MIN_ROWS token rows; "0" = tiled GEMM + LayerNorm kernel
+        rl = os.environ.get("RDB_BERT_ROWLN", "0")
+        self.rowln_o = rl in ("1", "o")
+        self.rowln_d = rl in ("1", "d")
+        self.rowln_min_rows = int(os.environ.get("RDB_BERT_ROWLN_MIN_ROWS", "2048"))
         env = os.environ.get("RDB_BERT_FOLD_LN", "")
         self.fold_ln_auto = env == ""
         self.fold_ln = env == "1" or (env == "" and self.auto_fold_ln(1))
@@ -176,6 +184,15 @@ class BertForSequenceClassification:
             self._packed = (key, [ops.pack_qkv_heads(L["w_qkv"], L["b_qkv"], H) for L in self.layers])
         return self._packed[1]
 
+    def _rowln_weights(self):
+        """Per layer (w_o, w_out) packed for ops.linear_rowln, rebuilt when a
+        source tensor is swapped or modified in place."""
+        key = tuple((t.data_ptr(), t._version) for L in self.layers for t in (L["w_o"], L["w_out"]))
+        if getattr(self, "_rowln", None) is None or self._rowln[0] != key:
+            self._rowln = (key, [(ops.pack_rowln_weight(L["w_o"]), ops.pack_rowln_weight(L["w_out"]))
+                                 for L in self.layers])
+        return self._rowln[1]
+
     def _folded_weights(self):
         key = self._fold_key()
         if self._folded is not None and getattr(self, "_folded_key", None) != key:
@@ -259,11 +276,23 @@ class BertForSequenceClassification:
                 h = ops.linear_residual_ln(inter, L["w_out"], L["b_out"], h1, L["ln2_g"], L["ln2_b"], c.eps,
                                            ws[4 * i + 2], ws[4 * i + 3].view(torch.int32))
                 continue
-            a = ops.linear(ctx, L["w_o"], L["b_o"], residual=h)
-            h1 = ops.layer_norm(a, L["ln1_g"], L["ln1_b"], c.eps)
+            rows = ctx.shape[0]
+            cls_rows = i == n - 1 and self.cls_only_last_layer
+            rowln = (not cls_rows and self.dtype == torch.bfloat16 and rows >= self.rowln_min_rows
+                     and (self.rowln_o or self.rowln_d) and ops.linear_rowln_supported(rows, D, D)
+                     and ops.linear_rowln_supported(rows, D, c.intermediate))
+            rp = self._rowln_weights()[i] if rowln else None
+            if rowln and self.rowln_o:
+                h1 = ops.linear_rowln(ctx, rp[0], L["b_o"], h, L["ln1_g"], L["ln1_b"], c.eps)
+            else:
+                a = ops.linear(ctx, L["w_o"], L["b_o"], residual=h)
+                h1 = ops.layer_norm(a, L["ln1_g"], L["ln1_b"], c.eps)
             inter = ops.linear(h1, L["w_i"], L["b_i"], act="gelu")
-            o = ops.linear(inter, L["w_out"], L["b_out"], residual=h1)
-            h = ops.layer_norm(o, L["ln2_g"], L["ln2_b"], c.eps)
+            if rowln and self.rowln_d:
+                h = ops.linear_rowln(inter, rp[1], L["b_out"], h1, L["ln2_g"], L["ln2_b"], c.eps)
+            else:
+                o = ops.linear(inter, L["w_out"], L["b_out"], residual=h1)
+                h = ops.layer_norm(o, L["ln2_g"], L["ln2_b"], c.eps)
         cls = h if self.cls_only_last_layer else h.view(B, S, D)[:, 0, :]
         pooled = ops.linear(cls, self.w_pool, self.b_pool, act="tanh")
         return ops.linear(pooled, self.w_cls, self.b_cls, out_dtype=torch.float32)

@@ -400,6 +400,51 @@ def linear_residual_ln(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, res
     return out
 
 
+def linear_rowln_supported(M: int, N: int, K: int) -> bool:
+    """Shapes the full-row GEMM + LayerNorm kernel (``gemm_rowln.hip``) takes."""
+    return N == 768 and K % 32 == 0 and M > 0
+
+
+def pack_rowln_weight(w: torch.Tensor) -> torch.Tensor:
+    """[N, K] weight -> the k-tile-major [K/32, N, 32] layout ``linear_rowln`` reads
+    (each 32-wide k-step of all N rows contiguous).  Done once per weight."""
+    N, K = w.shape
+    _check(K % 32 == 0, "pack_rowln_weight: K must be a multiple of 32")
+    return w.reshape(N, K // 32, 32).permute(1, 0, 2).contiguous()
+
+
+def linear_rowln(x: torch.Tensor, wp: torch.Tensor, bias: torch.Tensor, residual: torch.Tensor,
+                 gamma: torch.Tensor, beta: torch.Tensor, eps: float,
+                 out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """y = LayerNorm(x @ w.T + bias + residual) * gamma + beta (bf16, N = 768) in ONE
+    kernel whose 64-row blocks own whole output rows (``gemm_rowln.hip``): the row
+    statistics never leave the block -- no workspace, no zeroing, no cross-block
+    wait, no LayerNorm launch.  ``wp`` = ``pack_rowln_weight(w)``.  The post-LN
+    transformer's o-proj -> LN1 and FFN-down -> LN2."""
+    _check(x.is_cuda and x.dtype == torch.bfloat16 and wp.dtype == x.dtype, "linear_rowln: bf16 on the GPU")
+    _check(wp.dim() == 3 and wp.shape[2] == 32 and wp.is_contiguous(),
+           "linear_rowln: wp must be pack_rowln_weight(w), [K/32, N, 32]")
+    N, K = wp.shape[1], wp.shape[0] * 32
+    _check(x.dim() == 2 and x.stride(1) == 1 and x.shape[1] == K, "linear_rowln: x must be a 2-D [M, K] view")
+    M, lda = x.shape[0], x.stride(0)
+    _check(linear_rowln_supported(M, N, K), f"linear_rowln: unsupported shape M={M} N={N} K={K}")
+    _check(lda % 8 == 0 and _aligned(x) and _aligned(wp), "linear_rowln: x / w rows must be 16-byte aligned")
+    _check(bias.is_contiguous() and bias.numel() == N and bias.dtype == x.dtype and _aligned(bias, 8),
+           "linear_rowln: bad bias")
+    _check(residual.dim() == 2 and residual.shape == (M, N) and residual.stride(1) == 1
+           and residual.stride(0) % 4 == 0 and residual.dtype == x.dtype and _aligned(residual, 8),
+           "linear_rowln: bad residual")
+    for v in (gamma, beta):
+        _check(v.is_contiguous() and v.numel() == N and v.dtype == x.dtype and _aligned(v, 8), "linear_rowln: gamma/beta")
+    if out is None:
+        out = torch.empty(M, N, device=x.device, dtype=x.dtype)
+    _check(out.dim() == 2 and out.shape == (M, N) and out.stride(1) == 1 and out.stride(0) % 4 == 0
+           and _aligned(out, 8), "linear_rowln: bad out")
+    _ops().gemm_rowln(x.data_ptr(), lda, wp.data_ptr(), bias.data_ptr(), residual.data_ptr(), residual.stride(0),
+                      gamma.data_ptr(), beta.data_ptr(), out.data_ptr(), out.stride(0), M, N, K, float(eps), _stream())
+    return out
+
+
 def linear_residual_ln_ref(x, w, bias, residual, gamma, beta, eps=1e-12):
     y = x.float() @ w.float().t() + bias.float() + residual.float()
     return F.layer_norm(y, (y.shape[-1],), gamma.float(), beta.float(), eps).to(x.dtype)

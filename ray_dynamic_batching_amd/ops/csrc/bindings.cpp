@@ -19,6 +19,8 @@ void gemm_tn_ln(uintptr_t A, int lda, uintptr_t W, int ldw, uintptr_t C, int ldc
                 uintptr_t a_colsum, uintptr_t a_bias, uintptr_t r_stats, int r_ld, uintptr_t r_g, uintptr_t r_b,
                 uintptr_t o_stats, int o_ld, float a_inv_d, float r_inv_d, float eps, uintptr_t stream, int cfg,
                 uintptr_t panel, uintptr_t err);
+void gemm_rowln(uintptr_t A, int lda, uintptr_t W, uintptr_t bias, uintptr_t R, int ldr, uintptr_t gamma,
+                uintptr_t beta, uintptr_t C, int ldc, int M, int N, int K, float eps, uintptr_t stream);
 void norm_fwd(int dtype, int mode, uintptr_t x, uintptr_t res, uintptr_t res_out, uintptr_t gamma,
               uintptr_t beta, uintptr_t y, int rows, int D, int ldx, float eps, uintptr_t stream);
 void embed_ln_fwd(int dtype, uintptr_t ids, uintptr_t types, uintptr_t word, uintptr_t pos,
@@ -76,6 +78,7 @@ PYBIND11_MODULE(_rdb_ops, m) {
         py::arg("a_bias"), py::arg("r_stats"), py::arg("r_ld"), py::arg("r_g"), py::arg("r_b"), py::arg("o_stats"),
         py::arg("o_ld"), py::arg("a_inv_d"), py::arg("r_inv_d"), py::arg("eps"), py::arg("stream"), py::arg("cfg"),
         py::arg("panel") = 0, py::arg("err") = 0, py::call_guard<py::gil_scoped_release>());
+  m.def("gemm_rowln", &rdb::gemm_rowln, py::call_guard<py::gil_scoped_release>());
   m.def("norm_fwd", &rdb::norm_fwd, py::call_guard<py::gil_scoped_release>());
   m.def("embed_ln_fwd", &rdb::embed_ln_fwd, py::call_guard<py::gil_scoped_release>());
   m.def("attn_fwd", &rdb::attn_fwd, py::call_guard<py::gil_scoped_release>());

@@ -67,9 +67,12 @@ struct PPGeom {
   static __device__ __forceinline__ int off(int row, int chunk) { return row * ROWB + ((chunk ^ swz(row)) << 4); }
 };
 
+// OCC = waves per SIMD the register budget must allow: 2 = one 8-wave block
+// per CU (<= 256 VGPRs), 4 = two co-resident blocks (<= 128 VGPRs; the tile's
+// LDS must then fit twice in 160 KiB)
 template <typename T, typename OutT, int NW, int BM, int BN, int GM, int GN, int STAGES, bool HAS_BIAS, bool HAS_RES,
-          int BK_ = 64>
-__global__ void __launch_bounds__(64 * NW, 2)
+          int BK_ = 64, int OCC = 2>
+__global__ void __launch_bounds__(64 * NW, OCC)
 gemm_pp_kernel(const T* __restrict__ A, int lda, const T* __restrict__ W, int ldw, OutT* __restrict__ C, int ldc,
                const T* __restrict__ bias, const T* __restrict__ R, int ldr, int M, int N, int K, float alpha,
                int act) {
@@ -265,22 +268,22 @@ inline bool gemm_pp_ok(int N, int ldc, int ldr, const void* C, const void* bias,
   return act != ACT_SWIGLU && N % 8 == 0 && ldc % 8 == 0 && al(C) && (R == nullptr || (ldr % 8 == 0 && al(R)));
 }
 
-template <typename T, typename OutT, int NW, int BM, int BN, int GM, int GN, int STAGES, int BK = 64>
+template <typename T, typename OutT, int NW, int BM, int BN, int GM, int GN, int STAGES, int BK = 64, int OCC = 2>
 void launch_gemm_pp(const T* A, int lda, const T* W, int ldw, OutT* C, int ldc, const T* bias, const T* R, int ldr,
                     int M, int N, int K, float alpha, int act, hipStream_t s) {
   const int nwg = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
   const dim3 grid(nwg), block(64 * NW);
   if (bias && R)
-    hipLaunchKernelGGL((gemm_pp_kernel<T, OutT, NW, BM, BN, GM, GN, STAGES, true, true, BK>), grid, block, 0, s, A, lda, W,
+    hipLaunchKernelGGL((gemm_pp_kernel<T, OutT, NW, BM, BN, GM, GN, STAGES, true, true, BK, OCC>), grid, block, 0, s, A, lda, W,
                        ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act);
   else if (bias)
-    hipLaunchKernelGGL((gemm_pp_kernel<T, OutT, NW, BM, BN, GM, GN, STAGES, true, false, BK>), grid, block, 0, s, A, lda, W,
+    hipLaunchKernelGGL((gemm_pp_kernel<T, OutT, NW, BM, BN, GM, GN, STAGES, true, false, BK, OCC>), grid, block, 0, s, A, lda, W,
                        ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act);
   else if (R)
-    hipLaunchKernelGGL((gemm_pp_kernel<T, OutT, NW, BM, BN, GM, GN, STAGES, false, true, BK>), grid, block, 0, s, A, lda, W,
+    hipLaunchKernelGGL((gemm_pp_kernel<T, OutT, NW, BM, BN, GM, GN, STAGES, false, true, BK, OCC>), grid, block, 0, s, A, lda, W,
                        ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act);
   else
-    hipLaunchKernelGGL((gemm_pp_kernel<T, OutT, NW, BM, BN, GM, GN, STAGES, false, false, BK>), grid, block, 0, s, A, lda,
+    hipLaunchKernelGGL((gemm_pp_kernel<T, OutT, NW, BM, BN, GM, GN, STAGES, false, false, BK, OCC>), grid, block, 0, s, A, lda,
                        W, ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act);
 }
 

@@ -534,6 +534,37 @@ def test_linear_residual_ln_all_tiles(cfg, M):
     _close(outs[1], outs[0], 1e-2, 1e-2)
 
 
+@pytest.mark.parametrize("M,K", [(32, 768), (4096, 768), (4097, 768), (4096, 3072), (200, 800), (64, 832)])
+def test_linear_rowln_vs_fp32(M, K):
+    """Full-row GEMM + bias + residual + LayerNorm (gemm_rowln.hip) against the
+    fp32 reference: partial last block (M = 4097, 200), K steps not a multiple of
+    the 3-step unroll (800 = 25 steps, 832 = 26), FFN-down's K = 3072.  Repeat
+    launches are bit-identical (no atomics: the statistics are block-local)."""
+    ops = _ops()
+    torch.manual_seed(M + K)
+    N = 768
+    x = (torch.randn(M, K, device="cuda") * 1.5).to(torch.bfloat16)
+    w = (torch.randn(N, K, device="cuda") * K ** -0.5).to(torch.bfloat16)
+    b = (torch.randn(N, device="cuda") * 0.1).to(torch.bfloat16)
+    r = (torch.randn(M, N, device="cuda") * 2 + 0.5).to(torch.bfloat16)
+    g = (1 + 0.2 * torch.randn(N, device="cuda")).to(torch.bfloat16)
+    be = (0.1 * torch.randn(N, device="cuda")).to(torch.bfloat16)
+    ref = ops.linear_residual_ln_ref(x, w, b, r, g, be)
+    wp = ops.pack_rowln_weight(w)
+    y1 = ops.linear_rowln(x, wp, b, r, g, be, 1e-12)
+    y2 = ops.linear_rowln(x, wp, b, r, g, be, 1e-12)
+    torch.cuda.synchronize()
+    _close(y1, ref, 3e-2, 3e-2)
+    assert torch.equal(y1, y2)
+    # row-strided operands (a CLS-style view of x, a wider output buffer)
+    xs = torch.zeros(M, K + 64, device="cuda", dtype=torch.bfloat16)
+    xs[:, :K] = x
+    ob = torch.full((M, N + 32), float("nan"), device="cuda", dtype=torch.bfloat16)
+    ops.linear_rowln(xs[:, :K], wp, b, r, g, be, 1e-12, out=ob[:, :N])
+    torch.cuda.synchronize()
+    assert torch.equal(ob[:, :N], y1) and torch.isnan(ob[:, N:].float()).all()
+
+
 def test_layer_norm_row_strided_view_and_embed_zeroes_stats():
     ops = _ops()
     torch.manual_seed(1)
