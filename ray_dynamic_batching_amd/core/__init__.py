@@ -50,7 +50,8 @@ from typing import Any, Dict, List, Optional, Sequence, Tuple
 
 __all__ = ["init", "is_initialized", "shutdown", "remote", "get", "put", "wait", "kill", "get_actor",
            "get_gpu_ids", "cluster_resources", "available_resources", "timeline", "ObjectRef", "ActorHandle",
-           "RayError", "RayTaskError", "RayActorError", "GetTimeoutError", "state", "util", "data", "dag"]
+           "nodes", "get_runtime_context", "RayError", "RayTaskError", "RayActorError", "GetTimeoutError",
+           "TaskUnschedulableError", "state", "util", "data", "dag"]
 
 
 class RayError(Exception):
@@ -72,6 +73,10 @@ class RayActorError(RayError):
 
 class GetTimeoutError(RayError, TimeoutError):
     pass
+
+
+class TaskUnschedulableError(RayError):
+    """A hard scheduling constraint no node satisfies (e.g. node affinity to an unknown node)."""
 
 
 # ---------------------------------------------------------------------------
@@ -170,6 +175,52 @@ def available_resources() -> Dict[str, float]:
     ctx = _require_ctx()
     free = sum(s["free"] for s in ctx.allocator.snapshot())
     return {"CPU": float(ctx.num_cpus), "GPU": float(free)}
+
+
+def _node_id() -> str:
+    """This host's node id (56 hex chars, like Ray's NodeID): derived from the
+    hostname and the kernel boot id, so every process on the node agrees."""
+    import hashlib
+    import socket
+
+    try:
+        with open("/proc/sys/kernel/random/boot_id") as f:
+            boot = f.read().strip()
+    except OSError:
+        boot = ""
+    return hashlib.sha256(f"{socket.gethostname()}/{boot}".encode()).hexdigest()[:56]
+
+
+def nodes() -> List[Dict[str, Any]]:
+    """``ray.nodes()``: this single node (multi-node is out of scope)."""
+    import socket
+
+    return [{"NodeID": _node_id(), "Alive": True, "NodeManagerAddress": "127.0.0.1",
+             "NodeManagerHostname": socket.gethostname(), "Resources": cluster_resources()}]
+
+
+class RuntimeContext:
+    """``ray.get_runtime_context()`` subset: node / job ids, namespace and the
+    accelerators this worker was pinned to."""
+
+    def get_node_id(self) -> str:
+        return _node_id()
+
+    def get_job_id(self) -> str:
+        env = getattr(_tls, "env", None) or _WORKER
+        return env.get("RDB_CORE_JOB_ID", os.environ.get("RDB_CORE_JOB_ID", f"{os.getpid():08x}"))
+
+    @property
+    def namespace(self) -> str:
+        env = getattr(_tls, "env", None) or _WORKER
+        return env.get("RDB_CORE_NAMESPACE", _ctx.namespace if _ctx is not None else "default")
+
+    def get_accelerator_ids(self) -> Dict[str, List[str]]:
+        return {"GPU": [str(g) for g in get_gpu_ids()]}
+
+
+def get_runtime_context() -> RuntimeContext:
+    return RuntimeContext()
 
 
 def get_gpu_ids() -> List[int]:
@@ -556,6 +607,15 @@ def _pg_option(o: Dict[str, Any]):
     """(placement group, bundle index) from ``scheduling_strategy=`` or the
     legacy ``placement_group=`` / ``placement_group_bundle_index=`` options."""
     st = o.get("scheduling_strategy")
+    if isinstance(st, str):
+        if st not in ("DEFAULT", "SPREAD"):
+            raise ValueError(f"unknown scheduling_strategy {st!r} (DEFAULT, SPREAD or a strategy object)")
+        return None, -1
+    if st is not None and hasattr(st, "node_id"):    # NodeAffinitySchedulingStrategy
+        if st.node_id != _node_id() and not st.soft:
+            raise TaskUnschedulableError(f"node affinity to {st.node_id!r}: no such alive node "
+                                         f"(this node is {_node_id()})")
+        return None, -1
     if st is not None and hasattr(st, "placement_group"):
         return st.placement_group, int(st.placement_group_bundle_index)
     if o.get("placement_group") not in (None, "default"):
@@ -805,6 +865,10 @@ class RemoteFunction:
 
     def _remote_now(self, ctx, args, kwargs) -> ObjectRef:
         num_gpus = self._options.get("num_gpus", 0)
+        try:
+            _pg_option(self._options)          # validates scheduling_strategy (node affinity)
+        except TaskUnschedulableError as e:
+            return _failed_ref(e)
         if not num_gpus:
             fn = self._fn
 
@@ -818,7 +882,11 @@ class RemoteFunction:
 
             return _traced(ObjectRef(ctx.tasks.submit(run)), self.__name__, "tasks")
         # a GPU task runs in a one-shot process pinned to its GPUs
-        host = ActorClass(_FnHost, {"num_gpus": num_gpus}).remote(self._fn)
+        host_opts = {"num_gpus": num_gpus}
+        for k in ("scheduling_strategy", "placement_group", "placement_group_bundle_index"):
+            if k in self._options:
+                host_opts[k] = self._options[k]
+        host = ActorClass(_FnHost, host_opts).remote(self._fn)
         ref = host.run.remote(args, kwargs)
         ref._fut.add_done_callback(lambda _f: threading.Thread(target=kill, args=(host,), daemon=True).start())
         return ref

@@ -250,3 +250,47 @@ def test_actor_death_fails_pending_calls():
             ray.get(h.pid.remote(), timeout=30)
     finally:
         ray.shutdown()
+
+
+def test_nodes_runtime_context_and_node_affinity():
+    """ray.nodes() / get_runtime_context() / NodeAffinitySchedulingStrategy on the
+    single node: affinity to this node schedules, to an unknown node fails the ref
+    (hard) or falls back to this node (soft); string strategies DEFAULT / SPREAD."""
+    import pytest
+
+    from ray_dynamic_batching_amd import core
+    from ray_dynamic_batching_amd.core.util.scheduling_strategies import NodeAffinitySchedulingStrategy
+
+    core.init(num_gpus=0, local_mode=True, ignore_reinit_error=True)
+    try:
+        ns = core.nodes()
+        assert len(ns) == 1 and ns[0]["Alive"]
+        me = core.get_runtime_context().get_node_id()
+        assert ns[0]["NodeID"] == me and len(me) == 56
+
+        @core.remote
+        def where():
+            return core.get_runtime_context().get_node_id()
+
+        assert core.get(where.options(scheduling_strategy=NodeAffinitySchedulingStrategy(me, soft=False)).remote()) == me
+        assert core.get(where.options(scheduling_strategy="SPREAD").remote()) == me
+        bad = NodeAffinitySchedulingStrategy("ff" * 28, soft=False)
+        with pytest.raises(core.TaskUnschedulableError):
+            core.get(where.options(scheduling_strategy=bad).remote())
+        soft = NodeAffinitySchedulingStrategy("ff" * 28, soft=True)
+        assert core.get(where.options(scheduling_strategy=soft).remote()) == me
+        with pytest.raises(ValueError):
+            where.options(scheduling_strategy="PACKED_TIGHT").remote()
+
+        @core.remote
+        class A:
+            def node(self):
+                return core.get_runtime_context().get_node_id()
+
+        a = A.options(scheduling_strategy=NodeAffinitySchedulingStrategy(me, soft=False)).remote()
+        assert core.get(a.node.remote()) == me
+        with pytest.raises(core.TaskUnschedulableError):
+            A.options(scheduling_strategy=bad).remote()
+        assert core.get_runtime_context().get_accelerator_ids() == {"GPU": []}
+    finally:
+        core.shutdown()
