@@ -52,11 +52,11 @@ __global__ void fill_rand(bf16* p, size_t n, uint32_t seed, float scale) {
 struct Shape { int M, N, K; const char* name; };
 struct Variant { std::string name; std::function<void(const bf16*, const bf16*, const bf16*, bf16*, int, int, int, hipStream_t)> run; };
 
-template <int NW, int BM, int BN, int GM, int GN, int S, int BK = 64, int OCC = 2>
+template <int NW, int BM, int BN, int GM, int GN, int S, int BK = 64, int OCC = 2, int ACT = ACT_NONE>
 Variant pp(const char* nm) {
   return {nm, [](const bf16* A, const bf16* W, const bf16* b, bf16* C, int M, int N, int K, hipStream_t s) {
             launch_gemm_pp<bf16, bf16, NW, BM, BN, GM, GN, S, BK, OCC>(A, K, W, K, C, N, b, nullptr, 0, M, N, K, 1.f,
-                                                                   ACT_NONE, s);
+                                                                   ACT, s);
           }};
 }
 Variant e8(const char* nm) {
@@ -73,6 +73,7 @@ Variant core1(const char* nm) {
                                                                                1.f, ACT_NONE, s);
           }};
 }
+#if !defined(LAB_SET_GELU)   // the whole tile table: minutes of compile time
 Variant core(int cfg) {
   char nm[64];
   snprintf(nm, sizeof nm, "core cfg%d %dx%d/%dw", cfg, kTileBM[cfg], kTileBN[cfg], 4 * kTileNW[cfg] / 4);
@@ -81,6 +82,7 @@ Variant core(int cfg) {
             launch_mfma_gemm<bf16, bf16, DenseLoader>(p, W, K, C, N, b, nullptr, 0, M, N, K, 1.f, ACT_NONE, s, cfg);
           }};
 }
+#endif
 
 int main(int argc, char** argv) {
   int iters = 50;
@@ -97,7 +99,18 @@ int main(int argc, char** argv) {
                                {4096, 768, 3072, "bert.ffn2"},
                                {4096, 4096, 4096, "sq4096"}};
   std::vector<Variant> vs = {
-#if defined(LAB_SET_OCC)
+#if defined(LAB_SET_GELU)
+      // epilogue cost: the FFN-up tile with and without its GELU
+      pp<8, 256, 256, 2, 2, 4, 32, 2, ACT_NONE>("pp8 256x256 bk32 s4 none"),
+      pp<8, 256, 256, 2, 2, 4, 32, 2, ACT_GELU>("pp8 256x256 bk32 s4 gelu"),
+      pp<8, 256, 256, 2, 2, 4, 32, 2, ACT_GELU_TANH>("pp8 256x256 bk32 s4 gelu_tanh"),
+      pp<8, 256, 128, 2, 2, 3, 64, 2, ACT_NONE>("pp8 256x128 bk64 s3 none"),
+      pp<8, 256, 128, 2, 2, 3, 64, 2, ACT_GELU>("pp8 256x128 bk64 s3 gelu"),
+      // two co-resident blocks per CU: one block's GELU epilogue beside the other's MFMAs
+      pp<8, 128, 256, 1, 4, 3, 32, 4, ACT_GELU>("pp8 128x256 bk32 s3 occ4 gelu"),
+      pp<8, 256, 128, 2, 2, 3, 32, 4, ACT_GELU>("pp8 256x128 bk32 s3 occ4 gelu"),
+      pp<8, 256, 256, 2, 2, 4, 32, 2, ACT_SILU>("pp8 256x256 bk32 s4 silu"),
+#elif defined(LAB_SET_OCC)
       // occupancy: one 8-wave block per CU (OCC 2) vs two co-resident blocks (OCC 4, LDS <= 80 KiB)
       pp<8, 256, 128, 2, 2, 3, 64, 2>("pp8 256x128 bk64 s3"),
       pp<8, 256, 128, 2, 2, 3, 32, 4>("pp8 256x128 bk32 s3 occ4"),

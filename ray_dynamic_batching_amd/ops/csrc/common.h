@@ -58,18 +58,38 @@ __device__ __forceinline__ float fast_erf(float x) {
 template <int ACT>
 __device__ __forceinline__ float apply_act(float x) {
   if constexpr (ACT == ACT_GELU) {
+#ifdef RDB_GELU_OLD   // A/B build: the previous formulation
     return 0.5f * x * (1.0f + fast_erf(x * 0.70710678118654752f));
+#endif
+    // exact-erf GELU, rewritten so adjacent calls pack into v_pk_*_f32 (no
+    // copysign, the 1/sqrt2 folded into the constants):
+    //   0.5 x (1 + erf(x/sqrt2)) = 0.5 x + 0.5 |x| erf(|x|/sqrt2)
+    // erf(a) = 1 - t P(t) exp(-a^2), t = 1 / (1 + p a)  (A&S 7.1.26, |err| <= 1.5e-7)
+    // exp(-x^2/2) = exp2(-x^2 * log2(e) / 2) on v_exp_f32 (argument <= 0)
+    const float ax = fabsf(x);
+    const float t = __builtin_amdgcn_rcpf(fmaf(0.23164193f, ax, 1.0f));   // 0.3275911 / sqrt2
+    float p = fmaf(1.061405429f, t, -1.453152027f);
+    p = fmaf(p, t, 1.421413741f);
+    p = fmaf(p, t, -0.284496736f);
+    p = fmaf(p, t, 0.254829592f);
+    const float e = __builtin_amdgcn_exp2f(x * x * -0.72134752044448170f);
+    const float erfa = fmaf(-(p * t), e, 1.0f);
+    return fmaf(0.5f * ax, erfa, 0.5f * x);
   } else if constexpr (ACT == ACT_RELU) {
     return fmaxf(x, 0.0f);
   } else if constexpr (ACT == ACT_TANH) {
     return tanhf(x);
   } else if constexpr (ACT == ACT_SILU) {
-    return x / (1.0f + __expf(-x));
+    // x * sigmoid(x) with v_exp_f32 + v_rcp_f32 (1 ulp) instead of an IEEE
+    // division sequence (~10 VALU per element); exp2 overflow -> rcp(inf) = 0
+    return x * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(x * -1.4426950408889634f));
   } else if constexpr (ACT == ACT_GELU_TANH) {
-    const float c = 0.7978845608028654f;
-    return 0.5f * x * (1.0f + tanhf(c * (x + 0.044715f * x * x * x)));
+    // 0.5 x (1 + tanh(u)) == x * sigmoid(2u), u = sqrt(2/pi) (x + 0.044715 x^3):
+    // the same function without ocml's branchy tanhf (which spilled the GEMM epilogue)
+    const float u2 = x * fmaf(-0.10294324f, x * x, -2.3022082f);   // -2u * log2(e)
+    return x * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(u2));
   } else if constexpr (ACT == ACT_SIGMOID) {
-    return 1.0f / (1.0f + __expf(-x));
+    return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(x * -1.4426950408889634f));
   } else {
     return x;
   }

@@ -261,6 +261,22 @@ struct StagedEpi {
   static_assert(BN % 8 == 0 && RC >= 16 && BM % RC == 0, "staged epilogue geometry");
 };
 
+// 16-bit staging rows (residual-free epilogue): BN x 2 B + 32 B, so the 16 rows
+// of one ds_write_b64 wave instruction start 8 banks apart.
+template <int BM, int BN, int SMEM_BYTES>
+struct StagedEpi16 {
+  static constexpr int ROWB = BN * 2 + 32;
+  static constexpr int RC_MAX = (SMEM_BYTES / ROWB) / 16 * 16;
+  static constexpr int pick() {
+    int rc = RC_MAX < BM ? RC_MAX : BM;
+    while (rc > 16 && BM % rc) rc -= 16;
+    return rc;
+  }
+  static constexpr int RC = pick();
+  static constexpr int NV = BN / 8;
+  static_assert(BN % 8 == 0 && RC >= 16 && BM % RC == 0, "staged 16-bit epilogue geometry");
+};
+
 // BIAS_LDS >= 0: the tile's bias was staged (f32) at smem + BIAS_LDS by the
 // kernel's prologue, so no bias registers stay live across the epilogue.
 template <typename T, typename OutT, int BM, int BN, int SMEM_BYTES, int NT, int TM, int TN, bool HAS_BIAS,
@@ -288,6 +304,60 @@ __device__ __forceinline__ void staged_epilogue(char* smem, const f32x4 (&acc)[T
 #pragma unroll
       for (int q = 0; q < 4; ++q) bv[i][q] = 0.f;
     }
+  }
+#ifdef RDB_EPI_F32_STAGING
+  constexpr bool kStage16 = false;   // A/B build: the f32-staged epilogue for every GEMM
+#else
+  constexpr bool kStage16 = !HAS_RES && sizeof(OutT) == 2;
+#endif
+  if constexpr (kStage16) {
+    // No residual: bias + activation run once on the accumulator registers,
+    // the tile is parked as 16-bit output (half the LDS traffic of f32, twice
+    // the rows per chunk) and phase 2 only moves 16-B row segments to global.
+    typedef StagedEpi16<BM, BN, SMEM_BYTES> E16;
+    // bias + activation on EVERY wave's fragments first (all 8 waves busy: a
+    // row chunk may belong to one wave group only), packed to 16-bit pairs
+    u32x2 pk[TN][TM];
+#pragma unroll
+    for (int j = 0; j < TM; ++j)
+#pragma unroll
+      for (int i = 0; i < TN; ++i) {
+        const int nt = col_base + i * 16 + fg * 4;
+        f32x4 v = acc[i][j] * alpha;
+        if constexpr (BREG) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) v[q] += bv[i][q];
+        } else if constexpr (HAS_BIAS) {
+          v += *reinterpret_cast<const f32x4*>(smem + BIAS_LDS + nt * 4);
+        }
+        OutT o4[4] = {(OutT)actf(v[0]), (OutT)actf(v[1]), (OutT)actf(v[2]), (OutT)actf(v[3])};
+        pk[i][j] = *reinterpret_cast<const u32x2*>(o4);
+      }
+#pragma unroll 1
+    for (int c = 0; c < BM / E16::RC; ++c) {
+#pragma unroll
+      for (int j = 0; j < TM; ++j) {
+        const int rt = row_base + j * 16 + fr - c * E16::RC;
+        if (rt >= 0 && rt < E16::RC) {
+#pragma unroll
+          for (int i = 0; i < TN; ++i) {
+            const int nt = col_base + i * 16 + fg * 4;
+            *reinterpret_cast<u32x2*>(smem + rt * E16::ROWB + nt * 2) = pk[i][j];
+          }
+        }
+      }
+      __syncthreads();
+#pragma unroll 4
+      for (int idx = tid; idx < E16::RC * E16::NV; idx += NT) {
+        const int r = idx / E16::NV, vcol = idx - r * E16::NV;
+        const int m = m0 + c * E16::RC + r, n = n0 + vcol * 8;
+        if (m < M && n < N)
+          *reinterpret_cast<u32x4*>(C + (size_t)m * ldc + n) =
+              *reinterpret_cast<const u32x4*>(smem + r * E16::ROWB + vcol * 16);
+      }
+      __syncthreads();
+    }
+    return;
   }
 #pragma unroll 1
   for (int c = 0; c < BM / E::RC; ++c) {
@@ -877,14 +947,19 @@ namespace rdb {
 // 19..22 are the ping-pong kernel (gemm_pp.h, 8 waves in two staggered groups;
 // 22 = 256x256 at BK = 32 with 4 LDS stages, the best tile on large GEMMs:
 // 1.06 PF/s at 4096^3 vs 0.90 for 19, bench/gemm_lab).
-constexpr int kNumTiles = 23;
-//                                 0    1    2    3    4    5    6    7    8    9   10   11   12 | 8-wave: 13   14   15   16   17   18 | pp: 19   20   21   22
-constexpr int kTileBM[kNumTiles] = {128, 64, 128, 64, 128, 192, 256, 128, 128, 64, 128, 256, 128, 256, 128, 256, 256, 128, 256, 256, 256, 128, 256};
-constexpr int kTileBN[kNumTiles] = {128, 128, 64, 64, 192, 128, 128, 256, 144, 96, 96, 144, 48, 128, 256, 192, 144, 96, 96, 128, 144, 256, 256};
-constexpr int kTileWGM[kNumTiles] = {2, 2, 2, 2, 2, 2, 2, 2, 4, 2, 2, 4, 4, 4, 2, 4, 8, 4, 8, 4, 8, 2, 4};
-constexpr int kTileNW[kNumTiles] = {4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 8, 8, 8, 8, 8, 8, 8, 8, 8, 8};
+// 23 = 256x128 at BK = 32 with 3 stages (74 KiB) compiled for TWO co-resident
+// blocks per CU (<= 128 VGPRs): one block's epilogue (FFN-up's GELU: ~13k
+// VALU cycles per tile) runs beside the other block's MFMAs -- 3 % over 22 on
+// the FFN-up shape in the two-stream lab (profiles/gemm_lab_r3_gelu_epilogue.txt).
+constexpr int kNumTiles = 24;
+//                                 0    1    2    3    4    5    6    7    8    9   10   11   12 | 8-wave: 13   14   15   16   17   18 | pp: 19   20   21   22   23
+constexpr int kTileBM[kNumTiles] = {128, 64, 128, 64, 128, 192, 256, 128, 128, 64, 128, 256, 128, 256, 128, 256, 256, 128, 256, 256, 256, 128, 256, 256};
+constexpr int kTileBN[kNumTiles] = {128, 128, 64, 64, 192, 128, 128, 256, 144, 96, 96, 144, 48, 128, 256, 192, 144, 96, 96, 128, 144, 256, 256, 128};
+constexpr int kTileWGM[kNumTiles] = {2, 2, 2, 2, 2, 2, 2, 2, 4, 2, 2, 4, 4, 4, 2, 4, 8, 4, 8, 4, 8, 2, 4, 4};
+constexpr int kTileNW[kNumTiles] = {4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 8, 8, 8, 8, 8, 8, 8, 8, 8, 8, 8};
 
 inline int tile_blocks_per_cu(int cfg) {
+  if (cfg == 23) return 2;
   if (cfg >= 19) return 1;
   const int q = 8 * kTileNW[cfg];
   const int bnp = (kTileBN[cfg] + q - 1) / q * q;
@@ -985,6 +1060,9 @@ void launch_mfma_gemm_t(const P& ap, const T* W, int ldw, OutT* C, int ldc, cons
             return;
           case 22: launch_gemm_pp<T, OutT, 8, 256, 256, 2, 2, 4, 32>(static_cast<const T*>(ap.A), ap.lda, W, ldw, C,
                                                                       ldc, bias, R, ldr, M, N, K, alpha, act, s);
+            return;
+          case 23: launch_gemm_pp<T, OutT, 8, 256, 128, 2, 2, 3, 32, 4>(static_cast<const T*>(ap.A), ap.lda, W, ldw,
+                                                                         C, ldc, bias, R, ldr, M, N, K, alpha, act, s);
             return;
           default: break;
         }
