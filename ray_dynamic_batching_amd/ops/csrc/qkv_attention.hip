@@ -48,8 +48,10 @@ struct QkvLn {
 // for two sequences, 30 % fewer bytes per FLOP through the per-CU L2 -> LDS
 // path that bounds the projection; B*H/2 blocks.  Waves 0..3 then run the
 // attention of the first sequence, 4..7 of the second.
-template <typename T, int NW, int STAGES, bool LNA, int WGM_ = (NW == 8 ? 4 : 2), int SEQ = 1>
-__global__ void __launch_bounds__(64 * NW, NW == 8 && (STAGES == 3 || SEQ == 2) ? 1 : 2)
+// OCC (> 0) overrides the waves-per-SIMD register budget (4 = two co-resident
+// 8-wave blocks per CU).
+template <typename T, int NW, int STAGES, bool LNA, int WGM_ = (NW == 8 ? 4 : 2), int SEQ = 1, int OCC = 0>
+__global__ void __launch_bounds__(64 * NW, OCC > 0 ? OCC : (NW == 8 && (STAGES == 3 || SEQ == 2) ? 1 : 2))
 qkv_attn_kernel(DenseParams ap, const T* __restrict__ W, const T* __restrict__ bias, int S, int H,
                 const int* __restrict__ lens, T* __restrict__ out, int ld_out, float scale_log2e, QkvLn ln,
                 const int* __restrict__ kids, int pad) {
@@ -176,7 +178,11 @@ qkv_attn_kernel(DenseParams ap, const T* __restrict__ W, const T* __restrict__ b
     __syncthreads();
   }
   if (kids != nullptr) {
-    __shared__ int s_cnt[NW];
+    // the per-wave key counts live in the idle tail of the staging LDS (past the
+    // attention operands): a separate __shared__ array would push the 2-stage
+    // block to 81,952 B, just over the 80 KiB that lets two blocks share a CU
+    int* s_cnt = reinterpret_cast<int*>(smem + STAGES * kStage - 64);
+    static_assert(V_OFF + D * VT_LD * 2 <= STAGES * kStage - 64 && NW * 4 <= 64, "key-count slot");
     const unsigned long long bal = __ballot(kid != pad);
     if (lane == 0) s_cnt[wid] = __popcll(bal);
     __syncthreads();
@@ -340,6 +346,8 @@ qkv_attn_kernel(DenseParams ap, const T* __restrict__ W, const T* __restrict__ b
 // cfg: 0 = 8 waves (4x2) / 3 stages (1 block per CU), 1 = 8 waves (4x2) / 2 stages, 2 = 4 waves / 2 stages,
 //      3 = 8 waves (2x4: 64x48 wave tiles, fewer LDS fragment reads per MFMA) / 2 stages,
 //      4 = two sequences per block (256 x 192 tile, 8 waves 4x2, 2 stages; S == 128 only, else cfg 3)
+// The 2-stage configs (1, 3) take exactly 80 KiB of LDS and <= 128 VGPRs: two
+// blocks share a CU, one block's softmax beside the other's projection MFMAs.
 constexpr int kNumQkvAttnCfgs = 5;
 
 template <typename T, bool LNA>
