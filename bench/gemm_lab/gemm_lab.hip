@@ -73,7 +73,7 @@ Variant core1(const char* nm) {
                                                                                1.f, ACT_NONE, s);
           }};
 }
-#if !defined(LAB_SET_GELU)   // the whole tile table: minutes of compile time
+#if !defined(LAB_SET_GELU) && !defined(LAB_SET_FFN2)   // the whole tile table: minutes of compile time
 Variant core(int cfg) {
   char nm[64];
   snprintf(nm, sizeof nm, "core cfg%d %dx%d/%dw", cfg, kTileBM[cfg], kTileBN[cfg], 4 * kTileNW[cfg] / 4);
@@ -99,7 +99,14 @@ int main(int argc, char** argv) {
                                {4096, 768, 3072, "bert.ffn2"},
                                {4096, 4096, 4096, "sq4096"}};
   std::vector<Variant> vs = {
-#if defined(LAB_SET_GELU)
+#if defined(LAB_SET_FFN2)
+      // FFN-down (N = 768) on wider tiles: fewer L2 bytes per FLOP, fewer blocks
+      pp<8, 256, 128, 2, 2, 3, 64>("pp8 256x128 bk64 s3"),
+      pp<8, 256, 192, 2, 2, 4, 32>("pp8 256x192 2x2 bk32 s4"),
+      pp<8, 256, 192, 1, 4, 4, 32>("pp8 256x192 1x4 bk32 s4"),
+      pp<8, 256, 192, 2, 2, 3, 32>("pp8 256x192 2x2 bk32 s3"),
+      pp<8, 256, 256, 2, 2, 4, 32>("pp8 256x256 bk32 s4"),
+#elif defined(LAB_SET_GELU)
       // epilogue cost: the FFN-up tile with and without its GELU
       pp<8, 256, 256, 2, 2, 4, 32, 2, ACT_NONE>("pp8 256x256 bk32 s4 none"),
       pp<8, 256, 256, 2, 2, 4, 32, 2, ACT_GELU>("pp8 256x256 bk32 s4 gelu"),
