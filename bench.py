@@ -6,10 +6,11 @@ dynamic batching <= 32, one replica per MI355X (BASELINE.json metric).
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
-Every rank is one replica process pinned to its GPU (LOCAL_RANK).  Rank 0 also
-creates the shared-memory job and runs the ingress: a native closed-loop load
-generator whose requests go through the power-of-two-choices router over the
-shm queue depths of ALL replicas.  Each request is one 128-token sequence
+Every rank is one replica process pinned to its GPU (LOCAL_RANK).  Rank 0
+creates the shared-memory job; every rank runs an ingress: a native
+closed-loop load generator whose requests go through the power-of-two-choices
+router over the shm queue depths of ALL replicas (`--ingress rank0` keeps one
+node-wide ingress on rank 0).  Each request is one 128-token sequence
 (synthetic token ids, random-init weights); each replica's native engine
 coalesces up to 32 requests or 5 ms, pads to a bucket, gathers the payloads
 H2D on a side stream, replays the hipGraph of the batched forward, and returns
@@ -50,9 +51,12 @@ def parse():
     ap.add_argument("--tune-streams", type=int, default=0,
                     help="GEMM tile autotuning objective: throughput with this many concurrent streams "
                          "(0 = --compute-streams)")
+    ap.add_argument("--ingress", default="per-rank", choices=["per-rank", "rank0"],
+                    help="per-rank: every rank runs a load generator routing over all replicas; "
+                         "rank0: one node-wide ingress on rank 0")
     ap.add_argument("--ingress-threads", type=int, default=0,
-                    help="load-generator threads on rank 0, each with its own client / completion ring "
-                         "(0 = one per 2 GPUs, at most 4)")
+                    help="load-generator threads per ingress, each with its own client / completion ring "
+                         "(0 = 1 per rank with --ingress per-rank; one per 2 GPUs, at most 4, with rank0)")
     ap.add_argument("--rehearse-one-gpu", action="store_true",
                     help="rehearsal only: every rank's replica on cuda:0, gloo instead of RCCL (a 1-GPU box "
                          "running the N-rank protocol with real engines); never a measurement")
@@ -136,7 +140,7 @@ def main():
     name = f"bench_{port}"
     n = world
     if rank == 0:
-        job = rjob.Job(name, create=True, n_replicas=n, n_queues=n, n_clients=8, req_capacity=4096,
+        job = rjob.Job(name, create=True, n_replicas=n, n_queues=n, n_clients=max(8, n * max(4, args.ingress_threads)), req_capacity=4096,
                        req_slot_bytes=args.seq * 4, cmp_capacity=16384, cmp_slot_bytes=64)
     barrier()
     if rank != 0:
@@ -167,43 +171,46 @@ def main():
 
     result = {}
     per_step = args.max_batch * n
-    if rank == 0:
-        # The ingress: G native generator threads (GIL released inside run()),
-        # each with its own client and completion ring, all routing through the
-        # power-of-two choice over every replica's queue depth.  One thread
-        # sustains ~1 M req/s of bare ring traffic; several keep submission and
-        # completion draining off the critical path at 8 GPUs x ~29k req/s.
-        from concurrent.futures import ThreadPoolExecutor
+    # The ingress: every rank runs G native generator threads (GIL released
+    # inside run()), each with its own client and completion ring, all routing
+    # through the power-of-two choice over EVERY replica's queue depth -- like
+    # Serve, where each proxy / handle owns a router over all replicas.  One
+    # ingress per rank keeps submission and completion draining spread over
+    # the node's processes instead of funnelling 8 GPUs' traffic through rank 0.
+    # `--ingress rank0` keeps the single node-wide ingress on rank 0.
+    from concurrent.futures import ThreadPoolExecutor
 
-        G = args.ingress_threads or min(4, max(1, n // 2))
-        g = torch.Generator().manual_seed(1234)
+    drivers = range(n) if args.ingress == "per-rank" else [0]
+    n_drv = len(drivers)
+    is_driver = rank in drivers
+    G = args.ingress_threads or (1 if args.ingress == "per-rank" else min(4, max(1, n // 2)))
+    if is_driver:
+        g = torch.Generator().manual_seed(1234 + rank)
         payloads = []
         for _ in range(256):
             ids = torch.randint(1, cfg.vocab_size, (args.seq,), generator=g, dtype=torch.int32)
             ids[0] = 101
             payloads.append(ids.numpy().tobytes())
-        clients = [rjob.Client(job, seed=1234 + i) for i in range(G)]
+        clients = [rjob.Client(job, seed=1234 + 64 * rank + i) for i in range(G)]
         gens = [rjob.LoadGen(c, 0, payloads) for c in clients]
         pool = ThreadPoolExecutor(G)
-        conc = args.concurrency * n
-        rate = args.rate * n
+        slot = list(drivers).index(rank)
 
-        def split(total):
-            return [total // G + (1 if i < total % G else 0) for i in range(G)]
+        def share(total, k, i):
+            return total // k + (1 if i < total % k else 0)
+
+        conc = share(args.concurrency * n, n_drv, slot)
+        rate = args.rate * n / n_drv
 
         def drive(total, record, timeout_s):
-            parts = split(total)
-            cs, rs = split(conc), [rate / G] * G
-            futs = [pool.submit(gens[i].run, parts[i], max(1, cs[i]), rs[i], 0.0, record, timeout_s)
-                    for i in range(G)]
+            total = share(total, n_drv, slot)
+            futs = [pool.submit(gens[i].run, share(total, G, i), max(1, share(conc, G, i)), rate / G, 0.0,
+                                record, timeout_s) for i in range(G)]
             res = [f.result() for f in futs]
-            if not record:
-                return res[0]
-            for lg_i in gens[1:]:
-                gens[0].merge_from(lg_i)
-            out = {k: sum(r[k] for r in res) for k in ("ok", "completed", "dropped", "errors", "issued")}
-            out["latency"] = gens[0].latency()
-            return out
+            if record:
+                for lg_i in gens[1:]:
+                    gens[0].merge_from(lg_i)
+            return {k: sum(r[k] for r in res) for k in ("ok", "completed", "dropped", "errors", "issued")}
 
         drive(args.warmup * per_step, False, 600.0)
     barrier()
@@ -213,7 +220,7 @@ def main():
         rep0 = [job.replica_stats(r) for r in range(n)]
     barrier()
     t0 = time.perf_counter()
-    if rank == 0:
+    if is_driver:
         result = drive(args.steps * per_step, True, 1200.0)
     barrier()
     sync()
@@ -224,6 +231,20 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX, group=host_pg)
         elapsed = t.item()
+        if n_drv > 1:
+            # whole-node counts and latency histogram: every rank's ingress folded into rank 0's
+            counts = [result.get(k, 0) for k in ("ok", "completed", "dropped", "errors", "issued")]
+            c = torch.tensor(counts, dtype=torch.float64)
+            dist.all_reduce(c, group=host_pg)
+            result = dict(zip(("ok", "completed", "dropped", "errors", "issued"), (int(v) for v in c.tolist())))
+            states = [None] * world
+            dist.all_gather_object(states, gens[0].hist_state() if is_driver else None, group=host_pg)
+            if rank == 0:
+                for r, st in enumerate(states):
+                    if r != 0 and st is not None:
+                        gens[0].merge_state(*st)
+    if rank == 0:
+        result["latency"] = gens[0].latency()
     if rank == 0 and args.trace_out:
         from ray_dynamic_batching_amd.utils.tracing import collect, export_chrome_trace, summarize
 
@@ -264,7 +285,7 @@ def main():
             "mean_batch": round(sum(r["batch_items"] for r in rep) / max(1, sum(r["batches"] for r in rep)), 2),
             "gpu_busy_frac": round(sum(r["busy_ms"] for r in rep) / (n * elapsed * 1e3), 3) if elapsed > 0 else None,
             "per_replica_requests": [r["batch_items"] for r in rep],
-            "ingress_threads": G,
+            "ingress": f"{args.ingress} x{G} thread(s)",
         }
         if args.rehearse_one_gpu:
             line["metric"] = "REHEARSAL (all ranks on one GPU, gloo): " + METRIC
@@ -275,7 +296,7 @@ def main():
         if args.json_out:
             with open(args.json_out, "w") as f:
                 json.dump(line, f, indent=1)
-    if rank == 0:
+    if is_driver:
         pool.shutdown()
     runner.stop()
     barrier()

@@ -555,6 +555,22 @@ class LoadGen {
   }
   py::dict latency() const { return hist_dict(hist_); }
 
+  // The recorded latencies as plain numbers (bucket counts, count, sum, max) so
+  // that generators living in OTHER processes can be folded in: bench.py at N
+  // GPUs runs one ingress per rank and merges every rank's histogram on rank 0.
+  py::tuple hist_state() const {
+    std::vector<uint64_t> b(kHistBuckets);
+    for (int i = 0; i < kHistBuckets; ++i) b[i] = hist_.buckets[i].load();
+    return py::make_tuple(b, hist_.count.load(), hist_.sum_ns.load(), hist_.max_ns.load());
+  }
+  void merge_state(const std::vector<uint64_t>& b, uint64_t count, uint64_t sum_ns, uint64_t max_ns) {
+    if (b.size() != (size_t)kHistBuckets) throw std::invalid_argument("histogram state of the wrong size");
+    hist_.count.fetch_add(count);
+    hist_.sum_ns.fetch_add(sum_ns);
+    if (max_ns > hist_.max_ns.load()) hist_.max_ns.store(max_ns);
+    for (int i = 0; i < kHistBuckets; ++i) hist_.buckets[i].fetch_add(b[i]);
+  }
+
  private:
   Client& c_;
   uint32_t model_;
@@ -931,6 +947,9 @@ PYBIND11_MODULE(_rdb_runtime, m) {
            py::arg("rate") = 0.0, py::arg("deadline_ms") = 0.0, py::arg("record") = true,
            py::arg("timeout_s") = 600.0)
       .def("merge_from", &LoadGen::merge_from)
+      .def("hist_state", &LoadGen::hist_state)
+      .def("merge_state", &LoadGen::merge_state, py::arg("buckets"), py::arg("count"), py::arg("sum_ns"),
+           py::arg("max_ns"))
       .def("latency", &LoadGen::latency);
 
   py::class_<Consumer>(m, "Consumer")

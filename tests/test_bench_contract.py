@@ -6,15 +6,19 @@ import os
 import subprocess
 import sys
 
+import pytest
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
         "vs_baseline", "dtype", "data", "config"}
 
 
-def test_bench_two_ranks_echo_backend():
+@pytest.mark.parametrize("ingress", ["per-rank", "rank0"])
+def test_bench_two_ranks_echo_backend(ingress):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
            "127.0.0.1", "--master-port", str(29000 + os.getpid() % 1000), os.path.join(ROOT, "bench.py"), "--gpus", "2",
-           "--steps", "40", "--warmup", "4", "--backend", "echo", "--echo-service-us", "800"]
+           "--steps", "40", "--warmup", "4", "--backend", "echo", "--echo-service-us", "800",
+           "--ingress", ingress]
     out = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=ROOT,
                          env=dict(os.environ, PYTHONPATH=ROOT))
     assert out.returncode == 0, out.stderr[-3000:]
@@ -26,6 +30,8 @@ def test_bench_two_ranks_echo_backend():
     assert d["completed"] == 40 * 32 * 2 and d["errors"] == 0
     assert abs(d["value"] - d["completed"] / (d["ms_per_step"] * d["steps"] / 1e3)) / d["value"] < 0.01
     assert min(d["per_replica_requests"]) > 0
+    assert d["ingress"].startswith(ingress)
+    assert 0 < d["p50_ms"] <= d["p99_ms"]
 
 
 def test_bench_resolves_shipped_tile_table():

@@ -5,11 +5,13 @@ import os
 import subprocess
 import sys
 
+import pytest
+
 from ray_dynamic_batching_amd.runtime import job as rjob
 
 
-def _job(nq, **kw):
-    j = rjob.Job(rjob.unique_job_name("echo"), create=True, n_replicas=nq, n_queues=nq, n_clients=2,
+def _job(nq, n_clients=2, **kw):
+    j = rjob.Job(rjob.unique_job_name("echo"), create=True, n_replicas=nq, n_queues=nq, n_clients=n_clients,
                  req_capacity=1024, req_slot_bytes=256, cmp_capacity=2048, cmp_slot_bytes=64, **kw)
     for q in range(nq):
         j.configure_queue(q, q, 0, 1024, 0.0, True)
@@ -53,6 +55,34 @@ def test_pow2_routing_prefers_less_loaded_replica():
         j.close()
 
 
+def test_loadgen_histogram_state_merges_like_merge_from():
+    """hist_state()/merge_state() fold a generator's latencies across processes
+    (bench.py's per-rank ingress); the result equals the in-process merge_from."""
+    j = _job(2, n_clients=3)
+    servers = [rjob.EchoServer(j, r, [r], max_batch=16, service_us=200.0 * (r + 1)) for r in range(2)]
+    for s in servers:
+        s.start()
+    try:
+        a = rjob.LoadGen(rjob.Client(j, 0), 0, [b"a" * 32])
+        b = rjob.LoadGen(rjob.Client(j, 1), 0, [b"b" * 32])
+        assert a.run(800, 32, 0.0, 0.0, True, 60.0)["ok"] == 800
+        assert b.run(600, 16, 0.0, 0.0, True, 60.0)["ok"] == 600
+        st = b.hist_state()
+        assert len(st[0]) > 0 and st[1] == 600 and sum(st[0]) == 600
+        via_state = rjob.LoadGen(rjob.Client(j, 2), 0, [b"c"])
+        via_state.merge_state(*a.hist_state())
+        via_state.merge_state(*st)
+        a.merge_from(b)
+        assert via_state.latency() == a.latency()
+        assert a.latency()["count"] == 1400
+        with pytest.raises(ValueError):
+            via_state.merge_state([1, 2, 3], 6, 0, 0)
+    finally:
+        for s in servers:
+            s.stop()
+        j.close()
+
+
 def test_batches_form_under_load():
     j = _job(1)
     s = rjob.EchoServer(j, 0, [0], max_batch=32, service_us=500.0)
@@ -90,7 +120,15 @@ def test_trace_ring_and_chrome_export(tmp_path):
         lg = rjob.LoadGen(c, 0, [b"z" * 32])
         lg.run(400, 32, 0.0, 0.0, False, 30.0)
         j.trace_record(0, 1, 1000, 2000, 0, 3, 4)
-        ev = tracing.collect(j)
+        # the echo replica appends a batch's trace event after posting its
+        # completions: the last batch's record may land just after run() returns
+        import time
+        deadline = time.monotonic() + 5.0
+        while True:
+            ev = tracing.collect(j)
+            if sum(e["n"] for e in ev if e["replica"] == 1) >= 400 or time.monotonic() > deadline:
+                break
+            time.sleep(0.01)
         assert any(e["replica"] == 1 and e["kind"] == "gpu" for e in ev)
         assert sum(e["n"] for e in ev if e["replica"] == 1) == 400
         tr = tracing.export_chrome_trace(j, str(tmp_path / "t.json"))
