@@ -51,7 +51,7 @@ def _aligned(t: torch.Tensor, n: int = 16) -> bool:
 # while a hipGraph is being captured (those calls use the cached choice, or the
 # on-device heuristic if the shape was never seen eagerly).
 # ---------------------------------------------------------------------------
-NUM_TILE_CFGS = 24   # gemm_core.h kTileBM/BN: 0..12 4-wave (GEMM and conv), 13..18 8-wave, 19..23 ping-pong (GEMM only)
+NUM_TILE_CFGS = 26   # gemm_core.h kTileBM/BN: 0..12 4-wave (GEMM and conv), 13..18 8-wave, 19..25 ping-pong (GEMM only)
 NUM_LN_TILE_CFGS = 19  # the deferred-LayerNorm epilogues run on tiles 0..18
 NUM_CONV_TILE_CFGS = 13
 FORCE_TILED = 99      # tile_cfg value that bypasses the skinny-M GEMM (M <= 64)

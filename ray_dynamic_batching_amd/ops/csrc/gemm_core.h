@@ -951,12 +951,15 @@ namespace rdb {
 // blocks per CU (<= 128 VGPRs): one block's epilogue (FFN-up's GELU: ~13k
 // VALU cycles per tile) runs beside the other block's MFMAs -- 3 % over 22 on
 // the FFN-up shape in the two-stream lab (profiles/gemm_lab_r3_gelu_epilogue.txt).
-constexpr int kNumTiles = 24;
-//                                 0    1    2    3    4    5    6    7    8    9   10   11   12 | 8-wave: 13   14   15   16   17   18 | pp: 19   20   21   22   23
-constexpr int kTileBM[kNumTiles] = {128, 64, 128, 64, 128, 192, 256, 128, 128, 64, 128, 256, 128, 256, 128, 256, 256, 128, 256, 256, 256, 128, 256, 256};
-constexpr int kTileBN[kNumTiles] = {128, 128, 64, 64, 192, 128, 128, 256, 144, 96, 96, 144, 48, 128, 256, 192, 144, 96, 96, 128, 144, 256, 256, 128};
-constexpr int kTileWGM[kNumTiles] = {2, 2, 2, 2, 2, 2, 2, 2, 4, 2, 2, 4, 4, 4, 2, 4, 8, 4, 8, 4, 8, 2, 4, 4};
-constexpr int kTileNW[kNumTiles] = {4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 8, 8, 8, 8, 8, 8, 8, 8, 8, 8, 8};
+// 24 / 25 = ping-pong 256x192 at BK = 32 with 3 / 4 stages (89 / 119 KiB): a
+// 4096 x 3072 GEMM (BERT FFN-up) is exactly 256 tiles = one per CU, where 23
+// leaves 1.5 blocks per CU, at 1/110 operand bytes per FLOP vs 1/85 for 256x128.
+constexpr int kNumTiles = 26;
+//                                 0    1    2    3    4    5    6    7    8    9   10   11   12 | 8-wave: 13   14   15   16   17   18 | pp: 19   20   21   22   23   24   25
+constexpr int kTileBM[kNumTiles] = {128, 64, 128, 64, 128, 192, 256, 128, 128, 64, 128, 256, 128, 256, 128, 256, 256, 128, 256, 256, 256, 128, 256, 256, 256, 256};
+constexpr int kTileBN[kNumTiles] = {128, 128, 64, 64, 192, 128, 128, 256, 144, 96, 96, 144, 48, 128, 256, 192, 144, 96, 96, 128, 144, 256, 256, 128, 192, 192};
+constexpr int kTileWGM[kNumTiles] = {2, 2, 2, 2, 2, 2, 2, 2, 4, 2, 2, 4, 4, 4, 2, 4, 8, 4, 8, 4, 8, 2, 4, 4, 4, 4};
+constexpr int kTileNW[kNumTiles] = {4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 8, 8, 8, 8, 8, 8, 8, 8, 8, 8, 8, 8, 8};
 
 inline int tile_blocks_per_cu(int cfg) {
   if (cfg == 23) return 2;
@@ -1063,6 +1066,12 @@ void launch_mfma_gemm_t(const P& ap, const T* W, int ldw, OutT* C, int ldc, cons
             return;
           case 23: launch_gemm_pp<T, OutT, 8, 256, 128, 2, 2, 3, 32, 4>(static_cast<const T*>(ap.A), ap.lda, W, ldw,
                                                                          C, ldc, bias, R, ldr, M, N, K, alpha, act, s);
+            return;
+          case 24: launch_gemm_pp<T, OutT, 8, 256, 192, 2, 2, 3, 32>(static_cast<const T*>(ap.A), ap.lda, W, ldw, C,
+                                                                      ldc, bias, R, ldr, M, N, K, alpha, act, s);
+            return;
+          case 25: launch_gemm_pp<T, OutT, 8, 256, 192, 2, 2, 4, 32>(static_cast<const T*>(ap.A), ap.lda, W, ldw, C,
+                                                                      ldc, bias, R, ldr, M, N, K, alpha, act, s);
             return;
           default: break;
         }
