@@ -359,8 +359,33 @@ __device__ __forceinline__ void staged_epilogue(char* smem, const f32x4 (&acc)[T
     }
     return;
   }
+  // Residual prefetch: this thread's phase-2 residual vectors are loaded BEFORE
+  // phase 1, so their memory latency runs under the LDS parking and the
+  // barrier instead of after it (at most 8 x 16 B per thread, beside the
+  // accumulators).  The barrier then waits for LDS traffic only.  Probe on
+  // MI355X (bench/gemm_probe.py --res): FFN-down 4096x768x3072 on the 256x128
+  // ping-pong tile 42.2 -> 40.9 us (40.1 without a residual); the 4-wave
+  // 128x96 o-proj got slower (11.6 -> 12.0 us), so 4-wave tiles keep the loop.
+  constexpr int NVEC = E::RC * E::NV;
+  constexpr int PER = (NVEC + NT - 1) / NT;
+#ifdef RDB_EPI_NO_RES_PREFETCH
+  constexpr bool PREF = false;
+#else
+  constexpr bool PREF = HAS_RES && PER <= 8 && NT >= 512;   // 8-wave tiles (4-wave o-proj: +0.4 us measured)
+#endif
 #pragma unroll 1
   for (int c = 0; c < BM / E::RC; ++c) {
+    u32x4 rpre[PREF ? PER : 1];
+    if constexpr (PREF) {
+#pragma unroll
+      for (int u = 0; u < PER; ++u) {
+        const int idx = tid + u * NT;
+        const int r = idx / E::NV, vcol = idx - r * E::NV;
+        const int m = m0 + c * E::RC + r, n = n0 + vcol * 8;
+        rpre[u] = u32x4{0u, 0u, 0u, 0u};
+        if (idx < NVEC && m < M && n < N) rpre[u] = *reinterpret_cast<const u32x4*>(R + (size_t)m * ldr + n);
+      }
+    }
     // phase 1: alpha * acc + bias -> LDS (f32)
 #pragma unroll
     for (int j = 0; j < TM; ++j) {
@@ -379,6 +404,35 @@ __device__ __forceinline__ void staged_epilogue(char* smem, const f32x4 (&acc)[T
           *reinterpret_cast<f32x4*>(smem + rt * E::ROWB + nt * 4) = v;
         }
       }
+    }
+    if constexpr (PREF) {
+      // LDS writes done and visible; the prefetched residual loads stay in flight
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0), vmcnt / expcnt untouched
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int u = 0; u < PER; ++u) {
+        const int idx = tid + u * NT;
+        const int r = idx / E::NV, vcol = idx - r * E::NV;
+        const int m = m0 + c * E::RC + r, n = n0 + vcol * 8;
+        if (idx < NVEC && m < M && n < N) {
+          const f32x4 a = *reinterpret_cast<const f32x4*>(smem + r * E::ROWB + vcol * 32);
+          const f32x4 b = *reinterpret_cast<const f32x4*>(smem + r * E::ROWB + vcol * 32 + 16);
+          float x[8] = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+          const T* e = reinterpret_cast<const T*>(&rpre[u]);
+#pragma unroll
+          for (int q = 0; q < 8; ++q) x[q] += (float)e[q];
+          OutT o[8];
+#pragma unroll
+          for (int q = 0; q < 8; ++q) o[q] = (OutT)actf(x[q]);
+          *reinterpret_cast<u32x4*>(C + (size_t)m * ldc + n) = *reinterpret_cast<const u32x4*>(o);
+        }
+      }
+      __syncthreads();
+      continue;
     }
     __syncthreads();
     // phase 2: row-major, 8 columns per lane, 16-B residual loads and stores of
