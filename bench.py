@@ -6,6 +6,14 @@ dynamic batching <= 32, one replica per MI355X (BASELINE.json metric).
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
+Both forms run N ranks: without a launcher (no WORLD_SIZE in the environment)
+and N > 1, this process touches no GPU and starts the N ranks itself as ONE
+child ``torch.distributed.run`` (127.0.0.1 rendezvous on a free port), whose
+rank 0 prints the JSON line; the parent exits with the child's code.  This is
+the fork's one-invocation fan-out (``ray.init(num_gpus=N)`` + one GPUWorker
+per GPU, 293-project/src/scheduler.py:671-693).  Under a launcher,
+``--gpus`` must equal WORLD_SIZE.
+
 Every rank is one replica process pinned to its GPU (LOCAL_RANK).  Rank 0
 creates the shared-memory job; every rank runs an ingress: a native
 closed-loop load generator whose requests go through the power-of-two-choices
@@ -34,7 +42,8 @@ METRIC = "req/s (whole node) vs p99 latency, BERT-base dyn-batch<=32, at 1/2/4/8
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one replica per GPU); default: WORLD_SIZE under a launcher, else 1")
     ap.add_argument("--steps", type=int, default=300)
     ap.add_argument("--warmup", type=int, default=30)
     ap.add_argument("--max-batch", type=int, default=32)
@@ -95,8 +104,40 @@ class _EchoRunner:
         return ""
 
 
+def _free_port() -> int:
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def _fan_out(n: int) -> int:
+    """Start the N ranks as one child launcher and relay its output.  Runs
+    before anything here touches the GPU (the parent never initialises HIP: it
+    only waits), so no process that owns a GPU context is ever replaced."""
+    import subprocess
+
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("OMP_NUM_THREADS", "1")
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    here = os.path.dirname(os.path.abspath(__file__))
+    env["PYTHONPATH"] = here + (os.pathsep + env["PYTHONPATH"] if env.get("PYTHONPATH") else "")
+    return subprocess.run(cmd, env=env).returncode
+
+
 def main():
     args = parse()
+    launched = "WORLD_SIZE" in os.environ
+    if not launched and (args.gpus or 1) > 1:
+        sys.exit(_fan_out(args.gpus))
+    if launched and args.gpus is not None and args.gpus != int(os.environ["WORLD_SIZE"]):
+        print(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={os.environ['WORLD_SIZE']} ranks",
+              file=sys.stderr)
+        sys.exit(2)
     import torch
     import torch.distributed as dist
 

@@ -288,10 +288,7 @@ class ChannelWriter:
         self.rings = {d: TensorRing.attach(desc) for d, desc in (rings or {}).items()}
         self.seq = 0
 
-    def write(self, kind: str, value: Any = None, stop: Optional[threading.Event] = None,
-              timeout_s: float = 60.0) -> None:
-        seq = self.seq
-        self.seq += 1                     # every message takes a slot number (reader counts the same way)
+    def _encode(self, kind: str, value: Any, seq: int) -> bytes:
         if self.rings and kind == "val":
             try:
                 value = encode_tensors(value, self.rings, seq)
@@ -304,15 +301,42 @@ class ChannelWriter:
             from . import RayError
 
             data = _pack("err", RayError(f"{type(value).__name__}: {str(value)[:256]}"))
+        return data
+
+    def _too_big(self, n: int) -> ValueError:
+        return ValueError(f"value of {n} bytes exceeds the channel buffer "
+                          "(compile with a larger _buffer_size_bytes)")
+
+    def pack(self, kind: str, value: Any = None) -> bytes:
+        """The message bytes of (kind, value), size-checked, WITHOUT sending it
+        (raises ValueError if it can never fit).  For ring-less edges only: a
+        tensor edge encodes into the slot of the message actually sent."""
+        assert not self.rings, "pack() is for edges without tensor rings"
+        data = self._encode(kind, value, self.seq)
+        if len(data) > self.client_max:
+            raise self._too_big(len(data))
+        return data
+
+    def write(self, kind: str, value: Any = None, stop: Optional[threading.Event] = None,
+              timeout_s: float = 60.0, data: Optional[bytes] = None) -> None:
+        """Send one message.  The slot number (which the reader counts the same
+        way, one per message it pops) is taken only once the message is in the
+        ring: a value that is too large, or a ring that stays full, raises and
+        leaves the writer in step with its reader."""
+        seq = self.seq
+        if data is None:
+            data = self._encode(kind, value, seq)
+        if len(data) > self.client_max:
+            raise self._too_big(len(data))
         t_end = time.monotonic() + timeout_s
         delay = 0.0
         while True:
             rid = self.client.submit(self.queue, data)
             if rid > 0:
+                self.seq = seq + 1
                 return
             if rid == -3:
-                raise ValueError(f"value of {len(data)} bytes exceeds the channel buffer "
-                                 "(compile with a larger _buffer_size_bytes)")
+                raise self._too_big(len(data))
             if (stop is not None and stop.is_set()) or time.monotonic() > t_end:
                 raise TimeoutError("channel full: the reader is not consuming")
             time.sleep(delay)                      # ring full: back off

@@ -383,6 +383,7 @@ class ChannelCompiledDAG:
         self._cv = threading.Condition()
         self._stop = threading.Event()
         self._closed = False
+        self._broken: Optional[str] = None
         self._reader = threading.Thread(target=self._collect, daemon=True, name="rdb-dag-out")
         self._reader.start()
 
@@ -398,17 +399,36 @@ class ChannelCompiledDAG:
     def execute(self, *args, **kwargs):
         if self._closed:
             raise RayError("this compiled DAG was torn down")
-        self._slots.acquire()
-        futs = [Future() for _ in self._readers]
-        with self._cv:
-            self._pending.append(futs)
-            self._cv.notify_all()
+        if self._broken is not None:
+            raise RayError(f"this compiled DAG is broken ({self._broken}); tear it down")
+        # Every input is pickled and size-checked BEFORE an in-flight slot is
+        # taken and the execution's futures are queued: an oversized input
+        # raises here with no channel written, so channels and futures stay
+        # paired one message per execution.
+        data = []
         for w, src in self._writers:
             try:
                 v = ("val", self._input_value(src, args, kwargs))
             except Exception as e:  # noqa: BLE001
                 v = ("err", RayError(f"DAG input has no {getattr(src, 'key', '?')!r}: {e}"))
-            w.write(v[0], v[1], self._stop)
+            data.append(w.pack(*v))
+        self._slots.acquire()
+        futs = [Future() for _ in self._readers]
+        with self._cv:
+            self._pending.append(futs)
+            self._cv.notify_all()
+        for w_src, d in zip(self._writers, data):
+            try:
+                w_src[0].write("", None, self._stop, data=d)
+            except BaseException as e:
+                # A channel stayed full (or the DAG is stopping): that channel has
+                # no message for this execution, so later executions would pair
+                # values of different calls.  The DAG is unusable from here on.
+                self._broken = f"input channel write failed: {e}"
+                for f in futs:
+                    if not f.done():
+                        f.set_exception(RayError(self._broken))
+                raise
         refs = [ObjectRef(f) for f in futs]
         return refs if self.multi else refs[0]
 
@@ -429,6 +449,8 @@ class ChannelCompiledDAG:
             with self._cv:
                 self._pending.popleft()
             for f, (kind, val) in zip(futs, msgs):
+                if f.done():        # failed at submission (broken DAG)
+                    continue
                 if kind == "val":
                     f.set_result(val)
                 elif kind == "err":

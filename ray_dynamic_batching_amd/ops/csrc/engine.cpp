@@ -73,15 +73,21 @@ struct Session {
   // batch) and drives duty-cycle charging / backfill; est_wall_ns is the EMA of
   // the event-timed span under whatever overlap the compute streams had and
   // drives stale dropping (when a request would actually complete)
+  // est_prov: the solo estimate is only a seed (timed while other sessions
+  // were running, or from a first batch that overlapped another): the first
+  // batch that truly runs alone REPLACES it instead of being blended in
   std::unique_ptr<std::atomic<double>[]> est_ns, est_wall_ns;
+  std::unique_ptr<std::atomic<bool>[]> est_prov;
   size_t n_est = 0;
   void reset_estimates(size_t n) {
     n_est = n;
     est_ns.reset(new std::atomic<double>[n]);
     est_wall_ns.reset(new std::atomic<double>[n]);
+    est_prov.reset(new std::atomic<bool>[n]);
     for (size_t i = 0; i < n; ++i) {
       est_ns[i].store(0.0, std::memory_order_relaxed);
       est_wall_ns[i].store(0.0, std::memory_order_relaxed);
+      est_prov[i].store(true, std::memory_order_relaxed);
     }
   }
   double est(int bi) const { return est_ns[bi].load(std::memory_order_relaxed); }
@@ -309,11 +315,11 @@ class Engine {
   // the graphs, inputs and weights.  Requests still queued stay in the ring.
   bool retire_session(int sid, double timeout_s) {
     Session& s = sess(sid);
-    s.active.store(false, std::memory_order_seq_cst);
+    const bool was_active = s.active.exchange(false, std::memory_order_seq_cst);
     const int64_t end = now_ns() + (int64_t)(timeout_s * 1e9);
     while (s.inflight.load(std::memory_order_seq_cst) != 0) {
       if (now_ns() > end) {
-        s.active.store(true);   // could not drain: keep serving
+        s.active.store(was_active);   // could not drain: back to how it was (serving only if it was)
         return false;
       }
       std::this_thread::sleep_for(std::chrono::microseconds(100));
@@ -335,10 +341,16 @@ class Engine {
     s.graphs.at(bucket_idx).at(slot) = reinterpret_cast<hipGraphExec_t>(graph_exec);
     s.out_dev.at(bucket_idx).at(slot) = out_dev;
   }
-  void set_latency_estimate(int sid, int bucket_idx, double ms) {
+  void set_latency_estimate(int sid, int bucket_idx, double ms, bool provisional) {
     Session& s = sess(sid);
     if (bucket_idx < 0 || (size_t)bucket_idx >= s.n_est) throw std::out_of_range("bucket index");
     s.est_ns[bucket_idx].store(ms * 1e6, std::memory_order_relaxed);
+    s.est_prov[bucket_idx].store(provisional, std::memory_order_relaxed);
+  }
+  bool latency_estimate_provisional(int sid, int bucket_idx) {
+    Session& s = sess(sid);
+    if (bucket_idx < 0 || (size_t)bucket_idx >= s.n_est) throw std::out_of_range("bucket index");
+    return s.est_prov[bucket_idx].load(std::memory_order_relaxed);
   }
   // (solo, wall) service estimates of one bucket in ms
   std::pair<double, double> latency_estimate(int sid, int bucket_idx) {
@@ -754,8 +766,15 @@ class Engine {
             const bool solo = f.solo && launch_seq_.load(std::memory_order_acquire) == f.seq;
             std::atomic<double>& e = s.est_ns[f.bucket_idx];
             const double e0 = e.load(std::memory_order_relaxed);
-            if (e0 == 0.0) e.store(v, std::memory_order_relaxed);
-            else if (solo) e.store(0.9 * e0 + 0.1 * v, std::memory_order_relaxed);
+            std::atomic<bool>& prov = s.est_prov[f.bucket_idx];
+            if (solo && prov.load(std::memory_order_relaxed)) {
+              e.store(v, std::memory_order_relaxed);          // first solo batch replaces a seed
+              prov.store(false, std::memory_order_relaxed);
+            } else if (e0 == 0.0) {
+              e.store(v, std::memory_order_relaxed);          // overlapped: a seed, still provisional
+            } else if (solo) {
+              e.store(0.9 * e0 + 0.1 * v, std::memory_order_relaxed);
+            }
           }
           const char* out = reinterpret_cast<const char*>(s.host_out[f.slot]);
           const int64_t t_done = now_ns();
@@ -848,7 +867,9 @@ void register_engine(py::module_& m) {
            py::arg("drop_stale") = false)
       .def("set_input", &Engine::set_input)
       .def("set_graph", &Engine::set_graph)
-      .def("set_latency_estimate", &Engine::set_latency_estimate)
+      .def("set_latency_estimate", &Engine::set_latency_estimate, py::arg("sid"), py::arg("bucket_idx"),
+           py::arg("ms"), py::arg("provisional") = false)
+      .def("latency_estimate_provisional", &Engine::latency_estimate_provisional)
       .def("latency_estimate", &Engine::latency_estimate)
       .def("set_duty_share", &Engine::set_duty_share)
       .def("set_duty_cycle", &Engine::set_duty_cycle)

@@ -87,7 +87,8 @@ class DutyCycleExecutor(threading.Thread):
                 self.unloads += 1
                 if cons is not None:
                     # queued requests follow the model to a GPU that serves it
-                    self.rerouted += self.sched._reroute_queue(self.sched.queue_id(self.gpu, m), m, cons)
+                    moved = self.sched._reroute_queue(self.sched.queue_id(self.gpu, m), m, cons)
+                    self.rerouted += max(0, moved)
         for m in new_models:
             if m not in self.models:          # load
                 self.models[m] = self.sched.model_factories[m]()
@@ -232,6 +233,7 @@ class EngineExecutor:
         self.loads = 0
         self.unloads = 0
         self.rerouted = 0
+        self.failed_on_unload = 0
         with torch.cuda.device(device):
             self.runner = EngineRunner(sched.job_name, gpu, [], pipeline_depth=2, device=device,
                                        policy=EngineRunner.POLICY_DUTY_CYCLE, compute_streams=compute_streams)
@@ -287,7 +289,11 @@ class EngineExecutor:
         del self.index[m]
         self.unloads += 1
         # requests routed here after the drain: hand them to a GPU serving m
-        self.rerouted += self.sched._reroute_queue(self.sched.queue_id(self.gpu, m), m)
+        moved = self.sched._reroute_queue(self.sched.queue_id(self.gpu, m), m)
+        if moved >= 0:
+            self.rerouted += moved
+        else:
+            self.failed_on_unload += -moved
         return True
 
     def prepare(self, node: Optional[Node]) -> None:
@@ -325,6 +331,7 @@ class EngineExecutor:
         st = dict(self.runner.stats())
         st.update(resident_models=sorted(self.index), resident_bytes=self.resident_bytes(),
                   loads=self.loads, unloads=self.unloads, rerouted=self.rerouted,
+                  failed_on_unload=self.failed_on_unload,
                   capture_s=dict(self.capture_s))
         return st
 
@@ -359,6 +366,7 @@ class SLOScheduler:
         self.hbm_budget_bytes = int((hbm_budget_gb * 1e9) if hbm_budget_gb is not None else DEFAULT_HBM_BYTES)
         self._footprint_hint = {m: int(v * 1e9) for m, v in (model_footprint_gb or {}).items()}
         self.rejected_plans: List[Dict[str, Any]] = []
+        self.swapped_first: List[Any] = []      # (gpu, [models]) retired before their arrivals loaded
         self.profiles = profiles
         self.slos = dict(slos_ms)
         self.model_factories = model_factories
@@ -544,6 +552,25 @@ class SLOScheduler:
                 out[g] = dict(models=need, total=sum(need.values()), budget=self.hbm_budget_bytes)
         return out
 
+    def swap_first(self, placed: List[Optional[Node]]) -> List[int]:
+        """GPUs whose plan change would hold the leaving AND the arriving models
+        at once above the HBM budget (arrivals are loaded before departures are
+        unloaded, so the transition peaks at current + arriving).  _apply
+        retires their leaving models first on those GPUs."""
+        out = []
+        for g, node in enumerate(placed):
+            if not hasattr(self.executors[g], "unload"):
+                continue        # the Python executor already unloads before it loads
+            cur = set(getattr(self.executors[g], "index", {}) or {})
+            planned = set(node.models()) if node else set()
+            arriving = planned - cur
+            if not arriving or not (cur - planned):
+                continue
+            peak = sum(self.footprint_estimate(m) for m in cur | arriving)
+            if peak > self.hbm_budget_bytes:
+                out.append(g)
+        return out
+
     def _reroute_queue(self, q: int, m: str, consumer: Any = None) -> int:
         """Move the requests left in queue ``q`` (model ``m`` just left that GPU)
         to the least-loaded GPU queue that serves ``m`` (native
@@ -551,10 +578,19 @@ class SLOScheduler:
         client); held in the ring if no GPU serves ``m`` right now."""
         targets = [self.queue_id(g, m) for g in range(self.num_gpus)
                    if self.queue_id(g, m) != q and self.slots[g] is not None and m in self.slots[g].models()]
-        if not targets:
-            return 0
-        to = min(targets, key=self.job.queue_depth)
         cons = consumer if consumer is not None else rjob.Consumer(self.job, [q])
+        if not targets:
+            # no GPU serves m any more (it left the plan): fail the leftovers
+            # fast instead of leaving their clients to time out on a retired ring
+            failed = 0
+            while True:
+                got = cons.pop(256, 0)
+                if not got:
+                    return 0 if not failed else -failed
+                for rid, queue, client, _kind, t_sub, _dl, _payload in got:
+                    cons.complete(client, rid, queue, 2, t_sub, b"model unloaded: no GPU serves it")  # ST_ERROR
+                    failed += 1
+        to = min(targets, key=self.job.queue_depth)
         return int(cons.forward(to))
 
     def replan(self, update: Dict[str, float]) -> Plan:
@@ -604,6 +640,21 @@ class SLOScheduler:
             return plan
 
     def _apply(self, placed: List[Optional[Node]]) -> None:
+        # phase 0: on a GPU where old + new models would not fit the HBM budget
+        # together, the leaving models are taken off the router, drained and
+        # unloaded BEFORE the arrivals load (their requests are forwarded to
+        # another GPU serving them, or failed fast if none does)
+        for g in self.swap_first(placed):
+            ex = self.executors[g]
+            planned = set(placed[g].models()) if placed[g] else set()
+            leaving = [m for m in list(getattr(ex, "index", {})) if m not in planned]
+            for m in leaving:
+                self.job.configure_queue(self.queue_id(g, m), g, self.model_id(m), 0, float(self.slos[m]), False)
+            for m in leaving:
+                if not ex.unload(m):
+                    logger.warning("GPU %d: %s did not drain before the swap; the transition may exceed "
+                                   "the HBM budget", g, m)
+            self.swapped_first.append((g, leaving))
         # phase 1: models arriving on a GPU are loaded + captured (inactive)
         # while every session keeps serving; only then does the router see their
         # queues, so no request waits for a capture

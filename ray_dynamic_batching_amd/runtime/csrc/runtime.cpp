@@ -359,9 +359,11 @@ class Client {
       return -1;   // every candidate at max_ongoing
     }
     // Two random distinct candidates; fall back to a full scan when both are full.
-    const uint32_t a = cand_[rng_.next() % n];
-    uint32_t b = cand_[rng_.next() % n];
-    if (b == a) b = cand_[(std::find(cand_.begin(), cand_.end(), a) - cand_.begin() + 1) % n];
+    // (the second index is uniform over the other n - 1, as random.sample in
+    // the reference's pow_2_scheduler.py:346-495)
+    const size_t ia = rng_.next() % n;
+    const size_t ib = (ia + 1 + rng_.next() % (n - 1)) % n;
+    const uint32_t a = cand_[ia], b = cand_[ib];
     const int64_t da = depth(a), db = depth(b);
     const uint32_t best = da <= db ? a : b;
     const int64_t dbest = std::min(da, db);

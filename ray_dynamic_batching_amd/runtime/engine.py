@@ -200,7 +200,9 @@ class EngineRunner:
                 for _ in range(3):
                     g.replay()
             side.synchronize()
-            self.engine.set_latency_estimate(s.sid, bi, (time.perf_counter() - t) / 3 * 1e3)
+            # timed while the engine may be serving other sessions (live add):
+            # only a seed -- the first batch that runs alone replaces it
+            self.engine.set_latency_estimate(s.sid, bi, (time.perf_counter() - t) / 3 * 1e3, live)
         self.check_model_errors(m)
 
     def check_model_errors(self, m=None) -> None:

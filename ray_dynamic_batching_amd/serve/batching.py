@@ -84,12 +84,24 @@ class _BatchQueue:
         self._hook = batch_started_hook
         self.batches_processed = 0
         self.last_batch_sizes: List[int] = []
-        self._task = asyncio.get_running_loop().create_task(self._loop())
+        self.loop = asyncio.get_running_loop()
+        # The batching task runs only while requests are queued: it is started
+        # by put() and returns once the queue is drained, so an idle queue (or
+        # one whose event loop is closed without cancelling its tasks) leaves no
+        # pending task behind -- the reference cancels its long-lived task from
+        # __del__ (python/ray/serve/batching.py:323-333), which a closed loop
+        # can no longer run.
+        self._task: Optional[asyncio.Task] = None
         self.current_iteration_start: Optional[float] = None
 
     def put(self, req: _SingleRequest) -> None:
         self.queue.put_nowait(req)
         self._arrival.set()
+        if self._task is None or self._task.done():
+            self._task = self.loop.create_task(self._loop())
+
+    def is_alive(self) -> bool:
+        return self._task is not None and not self._task.done()
 
     async def wait_for_batch(self) -> List[_SingleRequest]:
         """Block for the first item, then keep adding until full or until
@@ -116,7 +128,7 @@ class _BatchQueue:
         return batch
 
     async def _loop(self) -> None:
-        while True:
+        while not self.queue.empty():
             batch = await self.wait_for_batch()
             # drop requests whose caller already gave up (cancelled)
             batch = [r for r in batch if not r.future.done()]
@@ -185,7 +197,8 @@ class _BatchQueue:
                 q.put_nowait(("error", e))
 
     def shutdown(self) -> None:
-        self._task.cancel()
+        if self._task is not None and not self._task.done() and not self.loop.is_closed():
+            self._task.cancel()
 
 
 class _LazyBatchQueue:
@@ -203,11 +216,22 @@ class _LazyBatchQueue:
         """One queue per (event loop, bound instance): replicas never share a batch."""
         key = (id(asyncio.get_running_loop()), id(owner))
         q = self._queues.get(key)
+        if q is not None and q.loop is not asyncio.get_running_loop():
+            q = None   # a closed loop's id was reused
         if q is None:
+            self._prune()
             q = _BatchQueue(self.max_batch_size, self.batch_wait_timeout_s, self._fn, self._gen)
             self._warn_if_ongoing_too_small()
             self._queues[key] = q
         return q
+
+    def _prune(self) -> None:
+        """Forget the queues of closed event loops (their pending items can never run)."""
+        for k in [k for k, q in self._queues.items() if q.loop.is_closed()]:
+            q = self._queues.pop(k)
+            while not q.queue.empty():
+                r = q.queue.get_nowait()
+                r.future.cancel() if not r.future.done() and not q.loop.is_closed() else None
 
     def set_max_batch_size(self, v: int) -> None:
         _validate_max_batch_size(v)
@@ -241,7 +265,7 @@ class _LazyBatchQueue:
         return [q.current_iteration_start for q in self._queues.values()]
 
     def _is_batching_task_alive(self) -> bool:
-        return any(not q._task.done() for q in self._queues.values())
+        return any(q.is_alive() for q in self._queues.values())
 
 
 def batch(_func: Optional[Callable] = None, /, max_batch_size: int = 10, batch_wait_timeout_s: float = 0.0):

@@ -53,3 +53,27 @@ def test_bench_resolves_shipped_tile_table():
     assert bench._tile_table(argparse.Namespace(**dict(vars(a), layers=2))) == ""
     assert bench._tile_table(argparse.Namespace(**dict(vars(a), tile_table="none"))) == ""
     assert bench._tile_table(argparse.Namespace(**dict(vars(a), backend="torch"))) == ""
+
+
+@pytest.mark.parametrize("n", [2, 4, 8])
+def test_bench_gpus_flag_launches_ranks_itself(n):
+    """`python bench.py --gpus N` with no launcher (the driver's command shape)
+    starts N ranks itself: n_gpus == N and every replica served requests."""
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(n), "--steps", "20", "--warmup", "2",
+           "--backend", "echo", "--echo-service-us", "800"]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=ROOT, env=env)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == n and d["config"]["parallelism"] == f"dp{n}"
+    assert len(d["per_replica_requests"]) == n and min(d["per_replica_requests"]) > 0
+    assert d["errors"] == 0 and d["completed"] == 20 * 32 * n
+
+
+def test_bench_gpus_must_match_launcher_world_size():
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4", "--steps", "2", "--backend", "echo"]
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=120, cwd=ROOT,
+                         env=dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0"))
+    assert out.returncode == 2 and "WORLD_SIZE=2" in out.stderr

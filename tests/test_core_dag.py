@@ -224,3 +224,51 @@ def test_tensor_ring_slot_reuse_protocol():
         assert decode_tensors(enc, r, seq=7)[0].tolist() == [-1.0] * 4
     finally:
         release_rings(job)
+
+
+class BlobStage:
+    def make(self, n):
+        import torch
+
+        if n < 0:
+            return b"x" * (-n)                 # a large NON-tensor value on a tensor edge
+        return {"x": torch.arange(n, dtype=torch.float64)}
+
+    def total(self, d):
+        return float(d["x"].sum())
+
+    def echo(self, x):
+        return len(x)
+
+
+def test_oversized_input_raises_before_queueing_and_next_execution_is_right(rt):
+    """An input larger than the channel buffer raises from execute() with no
+    channel written and no future queued; the next execution gets ITS result
+    (advisor finding: futures / slots used to stay queued on a failed write)."""
+    A = ray.remote(num_gpus=1)(BlobStage)
+    a = A.remote()
+    with InputNode() as inp:
+        out = a.echo.bind(inp)
+    cd = out.experimental_compile(_max_inflight_executions=2, _buffer_size_bytes=4096)
+    with pytest.raises(ValueError, match="exceeds"):
+        cd.execute(b"y" * 100_000)
+    for i in range(5):                          # more executions than in-flight slots: none leaked
+        assert ray.get(cd.execute(b"z" * (10 + i)), timeout=30) == 10 + i
+    cd.teardown(timeout=5)
+
+
+def test_oversized_plain_value_on_tensor_edge_keeps_slots_in_step(rt):
+    """A non-tensor value too large for a tensor edge's message becomes an error
+    for that execution only; the writer's slot numbering stays in step with the
+    reader, so the next tensor value is decoded from the right ring slot."""
+    A = ray.remote(num_gpus=1)(BlobStage)
+    a, b = A.remote(), A.remote()
+    with InputNode() as inp:
+        out = b.total.bind(a.make.bind(inp).with_tensor_transport())
+    cd = out.experimental_compile(_max_inflight_executions=1, _buffer_size_bytes=32 * 1024)
+    assert ray.get(cd.execute(100), timeout=30) == float(sum(range(100)))
+    with pytest.raises(Exception, match="exceeds|buffer"):
+        ray.get(cd.execute(-200_000), timeout=30)
+    for n in (10, 300, 77):
+        assert ray.get(cd.execute(n), timeout=30) == float(sum(range(n)))
+    cd.teardown(timeout=5)

@@ -52,6 +52,19 @@ def test_equal_depths_spread_over_all_candidates(job):
     assert min(got.values()) > 300          # roughly uniform (500 expected each)
 
 
+def test_second_sample_uniform_over_the_other_candidates(job):
+    """The pair is two DISTINCT uniform samples (reference random.sample): when
+    the deep queue 0 is drawn first, its partner is uniform over queues 1-5 --
+    no neighbour of queue 0 gets the collision mass."""
+    c = rjob.Client(job, 1, seed=5)
+    job._test_set_queue_depth(0, 3)
+    n = 30000
+    got = _choices(c, 0, n=n)
+    assert 0 not in got
+    expect = n / 5                              # 1/6 + 1/6 * 1/5 per shallow queue
+    assert max(abs(got[q] - expect) for q in range(1, 6)) < 0.05 * expect, got
+
+
 def test_full_scan_fallback_when_sampled_pair_is_full(job):
     c = rjob.Client(job, 1, seed=11)
     for q in range(6):

@@ -227,3 +227,87 @@ def test_consumer_forward_keeps_client_and_request_id():
         assert j.queue_stats(0)["submitted"] == 0 and j.queue_stats(1)["submitted"] == 5
     finally:
         j.close()
+
+
+class _RecordingExecutor:
+    """Stands in for EngineExecutor: records load / unload order."""
+
+    def __init__(self, log, g, resident):
+        self.log, self.g, self.index = log, g, {m: i for i, m in enumerate(resident)}
+
+    def unload(self, m, drain_timeout_s=10.0):
+        self.log.append(("unload", self.g, m))
+        self.index.pop(m, None)
+        return True
+
+    def prepare(self, node):
+        for m in (node.models() if node else []):
+            if m not in self.index:
+                self.log.append(("load", self.g, m))
+                self.index[m] = len(self.index)
+
+    def update(self, node):
+        planned = set(node.models()) if node else set()
+        self.prepare(node)
+        for m in list(self.index):
+            if m not in planned:
+                self.unload(m)
+
+    def shutdown(self):
+        pass
+
+
+def test_same_gpu_swap_over_budget_unloads_before_loading():
+    """Swapping a (0.6 GB) for b (0.6 GB) on a 1 GB GPU fits each plan, but not
+    both models at once: the leaving model is retired BEFORE the arrival is
+    loaded (advisor finding: prepare() used to load first -> transient OOM).
+    A swap that fits the budget keeps the serve-while-loading order."""
+    s = make_sched(hbm_budget_gb=1.0, model_footprint_gb={"a": 0.6, "b": 0.6})
+    real = s.executors
+    try:
+        log = []
+        s.executors = [_RecordingExecutor(log, 0, ["a"]), _RecordingExecutor(log, 1, [])]
+        s.slots = [Node([(Session("a", 200.0, 10.0, 4), 0.5)], 20.0), None]
+        assert s.restore_plan(_plan_with(s, {"b": 0}))
+        assert log.index(("unload", 0, "a")) < log.index(("load", 0, "b")), log
+        assert s.swapped_first == [(0, ["a"])]
+        # with room for both, the arrival loads first (no serving gap)
+        s2 = make_sched(hbm_budget_gb=2.0, model_footprint_gb={"a": 0.6, "b": 0.6})
+        try:
+            log2 = []
+            real2 = s2.executors
+            s2.executors = [_RecordingExecutor(log2, 0, ["a"]), _RecordingExecutor(log2, 1, [])]
+            s2.slots = [Node([(Session("a", 200.0, 10.0, 4), 0.5)], 20.0), None]
+            assert s2.restore_plan(_plan_with(s2, {"b": 0}))
+            assert log2.index(("load", 0, "b")) < log2.index(("unload", 0, "a")), log2
+            assert s2.swapped_first == []
+        finally:
+            s2.executors = real2
+            s2.shutdown()
+    finally:
+        s.executors = real
+        s.shutdown()
+
+
+def test_unload_with_no_other_server_fails_leftovers_fast():
+    """Requests still queued for a model that leaves the plan entirely are
+    completed with an error status instead of waiting on a retired ring."""
+    s = make_sched()
+    try:
+        assert s.restore_plan(_plan_with(s, {"a": 0, "b": 1}))
+        s.slots = [None, s.slots[1]]                      # 'a' served nowhere now
+        q = s.queue_id(0, "a")
+        s.job.configure_queue(q, 0, s.model_id("a"), 0, 200.0, True)
+        from ray_dynamic_batching_amd.runtime import job as rjob
+
+        c = rjob.Client(s.job)
+        rids = [c.submit(q, b"\0" * 128) for _ in range(5)]
+        assert s._reroute_queue(q, "a") == -5
+        got = {}
+        deadline = time.time() + 10
+        while len(got) < 5 and time.time() < deadline:
+            for comp in c.poll(64, 0.2):
+                got[comp[0]] = comp[1]
+        assert sorted(got) == sorted(rids) and set(got.values()) == {2}
+    finally:
+        s.shutdown()

@@ -185,3 +185,26 @@ def test_cancelled_caller_is_skipped():
         return await a
     assert run(main()) == "a"
     assert "b" not in seen
+
+
+def test_idle_queue_leaves_no_pending_task_and_dead_loops_are_pruned():
+    """The batching task exists only while requests are queued, and queues of
+    closed event loops are dropped (reference: _BatchQueue.__del__ cancels its
+    task, python/ray/serve/batching.py:323-333)."""
+    @serve.batch(max_batch_size=4, batch_wait_timeout_s=0.01)
+    async def f(xs):
+        return xs
+
+    lazy = f._rdb_batch_queue
+    for _ in range(3):
+        loop = asyncio.new_event_loop()
+        async def main():
+            return await asyncio.gather(*[f(i) for i in range(6)])
+        assert loop.run_until_complete(main()) == list(range(6))
+        assert not f._is_batching_task_alive()
+        assert not [t for t in asyncio.all_tasks(loop) if not t.done()]
+        loop.close()
+    loop = asyncio.new_event_loop()
+    assert loop.run_until_complete(f(7)) == 7
+    assert len(lazy._queues) == 1
+    loop.close()

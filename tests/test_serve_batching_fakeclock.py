@@ -34,7 +34,8 @@ def run(coro_fn):
         pending = [t for t in asyncio.all_tasks(loop) if not t.done()]
         for t in pending:
             t.cancel()
-        loop.run_until_complete(asyncio.gather(*pending, return_exceptions=True))
+        if pending:
+            loop.run_until_complete(asyncio.gather(*pending, return_exceptions=True))
         loop.close()
 
 
