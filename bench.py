@@ -54,6 +54,9 @@ def parse():
     ap.add_argument("--backend", default="hip", choices=["hip", "torch", "echo"],
                     help="echo = CPU rehearsal of the multi-rank path (native fake replicas, gloo)")
     ap.add_argument("--echo-service-us", type=float, default=1400.0, help="echo backend: batch service time")
+    ap.add_argument("--batch-policy", default="timeout", choices=["timeout", "idle"],
+                    help="timeout: @serve.batch semantics (full or max-wait after the first request); idle: also "
+                         "dispatch a partial batch as soon as a compute stream is idle")
     ap.add_argument("--pipeline-depth", type=int, default=4)
     ap.add_argument("--compute-streams", type=int, default=2, help="batches executing concurrently per GPU")
     ap.add_argument("--layers", type=int, default=12)
@@ -203,7 +206,7 @@ def main():
         model = BertForSequenceClassification(cfg, device="cuda", backend=args.backend)
         spec = SessionSpec(model=model, queue=rank, max_batch=args.max_batch, max_wait_s=args.max_wait_ms / 1e3)
         runner = EngineRunner(name, rank, [spec], pipeline_depth=args.pipeline_depth,
-                              compute_streams=args.compute_streams).build()
+                              compute_streams=args.compute_streams, batch_policy=args.batch_policy).build()
     runner.start()
     if not echo and getattr(runner, "tuning_changes", None):
         print(json.dumps({"rank": rank, "in_context_tile_changes": {str(k[2:5]): v for k, v in runner.tuning_changes.items()}}),
@@ -314,6 +317,7 @@ def main():
                        "global_batch": args.max_batch * n, "seq_len": args.seq,
                        "parallelism": f"dp{n}", "max_batch": args.max_batch,
                        "batch_wait_timeout_ms": args.max_wait_ms, "backend": args.backend,
+                       "batch_policy": args.batch_policy,
                        "load": (f"closed-loop x{args.concurrency}/GPU" if args.rate <= 0 else f"poisson {args.rate}/s/GPU"),
                        "tile_table": os.path.basename(os.environ.get("RDB_TUNE_FILE", "")) or "tuned at start-up"},
             "p50_ms": round(lat["p50_ms"], 3),
@@ -328,6 +332,9 @@ def main():
             "per_replica_requests": [r["batch_items"] for r in rep],
             "ingress": f"{args.ingress} x{G} thread(s)",
         }
+        if os.environ.get("RDB_ABLATE"):
+            line["metric"] = f"ABLATION (skips {os.environ['RDB_ABLATE']}: wrong outputs, not a measurement): " + METRIC
+            line["vs_baseline"] = None
         if args.rehearse_one_gpu:
             line["metric"] = "REHEARSAL (all ranks on one GPU, gloo): " + METRIC
             line["vs_baseline"] = None

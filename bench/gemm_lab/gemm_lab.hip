@@ -180,6 +180,7 @@ int main(int argc, char** argv) {
     for (auto& v : vs) {
       if (!only.empty() && v.name.find(only) == std::string::npos) continue;
       CK(hipMemset(C, 0, (size_t)M * N * 2));
+      CK(hipDeviceSynchronize());   // hipMemset runs on the null stream: order it before the s0 launch
       v.run(A, W, bias, C, M, N, K, s0);
       CK(hipStreamSynchronize(s0));
       CK(hipGetLastError());

@@ -14,6 +14,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("trace")
     ap.add_argument("--tail", type=float, default=0.5, help="fraction of the trace (by time) to analyse")
+    ap.add_argument("--timeline", default="", help="write a 3 ms kernel timeline (start end queue name) here")
     a = ap.parse_args()
     rows = list(csv.DictReader(open(a.trace)))
     ev = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Queue_Id"], r["Kernel_Name"]) for r in rows)
@@ -53,6 +54,42 @@ def main():
         depth += d
         last = t
     print(f">=2 kernels concurrently: {two / span:.1%}")
+    # per kernel name: how much of its time another queue's kernel ran beside it
+    other = collections.defaultdict(list)     # queue -> sorted (s, e) of every OTHER queue's kernels
+    for q in per_q:
+        other[q] = sorted((e[0], e[1]) for e in ev if e[2] != q)
+    import bisect
+
+    by_name = collections.defaultdict(lambda: [0, 0, 0])   # name -> [count, dur, overlapped]
+    for q, es in per_q.items():
+        o = other[q]
+        starts = [x[0] for x in o]
+        for s, e, _q, name in es:
+            ov = 0
+            i = max(0, bisect.bisect_left(starts, s) - 8)
+            while i < len(o) and o[i][0] < e:
+                ov += max(0, min(e, o[i][1]) - max(s, o[i][0]))
+                i += 1
+            rec = by_name[_short(name)]
+            rec[0] += 1
+            rec[1] += e - s
+            rec[2] += min(ov, e - s)
+    print("per kernel: share of its time with another queue's kernel running")
+    for name, (n, d, ov) in sorted(by_name.items(), key=lambda kv: -kv[1][1])[:16]:
+        print(f"  {d / span:6.1%} of window  {n:6d} x {d / n / 1e3:7.2f} us  overlapped {ov / d:5.1%}  {name}")
+    if a.timeline:
+        t_mid = ev[len(ev) // 2][0]
+        with open(a.timeline, "w") as f:
+            for s, e, q, name in ev:
+                if t_mid <= s < t_mid + 3_000_000:
+                    f.write(f"{(s - t_mid) / 1e3:9.2f} {(e - t_mid) / 1e3:9.2f} q{q} {_short(name)}\n")
+
+
+def _short(name: str) -> str:
+    n = name.split("(")[0]
+    for pre in ("void ", "rdb::"):
+        n = n.replace(pre, "")
+    return n[:90]
 
 
 if __name__ == "__main__":

@@ -90,6 +90,10 @@ class BertForSequenceClassification:
         self.rowln_o = rl in ("1", "o")
         self.rowln_d = rl in ("1", "d")
         self.rowln_min_rows = int(os.environ.get("RDB_BERT_ROWLN_MIN_ROWS", "2048"))
+        # RDB_ABLATE (profiling only -- WRONG outputs, never a measurement): comma
+        # list of ops to skip in the hip forward ("ln": the in-stack LayerNorm
+        # kernels, "gelu": FFN-up's activation) to bound what removing them can buy
+        self.ablate = {a for a in os.environ.get("RDB_ABLATE", "").split(",") if a}
         env = os.environ.get("RDB_BERT_FOLD_LN", "")
         self.fold_ln_auto = env == ""
         self.fold_ln = env == "1" or (env == "" and self.auto_fold_ln(1))
@@ -286,13 +290,13 @@ class BertForSequenceClassification:
                 h1 = ops.linear_rowln(ctx, rp[0], L["b_o"], h, L["ln1_g"], L["ln1_b"], c.eps)
             else:
                 a = ops.linear(ctx, L["w_o"], L["b_o"], residual=h)
-                h1 = ops.layer_norm(a, L["ln1_g"], L["ln1_b"], c.eps)
-            inter = ops.linear(h1, L["w_i"], L["b_i"], act="gelu")
+                h1 = a if "ln" in self.ablate and not cls_rows else ops.layer_norm(a, L["ln1_g"], L["ln1_b"], c.eps)
+            inter = ops.linear(h1, L["w_i"], L["b_i"], act="none" if "gelu" in self.ablate else "gelu")
             if rowln and self.rowln_d:
                 h = ops.linear_rowln(inter, rp[1], L["b_out"], h1, L["ln2_g"], L["ln2_b"], c.eps)
             else:
                 o = ops.linear(inter, L["w_out"], L["b_out"], residual=h1)
-                h = ops.layer_norm(o, L["ln2_g"], L["ln2_b"], c.eps)
+                h = o if "ln" in self.ablate and not cls_rows else ops.layer_norm(o, L["ln2_g"], L["ln2_b"], c.eps)
         cls = h if self.cls_only_last_layer else h.view(B, S, D)[:, 0, :]
         pooled = ops.linear(cls, self.w_pool, self.b_pool, act="tanh")
         return ops.linear(pooled, self.w_cls, self.b_cls, out_dtype=torch.float32)

@@ -242,6 +242,44 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
     return out
 
 
+def streamk_workspace(device, grid: int = 192, tile: int = 0) -> torch.Tensor:
+    """A zeroed workspace for ``linear_streamk`` (arrival counters + f32 partial
+    tiles).  One per stream: two launches must never share one at the same time."""
+    n = int(_ops().gemm_sk_workspace_size(int(tile), int(grid)))
+    return torch.zeros(n, device=device, dtype=torch.uint8)
+
+
+def linear_streamk(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, act: str = "none",
+                   residual: Optional[torch.Tensor] = None, workspace: Optional[torch.Tensor] = None,
+                   grid: int = 192, tile: int = 0, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``linear`` on the stream-K ping-pong GEMM (ops/csrc/gemm_sk.h): the
+    (tile, K-step) space split evenly over ``grid`` workgroups, split tiles
+    finished by their last-arriving segment.  bf16 only, contiguous operands,
+    N % 8 == 0.  tile 0 = 256 x 128 (BK 64, 3 stages), 1 = 128 x 128 (BK 64, 4 stages)."""
+    _check(x.is_cuda and w.is_cuda and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16,
+           "linear_streamk: bf16 GPU tensors")
+    _check(w.dim() == 2 and w.is_contiguous() and x.is_contiguous(), "linear_streamk: contiguous x, w")
+    N, K = w.shape
+    _check(x.shape[-1] == K and K % 8 == 0 and N % 8 == 0, "linear_streamk: shapes")
+    _check(act != "swiglu", "linear_streamk: no SwiGLU")
+    x2 = x.reshape(-1, K)
+    M = x2.shape[0]
+    if out is None:
+        out = torch.empty(*x.shape[:-1], N, device=x.device, dtype=x.dtype)
+    _check(out.is_contiguous() and out.numel() == M * N, "linear_streamk: bad out")
+    if residual is not None:
+        _check(residual.is_contiguous() and residual.numel() == M * N and residual.dtype == x.dtype,
+               "linear_streamk: bad residual")
+    if bias is not None:
+        _check(bias.is_contiguous() and bias.numel() == N and bias.dtype == x.dtype, "linear_streamk: bad bias")
+    need = int(_ops().gemm_sk_workspace_size(int(tile), int(grid)))
+    _check(workspace is not None and workspace.is_cuda and workspace.numel() >= need,
+           f"linear_streamk: needs a zeroed workspace of {need} bytes (ops.streamk_workspace)")
+    _ops().gemm_sk_bf16(x2.data_ptr(), K, w.data_ptr(), K, out.data_ptr(), N, _ptr(bias), _ptr(residual), N, M, N,
+                        K, 1.0, ACT_CODE[act], workspace.data_ptr(), int(grid), int(tile), _stream())
+    return out
+
+
 LN_LNA, LN_LNR, LN_STATS, LN_SELF = 1, 2, 4, 8
 
 

@@ -19,6 +19,10 @@ void gemm_tn_ln(uintptr_t A, int lda, uintptr_t W, int ldw, uintptr_t C, int ldc
                 uintptr_t a_colsum, uintptr_t a_bias, uintptr_t r_stats, int r_ld, uintptr_t r_g, uintptr_t r_b,
                 uintptr_t o_stats, int o_ld, float a_inv_d, float r_inv_d, float eps, uintptr_t stream, int cfg,
                 uintptr_t panel, uintptr_t err);
+void gemm_sk_bf16(uintptr_t A, int lda, uintptr_t W, int ldw, uintptr_t C, int ldc, uintptr_t bias, uintptr_t R,
+                  int ldr, int M, int N, int K, float alpha, int act, uintptr_t workspace, int grid, int tile,
+                  uintptr_t stream);
+size_t gemm_sk_workspace_size(int tile, int grid);
 void gemm_rowln(uintptr_t A, int lda, uintptr_t W, uintptr_t bias, uintptr_t R, int ldr, uintptr_t gamma,
                 uintptr_t beta, uintptr_t C, int ldc, int M, int N, int K, float eps, uintptr_t stream);
 void norm_fwd(int dtype, int mode, uintptr_t x, uintptr_t res, uintptr_t res_out, uintptr_t gamma,
@@ -79,6 +83,8 @@ PYBIND11_MODULE(_rdb_ops, m) {
         py::arg("o_ld"), py::arg("a_inv_d"), py::arg("r_inv_d"), py::arg("eps"), py::arg("stream"), py::arg("cfg"),
         py::arg("panel") = 0, py::arg("err") = 0, py::call_guard<py::gil_scoped_release>());
   m.def("gemm_rowln", &rdb::gemm_rowln, py::call_guard<py::gil_scoped_release>());
+  m.def("gemm_sk_bf16", &rdb::gemm_sk_bf16, py::call_guard<py::gil_scoped_release>());
+  m.def("gemm_sk_workspace_size", &rdb::gemm_sk_workspace_size);
   m.def("norm_fwd", &rdb::norm_fwd, py::call_guard<py::gil_scoped_release>());
   m.def("embed_ln_fwd", &rdb::embed_ln_fwd, py::call_guard<py::gil_scoped_release>());
   m.def("attn_fwd", &rdb::attn_fwd, py::call_guard<py::gil_scoped_release>());

@@ -178,6 +178,7 @@ class Engine {
     fault_drop_every_ = knob("RDB_FAULT_DROP_EVERY");
     fault_delay_batch_us_ = knob("RDB_FAULT_DELAY_BATCH_US");
     fault_kill_after_ = knob("RDB_FAULT_KILL_AFTER_BATCHES");
+    idle_dispatch_.store(knob("RDB_IDLE_DISPATCH") != 0);
     for (int s = 0; s < depth_; ++s) {
       hipEvent_t a, b, c;
       ENG_CHECK(hipEventCreateWithFlags(&a, hipEventDisableTiming));
@@ -374,6 +375,8 @@ class Engine {
     s.active.store(on, std::memory_order_seq_cst);
   }
   int compute_streams() const { return (int)compute_streams_.size(); }
+  void set_idle_dispatch(bool on) { idle_dispatch_.store(on, std::memory_order_relaxed); }
+  bool idle_dispatch() const { return idle_dispatch_.load(std::memory_order_relaxed); }
   void set_max_batch(int sid, int b) {
     Session& s = sess(sid);
     if (b < 1 || b > s.buckets.back()) throw std::invalid_argument("max_batch out of range");
@@ -637,6 +640,15 @@ class Engine {
           if (!h) {
             const int64_t left = flush_at - now_ns();
             if (left <= 0 || !running_) break;
+            if (idle_dispatch_.load(std::memory_order_relaxed)) {
+              // idle dispatch (opt-in): a partial batch goes out as soon as a
+              // compute stream has no batch running, instead of waiting out the
+              // first-arrival timeout while the GPU sits idle; the wait is
+              // chunked so a stream going idle is noticed within ~20 us
+              if (n > 0 && gpu_running_.load(std::memory_order_acquire) < (int)compute_streams_.size()) break;
+              s.ring.wait_for(s.peek_pos, std::min<int64_t>(left, 20000), 2000);
+              continue;
+            }
             if (!s.ring.wait_for(s.peek_pos, left, 4000)) break;
             continue;
           }
@@ -713,6 +725,7 @@ class Engine {
             f.solo = gpu_inflight_ == 0;
             f.seq = launch_seq_.fetch_add(1, std::memory_order_acq_rel) + 1;
             ++gpu_inflight_;
+            gpu_running_.fetch_add(1, std::memory_order_acq_rel);
           }
           inflight_.push_back(std::move(f));
         }
@@ -750,6 +763,7 @@ class Engine {
             if (q != hipErrorNotReady) ENG_CHECK(q);
             std::this_thread::yield();
           }
+          gpu_running_.fetch_sub(1, std::memory_order_acq_rel);
           const int64_t t_obs = now_ns();
           roctxRangePushA("rdb:complete");
           float ms = 0.f;
@@ -843,6 +857,8 @@ class Engine {
   std::vector<bool> slot_busy_;
   std::deque<InFlight> inflight_;
   int gpu_inflight_ = 0;                   // GPU batches launched and not yet completed (under mu_)
+  std::atomic<int> gpu_running_{0};        // GPU batches whose done-event has not fired yet
+  std::atomic<bool> idle_dispatch_{false}; // batch policy: dispatch partial batches onto an idle stream
   std::atomic<uint64_t> launch_seq_{0};    // GPU launches so far (solo detection)
   std::mutex mu_;
   std::condition_variable cv_;
@@ -884,6 +900,8 @@ void register_engine(py::module_& m) {
       .def("session_retired", &Engine::session_retired)
       .def("num_sessions", &Engine::num_sessions)
       .def("compute_streams", &Engine::compute_streams)
+      .def("set_idle_dispatch", &Engine::set_idle_dispatch)
+      .def("idle_dispatch", &Engine::idle_dispatch)
       .def("set_max_batch", &Engine::set_max_batch)
       .def("set_max_wait", &Engine::set_max_wait)
       .def("start", &Engine::start, py::call_guard<py::gil_scoped_release>())

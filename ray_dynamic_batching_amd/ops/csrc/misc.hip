@@ -12,35 +12,49 @@
 
 namespace rdb {
 
-// One wave per row, C <= 64 * 64 = 4096, k <= 16.
-__global__ void __launch_bounds__(256)
-softmax_topk_kernel(const float* __restrict__ x, int rows, int C, int k,
-                    float* __restrict__ probs, int* __restrict__ idx) {
-  const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= rows) return;
+// One wave per row, one row per 64-thread workgroup (so a 32-row batch runs on
+// 32 CUs, not 8), C <= 4096, k <= 16.  Each lane holds NV float4 of the row
+// (16-B loads when C % 4 == 0 and the rows are 16-B aligned, else element
+// loads): C = 1000 is 4 float4 per lane instead of the 64 scalar registers a
+// fixed 4096-wide layout scans per top-k pass.
+template <int NV, bool VEC>
+__global__ void __launch_bounds__(64)
+softmax_topk_kernel(const float* __restrict__ x, int rows, int C, int k, float* __restrict__ probs,
+                    int* __restrict__ idx) {
+  const int lane = threadIdx.x;
+  const int row = blockIdx.x;
   const float* xr = x + (size_t)row * C;
-  float v[64];
+  // element e of this lane: column 4 * (lane + 64 * (e / 4)) + e % 4
+  float v[NV * 4];
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c0 = 4 * (lane + 64 * i);
+    if constexpr (VEC) {
+      f32x4 q = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+      if (c0 < C) q = *reinterpret_cast<const f32x4*>(xr + c0);   // C % 4 == 0: whole vector in range
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[4 * i + e] = q[e];
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[4 * i + e] = c0 + e < C ? xr[c0 + e] : -INFINITY;
+    }
+  }
   float mx = -INFINITY;
 #pragma unroll
-  for (int i = 0; i < 64; ++i) {
-    const int c = lane + 64 * i;
-    v[i] = (c < C) ? xr[c] : -INFINITY;
-    mx = fmaxf(mx, v[i]);
-  }
+  for (int e = 0; e < NV * 4; ++e) mx = fmaxf(mx, v[e]);
   mx = wave_max(mx);
   float s = 0.f;
 #pragma unroll
-  for (int i = 0; i < 64; ++i) s += (lane + 64 * i < C) ? __expf(v[i] - mx) : 0.f;
+  for (int e = 0; e < NV * 4; ++e) s += __expf(v[e] - mx);   // exp(-inf) = 0 for the padding
   s = wave_sum(s);
   const float inv = 1.f / s;
   for (int t = 0; t < k; ++t) {
     float best = -INFINITY;
     int bi = 0x7fffffff;
 #pragma unroll
-    for (int i = 0; i < 64; ++i) {
-      const int c = lane + 64 * i;
-      if (v[i] > best || (v[i] == best && c < bi)) { best = v[i]; bi = c; }
+    for (int e = 0; e < NV * 4; ++e) {
+      const int c = 4 * (lane + 64 * (e >> 2)) + (e & 3);
+      if (v[e] > best) { best = v[e]; bi = c; }   // ascending c per lane: the first max wins ties
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
@@ -52,19 +66,34 @@ softmax_topk_kernel(const float* __restrict__ x, int rows, int C, int k,
       probs[(size_t)row * k + t] = __expf(best - mx) * inv;
       idx[(size_t)row * k + t] = bi < C ? bi : -1;
     }
-    // remove the winner
 #pragma unroll
-    for (int i = 0; i < 64; ++i)
-      if (lane + 64 * i == bi) v[i] = -INFINITY;
+    for (int e = 0; e < NV * 4; ++e)
+      if (4 * (lane + 64 * (e >> 2)) + (e & 3) == bi) v[e] = -INFINITY;   // remove the winner
   }
+}
+
+template <int NV>
+static void launch_softmax_topk(const float* x, int rows, int C, int k, float* probs, int* idx, hipStream_t st) {
+  const bool vec = (C & 3) == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0;
+  if (vec)
+    hipLaunchKernelGGL((softmax_topk_kernel<NV, true>), dim3(rows), dim3(64), 0, st, x, rows, C, k, probs, idx);
+  else
+    hipLaunchKernelGGL((softmax_topk_kernel<NV, false>), dim3(rows), dim3(64), 0, st, x, rows, C, k, probs, idx);
 }
 
 void softmax_topk(uintptr_t x, int rows, int C, int k, uintptr_t probs, uintptr_t idx, uintptr_t stream) {
   if (C > 4096 || k < 1 || k > 16 || k > C) throw std::invalid_argument("softmax_topk: need C <= 4096, 1 <= k <= min(16, C)");
   if (rows <= 0) return;
-  hipLaunchKernelGGL(softmax_topk_kernel, dim3((rows + 3) / 4), dim3(256), 0,
-                     reinterpret_cast<hipStream_t>(stream), (const float*)x, rows, C, k,
-                     (float*)probs, (int*)idx);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const float* xp = (const float*)x;
+  float* pp = (float*)probs;
+  int* ip = (int*)idx;
+  const int nv = (C + 255) / 256;   // float4 per lane
+  if (nv <= 1) launch_softmax_topk<1>(xp, rows, C, k, pp, ip, st);
+  else if (nv <= 2) launch_softmax_topk<2>(xp, rows, C, k, pp, ip, st);
+  else if (nv <= 4) launch_softmax_topk<4>(xp, rows, C, k, pp, ip, st);
+  else if (nv <= 8) launch_softmax_topk<8>(xp, rows, C, k, pp, ip, st);
+  else launch_softmax_topk<16>(xp, rows, C, k, pp, ip, st);
   RDB_HIP_CHECK(hipGetLastError());
 }
 

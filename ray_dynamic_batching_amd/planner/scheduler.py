@@ -216,7 +216,10 @@ class EngineExecutor:
     resident set would exceed ``hbm_budget_bytes``."""
 
     def __init__(self, sched: "SLOScheduler", gpu: int, device: int, max_batch: Dict[str, int],
-                 compute_streams: int = 1):
+                 compute_streams: int = 1, policy: str = "duty"):
+        """``policy``: "duty" (Nexus duty cycle: each session's planned batch per
+        cycle within its GPU-time share, work-conserving backfill) or
+        "priority" (no cycle: highest priority, then earliest deadline first)."""
         import torch
 
         from ..runtime.engine import EngineRunner
@@ -235,8 +238,13 @@ class EngineExecutor:
         self.rerouted = 0
         self.failed_on_unload = 0
         with torch.cuda.device(device):
+            if policy not in ("duty", "priority"):
+                raise ValueError(f"engine policy must be 'duty' or 'priority', got {policy!r}")
+            self.policy = policy
             self.runner = EngineRunner(sched.job_name, gpu, [], pipeline_depth=2, device=device,
-                                       policy=EngineRunner.POLICY_DUTY_CYCLE, compute_streams=compute_streams)
+                                       policy=(EngineRunner.POLICY_DUTY_CYCLE if policy == "duty"
+                                               else EngineRunner.POLICY_PRIORITY_EDF),
+                                       compute_streams=compute_streams)
             self.runner.tune_in_context = False
             self.runner.pools = [torch.cuda.graph_pool_handle() for _ in range(self.runner.compute_streams)]
         self.runner.start()
@@ -348,7 +356,7 @@ class SLOScheduler:
                  executor: str = "python", devices: Optional[List[int]] = None,
                  max_batch: Optional[Dict[str, int]] = None, plan_path: Optional[str] = None,
                  hbm_budget_gb: Optional[float] = None, model_footprint_gb: Optional[Dict[str, float]] = None,
-                 compute_streams: int = 1):
+                 compute_streams: int = 1, engine_policy: str = "duty"):
         """``executor``: "python" (DutyCycleExecutor threads; CPU / arbitrary torch
         models) or "engine" (native GPU engines, one per entry of ``devices``;
         ``max_batch`` = largest batch captured per model).  ``plan_path``: every
@@ -403,8 +411,8 @@ class SLOScheduler:
         if executor == "engine":
             devices = list(devices if devices is not None else range(num_gpus))
             mb = {m: (max_batch or {}).get(m, 32) for m in self.models}
-            self.executors = [EngineExecutor(self, g, devices[g], mb, compute_streams=compute_streams)
-                              for g in range(num_gpus)]
+            self.executors = [EngineExecutor(self, g, devices[g], mb, compute_streams=compute_streams,
+                                             policy=engine_policy) for g in range(num_gpus)]
         else:
             self.executors = [DutyCycleExecutor(self, g) for g in range(num_gpus)]
             for e in self.executors:

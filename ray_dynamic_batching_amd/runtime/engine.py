@@ -53,12 +53,18 @@ class EngineRunner:
 
     def __init__(self, job_name: str, replica: int, sessions: Sequence[SessionSpec], pipeline_depth: int = 2,
                  zero_copy: bool = True, device: Optional[int] = None, warmup_iters: int = 2, policy: int = 0,
-                 compute_streams: int = 1):
+                 compute_streams: int = 1, batch_policy: str = "timeout"):
         """``policy``: 0 = priority then earliest-deadline-first across sessions
         (co-located models, config 5); 1 = Nexus duty cycle (``set_duty_cycle`` +
         per-session ``set_duty_share``).  ``compute_streams`` > 1 runs that many
         batches concurrently (one hipGraph per pipeline slot, slot i on stream
-        i % n, separate graph memory pools per stream so they never alias)."""
+        i % n, separate graph memory pools per stream so they never alias).
+        ``batch_policy``: "timeout" (default, ``@serve.batch`` semantics: a batch
+        closes when full or ``max_wait`` after its first request) or "idle" (a
+        partial batch is also dispatched as soon as a compute stream has no batch
+        running -- lower latency at low load, same batches under saturation)."""
+        if batch_policy not in ("timeout", "idle"):
+            raise ValueError(f"batch_policy must be 'timeout' or 'idle', got {batch_policy!r}")
         self.ops = require_gpu_ops()
         self.device = torch.cuda.current_device() if device is None else device
         self.job_name = job_name
@@ -68,6 +74,9 @@ class EngineRunner:
         self.compute_streams = max(1, min(compute_streams, pipeline_depth))
         self.engine = self.ops.Engine(job_name, replica, pipeline_depth, zero_copy, self.device, policy,
                                       self.compute_streams)
+        self.batch_policy = batch_policy
+        if batch_policy == "idle":
+            self.engine.set_idle_dispatch(True)
         self.pools = []
         self.capture_s = 0.0
         self.warmup_iters = warmup_iters

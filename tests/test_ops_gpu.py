@@ -190,14 +190,23 @@ def test_qkv_attention_matches_two_kernel_path():
     _close(y, two, 2e-2, 2e-2)
 
 
-def test_softmax_topk():
+@pytest.mark.parametrize("C,k", [(1000, 5), (999, 5), (10, 1), (257, 16), (4096, 3), (1000, 1)])
+def test_softmax_topk(C, k):
+    """wave-per-row kernel (float4 lanes when C % 4 == 0, element loads otherwise)
+    against the fp32 reference, including the tie rule (lowest index first)."""
     ops = _ops()
     torch.manual_seed(6)
-    x = torch.randn(37, 1000, device="cuda")
-    p, i = ops.softmax_topk(x, 5)
-    pr, ir = ops.softmax_topk_ref(x, 5)
+    x = torch.randn(37, C, device="cuda")
+    p, i = ops.softmax_topk(x, k)
+    pr, ir = ops.softmax_topk_ref(x, k)
     assert torch.equal(i, ir)
     _close(p, pr, 1e-5, 1e-4)
+    # ties: small integers, many equal maxima -> lowest column wins, like torch.topk on sorted ties
+    xt = torch.randint(0, 3, (8, C), device="cuda").float()
+    pt, it = ops.softmax_topk(xt, k)
+    mx = xt.max(dim=1, keepdim=True).values
+    first = torch.stack([torch.nonzero(xt[r] == mx[r]).flatten()[0] for r in range(8)])
+    assert torch.equal(it[:, 0].long(), first)
 
 
 def test_rope():
@@ -614,3 +623,26 @@ def test_graph_replayed_plain_store_kernel_visible_to_d2h(readback):
         got = (y.clone() if readback == "blit" else y).cpu()
         ref = ops.linear_ref(x, w, b, act="gelu").cpu()
         _close(got, ref, 2e-2, 2e-2)
+
+
+@pytest.mark.parametrize("M,N,K,tile,grid", [(4096, 768, 3072, 0, 192), (4096, 768, 768, 1, 192),
+                                             (1000, 768, 3072, 0, 256), (37, 256, 512, 0, 64),
+                                             (4096, 2304, 768, 1, 256)])
+def test_linear_streamk(M, N, K, tile, grid):
+    """stream-K GEMM (split tiles finished by the last-arriving segment) against
+    the fp32 reference, over repeated launches on one workspace (the arrival
+    counters must reset themselves) and on a ragged M."""
+    ops = _ops()
+    torch.manual_seed(11)
+    x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    w = torch.randn(N, K, device="cuda", dtype=torch.bfloat16) * 0.03
+    b = torch.randn(N, device="cuda", dtype=torch.bfloat16) * 0.1
+    r = torch.randn(M, N, device="cuda", dtype=torch.bfloat16)
+    ws = ops.streamk_workspace("cuda", grid, tile)
+    ref = x.float() @ w.float().t() + b.float() + r.float()
+    for _ in range(3):
+        y = ops.linear_streamk(x, w, b, residual=r, workspace=ws, grid=grid, tile=tile)
+        _close(y, ref, 2e-2, 2e-2)
+    g = ops.linear_streamk(x, w, b, act="gelu", workspace=ws, grid=grid, tile=tile)
+    _close(g, torch.nn.functional.gelu(x.float() @ w.float().t() + b.float()), 2e-2, 2e-2)
+    assert int(ws[:65536].view(torch.int32).abs().sum()) == 0     # counters clean after every launch
