@@ -315,24 +315,25 @@ __device__ __forceinline__ void staged_epilogue(char* smem, const f32x4 (&acc)[T
     // the tile is parked as 16-bit output (half the LDS traffic of f32, twice
     // the rows per chunk) and phase 2 only moves 16-B row segments to global.
     typedef StagedEpi16<BM, BN, SMEM_BYTES> E16;
-    // bias + activation on EVERY wave's fragments first (all 8 waves busy: a
-    // row chunk may belong to one wave group only), packed to 16-bit pairs
-    u32x2 pk[TN][TM];
+    // bias + activation fragment by fragment, each packed to 16-bit pairs and
+    // parked right away: only the accumulators stay live.  (Building the
+    // whole packed tile first held it beside the accumulators and the
+    // activation temporaries -- 128 VGPRs spilled on the 2-blocks-per-CU
+    // 256x128 FFN-up tile, 244 on 256x256.)  A fragment's 16 rows never
+    // straddle a chunk (RC % 16 == 0), so the chunk test is wave-uniform; with
+    // several chunks only the waves owning the chunk's rows compute in it.
+    auto park = [&](int i, int j, int rt) {
+      const int nt = col_base + i * 16 + fg * 4;
+      f32x4 v = acc[i][j] * alpha;
+      if constexpr (BREG) {
 #pragma unroll
-    for (int j = 0; j < TM; ++j)
-#pragma unroll
-      for (int i = 0; i < TN; ++i) {
-        const int nt = col_base + i * 16 + fg * 4;
-        f32x4 v = acc[i][j] * alpha;
-        if constexpr (BREG) {
-#pragma unroll
-          for (int q = 0; q < 4; ++q) v[q] += bv[i][q];
-        } else if constexpr (HAS_BIAS) {
-          v += *reinterpret_cast<const f32x4*>(smem + BIAS_LDS + nt * 4);
-        }
-        OutT o4[4] = {(OutT)actf(v[0]), (OutT)actf(v[1]), (OutT)actf(v[2]), (OutT)actf(v[3])};
-        pk[i][j] = *reinterpret_cast<const u32x2*>(o4);
+        for (int q = 0; q < 4; ++q) v[q] += bv[i][q];
+      } else if constexpr (HAS_BIAS) {
+        v += *reinterpret_cast<const f32x4*>(smem + BIAS_LDS + nt * 4);
       }
+      OutT o4[4] = {(OutT)actf(v[0]), (OutT)actf(v[1]), (OutT)actf(v[2]), (OutT)actf(v[3])};
+      *reinterpret_cast<u32x2*>(smem + rt * E16::ROWB + nt * 2) = *reinterpret_cast<const u32x2*>(o4);
+    };
 #pragma unroll 1
     for (int c = 0; c < BM / E16::RC; ++c) {
 #pragma unroll
@@ -341,8 +342,10 @@ __device__ __forceinline__ void staged_epilogue(char* smem, const f32x4 (&acc)[T
         if (rt >= 0 && rt < E16::RC) {
 #pragma unroll
           for (int i = 0; i < TN; ++i) {
-            const int nt = col_base + i * 16 + fg * 4;
-            *reinterpret_cast<u32x2*>(smem + rt * E16::ROWB + nt * 2) = pk[i][j];
+            park(i, j, rt);
+            // keep the scheduler from interleaving every fragment's activation
+            // (the no-bias variants spilled 51..245 VGPRs without it)
+            __builtin_amdgcn_sched_barrier(0);
           }
         }
       }
