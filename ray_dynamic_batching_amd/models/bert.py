@@ -94,6 +94,12 @@ class BertForSequenceClassification:
         # list of ops to skip in the hip forward ("ln": the in-stack LayerNorm
         # kernels, "gelu": FFN-up's activation) to bound what removing them can buy
         self.ablate = {a for a in os.environ.get("RDB_ABLATE", "").split(",") if a}
+        # RDB_BERT_LN_PSTATS=1: no LayerNorm kernel in the stack and no statistics
+        # work in any main loop -- o-proj / FFN-down write per-N-tile partial row
+        # statistics from their staged epilogues, FFN-up / the next QKV+attention
+        # run on the raw rows with the LayerNorm folded into their weights, residual
+        # adds normalise on load (_forward_hip_pstats)
+        self.ln_pstats = os.environ.get("RDB_BERT_LN_PSTATS", "0") == "1"
         env = os.environ.get("RDB_BERT_FOLD_LN", "")
         self.fold_ln_auto = env == ""
         self.fold_ln = env == "1" or (env == "" and self.auto_fold_ln(1))
@@ -241,6 +247,10 @@ class BertForSequenceClassification:
 
     def _forward_hip(self, ids: torch.Tensor) -> torch.Tensor:
         c = self.cfg
+        if (self.ln_pstats and self.dtype == torch.bfloat16 and c.hidden % 8 == 0 and c.intermediate % 8 == 0
+                and self.fuse_qkv_attn and ops.qkv_attention_supported(ids.shape[1], c.heads, c.hidden // c.heads,
+                                                                       c.hidden)):
+            return self._forward_hip_pstats(ids)
         if self.fold_ln and self.dtype == torch.bfloat16 and c.hidden % 4 == 0:
             if self.fuse_qkv_attn and ops.qkv_attention_supported(ids.shape[1], c.heads, c.hidden // c.heads, c.hidden):
                 return self._forward_hip_fused_deferred(ids)
@@ -345,6 +355,54 @@ class BertForSequenceClassification:
             x, xg, xb = o, L["ln2_g"], L["ln2_b"]
         if h is None:
             h = ops.layer_norm(x, xg, xb, eps) if xg is not None else x
+            h = h.view(B, S, D)[:, 0, :]
+        pooled = ops.linear(h, self.w_pool, self.b_pool, act="tanh")
+        return ops.linear(pooled, self.w_cls, self.b_cls, out_dtype=torch.float32)
+
+    def _forward_hip_pstats(self, ids: torch.Tensor) -> torch.Tensor:
+        """Four kernels per layer, no LayerNorm kernel and no statistics work in
+        any main loop (gemm_core.h EPI_STG): the o-projection and FFN-down write
+        per-N-tile partial (sum, sum of squares) of their raw (pre-LayerNorm)
+        rows from the row-major phase of their staged epilogues; FFN-up and the
+        next layer's fused QKV+attention consume those raw rows with the
+        LayerNorm folded into their weights and correct in their epilogues
+        (rstd (x W'^T - mean colsum) + b'); the residual adds normalise their
+        operand on load.  Layer 0 reads embed_ln's normalised rows directly."""
+        c = self.cfg
+        B, S = ids.shape
+        D, H, eps = c.hidden, c.heads, c.eps
+        Wd = self._deferred_weights()
+        kid = (ids.contiguous(), c.pad_token_id) if ids.dtype == torch.int32 else None
+        lens = None if kid is not None else ops.seq_lens(ids, c.pad_token_id)
+        M = B * S
+        n = len(self.layers)
+        x = ops.embed_ln(ids, self.word, self.pos, self.typ, self.emb_g, self.emb_b, eps).reshape(M, D)
+        xst = xg = xb = None       # x is raw (pre-LN2 of the previous layer) iff xst is not None
+        h = None
+        for i, L in enumerate(self.layers):
+            d = Wd[i]
+            if xst is None:
+                ctx = ops.qkv_attention(x, d["wq"], d["bq"], B, S, H, lens=lens, key_ids=kid)
+            else:
+                ctx = ops.qkv_attention(x, d["wq"], None, B, S, H, lens=lens, key_ids=kid,
+                                        lna=(d["csq"], d["bfq"], eps), a_stats=xst)
+            if i == n - 1 and self.cls_only_last_layer:
+                xc = x.view(B, S, D)[:, 0, :]
+                hc = xc if xst is None else ops.layer_norm(xc, xg, xb, eps)
+                a = ops.linear(ctx.view(B, S, D)[:, 0, :], L["w_o"], L["b_o"], residual=hc)
+                h1 = ops.layer_norm(a, L["ln1_g"], L["ln1_b"], eps)
+                inter = ops.linear(h1, L["w_i"], L["b_i"], act="gelu")
+                o = ops.linear(inter, L["w_out"], L["b_out"], residual=h1)
+                h = ops.layer_norm(o, L["ln2_g"], L["ln2_b"], eps)
+                break
+            lnr = None if xst is None else (xst, xg, xb, D, eps)
+            a, ast = ops.linear_ln_staged(ctx, L["w_o"], L["b_o"], residual=x, lnr=lnr, pstats=True)
+            inter = ops.linear_ln_staged(a, d["w_i"], act="gelu", lna=(ast, d["cs_i"], d["b_i"], D, eps))
+            o, ost = ops.linear_ln_staged(inter, L["w_out"], L["b_out"], residual=a,
+                                          lnr=(ast, L["ln1_g"], L["ln1_b"], D, eps), pstats=True)
+            x, xst, xg, xb = o, ost, L["ln2_g"], L["ln2_b"]
+        if h is None:
+            h = ops.layer_norm(x, xg, xb, eps) if xst is not None else x
             h = h.view(B, S, D)[:, 0, :]
         pooled = ops.linear(h, self.w_pool, self.b_pool, act="tanh")
         return ops.linear(pooled, self.w_cls, self.b_cls, out_dtype=torch.float32)

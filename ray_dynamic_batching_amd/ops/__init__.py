@@ -281,12 +281,103 @@ def linear_streamk(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor
 
 
 LN_LNA, LN_LNR, LN_STATS, LN_SELF = 1, 2, 4, 8
+LN_STG = 32            # gemm_core.h EPI_STG: staged LayerNorm epilogues with per-N-tile partial statistics
+STG_TILE_CFGS = (0, 9, 10, 12, 19, 21, 23, 24)   # gemm_core.h kStgTiles
+_PSTATS_MAX = 16       # partials per row a producer may write (N / smallest staged BN, N = 768: 768 / 48)
+
+
+def _pstats_layout(st: torch.Tensor, M: int, what: str):
+    """(row stride in floats, partials per row) of a [M, P, 2] f32 partial-statistics view."""
+    _check(st.dtype == torch.float32 and st.dim() == 3 and st.shape[0] == M and st.shape[2] == 2
+           and st.stride(2) == 1 and st.stride(1) == 2 and st.stride(0) % 2 == 0 and _aligned(st, 8),
+           f"{what}: partial statistics must be a [M, P, 2] f32 row-strided view")
+    return st.stride(0), st.shape[1]
 
 
 def _stats_ld(st: torch.Tensor, M: int, what: str) -> int:
     _check(st.dtype == torch.float32 and st.dim() == 2 and st.shape[0] == M and st.shape[1] >= 2
            and st.stride(1) == 1 and st.stride(0) % 2 == 0 and _aligned(st, 8), f"linear_ln: bad {what} stats")
     return st.stride(0)
+
+
+def linear_ln_staged(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, act: str = "none",
+                     residual: Optional[torch.Tensor] = None, lna: Optional[tuple] = None,
+                     lnr: Optional[tuple] = None, pstats: bool = False, out: Optional[torch.Tensor] = None,
+                     tile_cfg: int = -1):
+    """The deferred-LayerNorm GEMM on the STAGED epilogue with partial statistics
+    (gemm_core.h EPI_STG; ping-pong and 4-wave tiles):
+
+    * ``lna=(stats, colsum, bias_f32, D, eps)``: x holds RAW rows whose LayerNorm
+      is folded into w (``fold_ln_weights``); ``stats`` [M, P, 2] f32 = the
+      producer's per-N-tile partial (sum, sum of squares) of every row.
+      y = act(LN(x) @ W.T + b); no ``bias`` / ``residual``.
+    * ``lnr=(stats, gamma, beta, D, eps)``: ``residual`` holds RAW rows (partials
+      ``stats``), added as LayerNorm(residual).
+    * ``pstats=True``: also returns this GEMM's output statistics as partials
+      [M, P, 2] (P = N-tiles of the tile it ran): ``(out, stats)``.  No zeroing,
+      no atomics: each N-tile writes its own partial.
+    """
+    _check(x.is_cuda and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16, "linear_ln_staged: bf16 on the GPU")
+    _check(w.dim() == 2 and w.is_contiguous(), "linear_ln_staged: w must be a contiguous [N, K] matrix")
+    N, K = w.shape
+    _check(x.dim() == 2 and x.stride(1) == 1 and x.shape[1] == K, "linear_ln_staged: x must be a 2-D [M, K] view")
+    M, lda = x.shape[0], x.stride(0)
+    _check(K % 8 == 0 and lda % 8 == 0 and N % 8 == 0 and _aligned(x) and _aligned(w), "linear_ln_staged: alignment")
+    _check(act != "swiglu", "linear_ln_staged: no swiglu")
+    mode = LN_STG | (LN_LNA if lna is not None else 0) | (LN_LNR if lnr is not None else 0) | \
+        (LN_STATS if pstats else 0)
+    _check(mode in (LN_STG | LN_LNA, LN_STG | LN_STATS, LN_STG | LN_LNR | LN_STATS, LN_STG | LN_LNR),
+           "linear_ln_staged: modes are lna, pstats, lnr + pstats, lnr")
+    if out is None:
+        out = torch.empty(M, N, device=x.device, dtype=x.dtype)
+    _check(out.is_contiguous() and out.shape == (M, N) and _aligned(out), "linear_ln_staged: bad out")
+    if bias is not None:
+        _check(bias.is_contiguous() and bias.numel() == N and bias.dtype == x.dtype, "linear_ln_staged: bad bias")
+    ldr = 0
+    if residual is not None:
+        _check(residual.dim() == 2 and residual.shape == (M, N) and residual.stride(1) == 1
+               and residual.stride(0) % 8 == 0 and residual.dtype == x.dtype and _aligned(residual),
+               "linear_ln_staged: bad residual")
+        ldr = residual.stride(0)
+    a_st = a_cs = a_b = r_st = r_g = r_b = None
+    a_ld = r_ld = 0
+    a_parts = r_parts = 1
+    a_inv = r_inv = 0.0
+    eps = 0.0
+    if lna is not None:
+        a_st, a_cs, a_b, d, eps = lna
+        a_ld, a_parts = _pstats_layout(a_st, M, "lna")
+        _check(a_cs.dtype == torch.float32 and a_cs.numel() == N and a_cs.is_contiguous()
+               and a_b.dtype == torch.float32 and a_b.numel() == N and a_b.is_contiguous(),
+               "linear_ln_staged: bad lna vectors")
+        a_inv = 1.0 / d
+    if lnr is not None:
+        _check(residual is not None, "linear_ln_staged: lnr needs the residual")
+        r_st, r_g, r_b, d, eps = lnr
+        r_ld, r_parts = _pstats_layout(r_st, M, "lnr")
+        _check(r_g.numel() == N and r_b.numel() == N and r_g.dtype == x.dtype and r_b.dtype == x.dtype
+               and r_g.is_contiguous() and r_b.is_contiguous(), "linear_ln_staged: bad lnr gamma/beta")
+        r_inv = 1.0 / d
+    o_buf = None
+    if pstats:
+        o_buf = torch.empty(M, _PSTATS_MAX, 2, device=x.device, dtype=torch.float32)
+    fn = _ops().gemm_tn_ln
+
+    def launch(c):
+        fn(x.data_ptr(), lda, w.data_ptr(), K, out.data_ptr(), N, _ptr(bias), _ptr(residual), ldr, M, N, K, 1.0,
+           ACT_CODE[act], mode, _ptr(a_st), a_ld, _ptr(a_cs), _ptr(a_b), _ptr(r_st), r_ld, _ptr(r_g), _ptr(r_b),
+           _ptr(o_buf), 2 * _PSTATS_MAX if pstats else 0, float(a_inv), float(r_inv), float(eps), _stream(), c,
+           0, 0, a_parts, r_parts)
+
+    if tile_cfg < 0:
+        key = ("gemm_stg", x.dtype, M, N, K, lda, act, mode, a_parts, r_parts)
+        tile_cfg = _tuned_cfg(key, launch, STG_TILE_CFGS)
+    tile_cfg = int(_ops().gemm_stg_cfg(int(tile_cfg)))
+    launch(tile_cfg)
+    if not pstats:
+        return out
+    bn = int(_ops().gemm_tile_bn(tile_cfg))
+    return out, o_buf[:, : -(-N // bn), :]
 
 
 def linear_ln(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, act: str = "none",
@@ -693,7 +784,8 @@ def qkv_attention_supported(S: int, H: int, D: int, K: int) -> bool:
 def qkv_attention(x: torch.Tensor, w_packed: torch.Tensor, b_packed: Optional[torch.Tensor], B: int, S: int, H: int,
                   lens: Optional[torch.Tensor] = None, scale: Optional[float] = None,
                   out: Optional[torch.Tensor] = None, cfg: int = -1, lna: Optional[tuple] = None,
-                  stats_out: Optional[torch.Tensor] = None, key_ids: Optional[tuple] = None) -> torch.Tensor:
+                  stats_out: Optional[torch.Tensor] = None, key_ids: Optional[tuple] = None,
+                  a_stats: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Fused QKV projection + bidirectional attention (qkv_attention.hip):
     ctx [B*S, H*64] = MHA(x @ W^T + b) for S <= 128, head dim 64, with the
     projection weight in ``pack_qkv_heads`` layout.  The [B*S, 3*H*64] QKV
@@ -707,7 +799,10 @@ def qkv_attention(x: torch.Tensor, w_packed: torch.Tensor, b_packed: Optional[to
     LayerNorm is folded into ``w_packed`` (``fold_ln_weights`` then packing);
     the kernel computes each row's statistics itself and, with ``stats_out``
     [B*S, 2] f32, stores (sum, sum of squares) for a later ``linear_ln(lnr=...)``.
-    ``b_packed`` must then be None."""
+    ``b_packed`` must then be None.  ``a_stats`` [B*S, P, 2] f32 (P <= 8, row-
+    strided view): the producer's per-N-tile partial statistics of x
+    (``linear_ln(..., pstats=True)``) -- the kernel sums them instead of
+    computing statistics in its main loop."""
     _check(x.is_cuda and x.dtype in (torch.bfloat16, torch.float16) and x.dim() == 2 and x.stride(1) == 1,
            "qkv_attention: x must be a 2-D [B*S, K] (row-strided) bf16/f16 view")
     N, K = w_packed.shape
@@ -744,10 +839,15 @@ def qkv_attention(x: torch.Tensor, w_packed: torch.Tensor, b_packed: Optional[to
     scale = 1.0 / 8.0 if scale is None else scale
     args = (DTYPE_CODE[x.dtype], x.data_ptr(), x.stride(0), w_packed.data_ptr(), _ptr(b_packed), B, S, H, K,
             _ptr(lens), out.data_ptr(), H * 64, float(scale))
-    extra = (_ptr(cs), _ptr(bf), _ptr(stats_out), float(eps), _ptr(kid), int(pad))
+    a_ld = a_parts = 0
+    if a_stats is not None:
+        _check(lna is not None and stats_out is None, "qkv_attention: a_stats needs lna and no stats_out")
+        a_ld, a_parts = _pstats_layout(a_stats, B * S, "qkv_attention a_stats")
+        _check(a_parts <= 8, "qkv_attention: at most 8 partials per row")
+    extra = (_ptr(cs), _ptr(bf), _ptr(stats_out), float(eps), _ptr(kid), int(pad), _ptr(a_stats), a_ld, a_parts)
     fn = _ops().qkv_attn_fwd
     if cfg < 0:
-        key = ("qkv_attn", x.dtype, B, S, H, K, x.stride(0), lna is not None)
+        key = ("qkv_attn", x.dtype, B, S, H, K, x.stride(0), lna is not None) + (("pstats",) if a_stats is not None else ())
         cfg = _tuned_cfg(key, lambda c: fn(*args, c, _stream(), *extra), range(NUM_QKV_ATTN_CFGS))
     fn(*args, int(cfg), _stream(), *extra)
     return out

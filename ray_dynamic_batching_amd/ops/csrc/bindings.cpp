@@ -18,7 +18,9 @@ void gemm_tn_ln(uintptr_t A, int lda, uintptr_t W, int ldw, uintptr_t C, int ldc
                 int ldr, int M, int N, int K, float alpha, int act, int mode, uintptr_t a_stats, int a_ld,
                 uintptr_t a_colsum, uintptr_t a_bias, uintptr_t r_stats, int r_ld, uintptr_t r_g, uintptr_t r_b,
                 uintptr_t o_stats, int o_ld, float a_inv_d, float r_inv_d, float eps, uintptr_t stream, int cfg,
-                uintptr_t panel, uintptr_t err);
+                uintptr_t panel, uintptr_t err, int a_parts, int r_parts);
+int gemm_stg_cfg(int cfg);
+int gemm_tile_bn(int cfg);
 void gemm_sk_bf16(uintptr_t A, int lda, uintptr_t W, int ldw, uintptr_t C, int ldc, uintptr_t bias, uintptr_t R,
                   int ldr, int M, int N, int K, float alpha, int act, uintptr_t workspace, int grid, int tile,
                   uintptr_t stream);
@@ -35,7 +37,8 @@ void attn_fwd(int dtype, uintptr_t qkv, int ld_qkv, int q_off, int k_off, int v_
               uintptr_t stream);
 void qkv_attn_fwd(int dtype, uintptr_t X, int ldx, uintptr_t Wp, uintptr_t bp, int B, int S, int H, int hidden,
                   uintptr_t lens, uintptr_t out, int ld_out, float scale, int cfg, uintptr_t stream,
-                  uintptr_t colsum, uintptr_t bias_f, uintptr_t stats_out, float eps, uintptr_t key_ids, int pad);
+                  uintptr_t colsum, uintptr_t bias_f, uintptr_t stats_out, float eps, uintptr_t key_ids, int pad,
+                  uintptr_t a_stats, int a_ld, int a_parts);
 void softmax_topk(uintptr_t x, int rows, int C, int k, uintptr_t probs, uintptr_t idx, uintptr_t stream);
 void rope(uintptr_t qkv, int ld, int q_off, int k_off, int H, int Hkv, int D, int S, uintptr_t cos_t,
           uintptr_t sin_t, int T, int pos_offset, uintptr_t stream);
@@ -81,7 +84,10 @@ PYBIND11_MODULE(_rdb_ops, m) {
         py::arg("alpha"), py::arg("act"), py::arg("mode"), py::arg("a_stats"), py::arg("a_ld"), py::arg("a_colsum"),
         py::arg("a_bias"), py::arg("r_stats"), py::arg("r_ld"), py::arg("r_g"), py::arg("r_b"), py::arg("o_stats"),
         py::arg("o_ld"), py::arg("a_inv_d"), py::arg("r_inv_d"), py::arg("eps"), py::arg("stream"), py::arg("cfg"),
-        py::arg("panel") = 0, py::arg("err") = 0, py::call_guard<py::gil_scoped_release>());
+        py::arg("panel") = 0, py::arg("err") = 0, py::arg("a_parts") = 1, py::arg("r_parts") = 1,
+        py::call_guard<py::gil_scoped_release>());
+  m.def("gemm_stg_cfg", &rdb::gemm_stg_cfg, "tile the staged-LayerNorm modes run for a requested cfg");
+  m.def("gemm_tile_bn", &rdb::gemm_tile_bn, "N extent of tile cfg (partial-statistics count = ceil(N / BN))");
   m.def("gemm_rowln", &rdb::gemm_rowln, py::call_guard<py::gil_scoped_release>());
   m.def("gemm_sk_bf16", &rdb::gemm_sk_bf16, py::call_guard<py::gil_scoped_release>());
   m.def("gemm_sk_workspace_size", &rdb::gemm_sk_workspace_size);
@@ -92,7 +98,7 @@ PYBIND11_MODULE(_rdb_ops, m) {
         py::arg("bp"), py::arg("B"), py::arg("S"), py::arg("H"), py::arg("hidden"), py::arg("lens"), py::arg("out"),
         py::arg("ld_out"), py::arg("scale"), py::arg("cfg"), py::arg("stream"), py::arg("colsum") = 0,
         py::arg("bias_f") = 0, py::arg("stats_out") = 0, py::arg("eps") = 0.0f, py::arg("key_ids") = 0,
-        py::arg("pad") = 0, py::call_guard<py::gil_scoped_release>());
+        py::arg("pad") = 0, py::arg("a_stats") = 0, py::arg("a_ld") = 0, py::arg("a_parts") = 0, py::call_guard<py::gil_scoped_release>());
   m.def("softmax_topk", &rdb::softmax_topk, py::call_guard<py::gil_scoped_release>());
   m.def("rope", &rdb::rope, py::call_guard<py::gil_scoped_release>());
   m.def("gather_rows", &rdb::gather_rows, py::call_guard<py::gil_scoped_release>());

@@ -196,6 +196,14 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, char* lds, uint3
 // row panel (the tiles_n blocks sharing BM rows) reduces each row's statistics
 // through a zeroed workspace and a per-panel arrival counter (staged_ln_epilogue).
 constexpr int EPI_LNA = 1, EPI_LNR = 2, EPI_STATS = 4, EPI_SELF = 8, EPI_LNOUT = 16;
+// EPI_STG: the LayerNorm modes on the LDS-STAGED epilogue (ping-pong and 4-/8-wave
+// tiles alike) with PARTIAL statistics: a producer (STATS) stores, per row, one
+// (sum, sum of squares) per N-tile -- stats[m][tile_n] = partial over its BN
+// columns, plain stores, no atomics, nothing to zero -- and a consumer (LNA /
+// LNR) sums the row's `parts` partials.  The row statistics and the per-column
+// vectors are staged in LDS by the kernel's prologue (ln_stage), so the
+// epilogue reads them like the bias.
+constexpr int EPI_STG = 32;
 struct LnEpi {
   const float* a_stats;   // LNA: (sum, sumsq) of A's rows, row stride a_ld floats
   const float* a_colsum;  // LNA: colsum(W') [N]
@@ -209,6 +217,7 @@ struct LnEpi {
   float a_inv_d, r_inv_d, eps;
   int* panel;             // LNOUT: zeroed arrival counters, one per row panel (tiles_m)
   int* err;               // LNOUT: set to 1 if a panel wait timed out (never hangs)
+  int a_parts, r_parts;   // STG: partials per row in a_stats / r_stats (row stride a_ld / r_ld floats)
 };
 
 // (sum, sum of squares) of the 8 elements of an MFMA fragment, accumulated with
@@ -234,6 +243,69 @@ __device__ __forceinline__ void frag_stats(const F8& f, float& s1, float& s2) {
 __device__ __forceinline__ void ln_row_stats(float2 v, float inv_d, float eps, float& mu, float& rstd) {
   mu = v.x * inv_d;
   rstd = rsqrtf(fmaxf(v.y * inv_d - mu * mu, 0.f) + eps);
+}
+
+// LDS regions of the staged LayerNorm epilogues (EPI_STG), after the staging
+// buffers and the bias: per tile row (mean, rstd) of A (LNA) or of the
+// residual (LNR); two f32 column vectors (LNA: colsum(W'), folded bias; LNR:
+// gamma, beta); per tile row the (sum, sum of squares) accumulator of STATS.
+template <int BM, int BN>
+struct LnLds {
+  static constexpr int ROWS = 0, COLA = BM * 8, COLB = COLA + BN * 4, RACC = COLB + BN * 4, BYTES = RACC + BM * 8;
+};
+
+// Kernel prologue of the EPI_STG modes (before the first LDS-DMA, like the bias
+// staging: an ordinary load behind an in-flight DMA would drain it): fills
+// the LnLds regions at `base`; visible after the prologue barrier.
+template <typename T, int EPI, int BM, int BN, int NT>
+__device__ __forceinline__ void ln_stage(char* base, const LnEpi& ln, int m0, int n0, int M, int N) {
+  constexpr bool LNA = (EPI & EPI_LNA) != 0, LNR = (EPI & EPI_LNR) != 0, OST = (EPI & EPI_STATS) != 0;
+  typedef LnLds<BM, BN> L;
+  const int tid = threadIdx.x;
+  if constexpr (LNA || LNR) {
+    const float* st = LNA ? ln.a_stats : ln.r_stats;
+    const int ld = LNA ? ln.a_ld : ln.r_ld, parts = LNA ? ln.a_parts : ln.r_parts;
+    const float inv_d = LNA ? ln.a_inv_d : ln.r_inv_d;
+    for (int r = tid; r < BM; r += NT) {
+      const int m = m0 + r < M ? m0 + r : M - 1;
+      const float* row = st + (size_t)m * ld;
+      float s1 = 0.f, s2 = 0.f;
+      for (int p = 0; p < parts; ++p) {
+        const float2 v = *reinterpret_cast<const float2*>(row + 2 * p);
+        s1 += v.x;
+        s2 += v.y;
+      }
+      float mu, rs;
+      ln_row_stats(float2{s1, s2}, inv_d, ln.eps, mu, rs);
+      reinterpret_cast<float2*>(base + L::ROWS)[r] = float2{mu, rs};
+    }
+    for (int c = tid; c < BN; c += NT) {
+      const int n = n0 + c < N ? n0 + c : N - 1;
+      float a, b;
+      if constexpr (LNA) {
+        a = ln.a_colsum[n];
+        b = ln.a_bias[n];
+      } else {
+        a = (float)static_cast<const T*>(ln.r_g)[n];
+        b = (float)static_cast<const T*>(ln.r_b)[n];
+      }
+      reinterpret_cast<float*>(base + L::COLA)[c] = a;
+      reinterpret_cast<float*>(base + L::COLB)[c] = b;
+    }
+  }
+  if constexpr (OST)
+    for (int r = tid; r < BM; r += NT) reinterpret_cast<float2*>(base + L::RACC)[r] = float2{0.f, 0.f};
+}
+
+// Epilogue end of EPI_STG | EPI_STATS: each tile row's partial (sum, sum of
+// squares) of the values as STORED goes to o_stats[m][tile_n] (plain stores).
+template <int BM, int BN, int NT>
+__device__ __forceinline__ void ln_store_partials(const char* base, const LnEpi& ln, int m0, int M, int tile_n) {
+  typedef LnLds<BM, BN> L;
+  for (int r = threadIdx.x; r < BM; r += NT)
+    if (m0 + r < M)
+      *reinterpret_cast<float2*>(ln.o_stats + (size_t)(m0 + r) * ln.o_ld + 2 * tile_n) =
+          reinterpret_cast<const float2*>(base + L::RACC)[r];
 }
 
 // ---- LDS-staged, row-coalesced epilogue ----------------------------------------
@@ -279,13 +351,25 @@ struct StagedEpi16 {
 
 // BIAS_LDS >= 0: the tile's bias was staged (f32) at smem + BIAS_LDS by the
 // kernel's prologue, so no bias registers stay live across the epilogue.
+// EPI (EPI_STG modes only) / LN_LDS: the LayerNorm epilogues, their operands
+// staged by ln_stage at smem + LN_LDS (LnLds layout):
+//   EPI_LNA   y = act(rstd[m] (alpha acc - mean[m] colsum[n]) + bias'[n])   (16-bit staging)
+//   EPI_LNR   the residual is added as LayerNorm(R) (normalised on load)     (f32 staging)
+//   EPI_STATS each tile row's (sum, sum of squares) of the stored values -> o_stats[m][tile_n]
 template <typename T, typename OutT, int BM, int BN, int SMEM_BYTES, int NT, int TM, int TN, bool HAS_BIAS,
-          bool HAS_RES, typename ActF, int BIAS_LDS = -1>
+          bool HAS_RES, typename ActF, int BIAS_LDS = -1, int EPI = 0, int LN_LDS = -1>
 __device__ __forceinline__ void staged_epilogue(char* smem, const f32x4 (&acc)[TN][TM], int row_base, int col_base,
                                                 int m0, int n0, int M, int N, OutT* __restrict__ C, int ldc,
                                                 const T* __restrict__ bias, const T* __restrict__ R, int ldr,
-                                                float alpha, ActF actf) {
+                                                float alpha, ActF actf, const LnEpi* ln = nullptr, int tile_n = 0) {
   typedef StagedEpi<BM, BN, SMEM_BYTES> E;
+  constexpr bool SLNA = (EPI & EPI_STG) && (EPI & EPI_LNA), SLNR = (EPI & EPI_STG) && (EPI & EPI_LNR);
+  constexpr bool SOST = (EPI & EPI_STG) && (EPI & EPI_STATS);
+  static_assert(!(EPI & EPI_STG) || LN_LDS >= 0, "staged LN modes need their LDS operands");
+  static_assert(!SLNA || (!HAS_RES && !HAS_BIAS && !SOST), "staged LNA: no residual, bias folded, no stats out");
+  static_assert(!SLNR || HAS_RES, "staged LNR normalises the residual");
+  typedef LnLds<BM, BN> LL;
+  const char* lnb = smem + (LN_LDS >= 0 ? LN_LDS : 0);
   const int tid = threadIdx.x, lane = tid & 63;
   const int fr = lane & 15, fg = lane >> 4;
   // bias in the fragment layout (TN x 8 B per lane), fetched once for all chunks
@@ -308,7 +392,7 @@ __device__ __forceinline__ void staged_epilogue(char* smem, const f32x4 (&acc)[T
 #ifdef RDB_EPI_F32_STAGING
   constexpr bool kStage16 = false;   // A/B build: the f32-staged epilogue for every GEMM
 #else
-  constexpr bool kStage16 = !HAS_RES && sizeof(OutT) == 2;
+  constexpr bool kStage16 = !HAS_RES && sizeof(OutT) == 2 && !SOST;
 #endif
   if constexpr (kStage16) {
     // No residual: bias + activation run once on the accumulator registers,
@@ -322,10 +406,15 @@ __device__ __forceinline__ void staged_epilogue(char* smem, const f32x4 (&acc)[T
     // 256x128 FFN-up tile, 244 on 256x256.)  A fragment's 16 rows never
     // straddle a chunk (RC % 16 == 0), so the chunk test is wave-uniform; with
     // several chunks only the waves owning the chunk's rows compute in it.
-    auto park = [&](int i, int j, int rt) {
+    auto park = [&](int i, int j, int rt, int trow) {
       const int nt = col_base + i * 16 + fg * 4;
       f32x4 v = acc[i][j] * alpha;
-      if constexpr (BREG) {
+      if constexpr (SLNA) {
+        const float2 st = reinterpret_cast<const float2*>(lnb + LL::ROWS)[trow];
+        const f32x4 cs = *reinterpret_cast<const f32x4*>(lnb + LL::COLA + nt * 4);
+        const f32x4 bb = *reinterpret_cast<const f32x4*>(lnb + LL::COLB + nt * 4);
+        v = (v - st.x * cs) * st.y + bb;
+      } else if constexpr (BREG) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) v[q] += bv[i][q];
       } else if constexpr (HAS_BIAS) {
@@ -342,7 +431,7 @@ __device__ __forceinline__ void staged_epilogue(char* smem, const f32x4 (&acc)[T
         if (rt >= 0 && rt < E16::RC) {
 #pragma unroll
           for (int i = 0; i < TN; ++i) {
-            park(i, j, rt);
+            park(i, j, rt, row_base + j * 16 + fr);
             // keep the scheduler from interleaving every fragment's activation
             // (the no-bias variants spilled 51..245 VGPRs without it)
             __builtin_amdgcn_sched_barrier(0);
@@ -369,6 +458,44 @@ __device__ __forceinline__ void staged_epilogue(char* smem, const f32x4 (&acc)[T
   // MI355X (bench/gemm_probe.py --res): FFN-down 4096x768x3072 on the 256x128
   // ping-pong tile 42.2 -> 40.9 us (40.1 without a residual); the 4-wave
   // 128x96 o-proj got slower (11.6 -> 12.0 us), so 4-wave tiles keep the loop.
+  // phase-2 finish of one 8-column vector of tile row trow: + residual (LNR:
+  // normalised on load), activation, 16-B store; STATS: row sums into LDS
+  auto finish = [&](float (&x)[8], const u32x4& rraw, int trow, int vcol, int m, int n) {
+    if constexpr (HAS_RES) {
+      const T* e = reinterpret_cast<const T*>(&rraw);
+      if constexpr (SLNR) {
+        const float2 st = reinterpret_cast<const float2*>(lnb + LL::ROWS)[trow];
+        const f32x4* g = reinterpret_cast<const f32x4*>(lnb + LL::COLA + (n - n0) * 4);
+        const f32x4* be = reinterpret_cast<const f32x4*>(lnb + LL::COLB + (n - n0) * 4);
+        const f32x4 g0 = g[0], g1 = g[1], b0 = be[0], b1 = be[1];
+        const float gg[8] = {g0[0], g0[1], g0[2], g0[3], g1[0], g1[1], g1[2], g1[3]};
+        const float bb[8] = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
+#pragma unroll
+        for (int q = 0; q < 8; ++q) x[q] += ((float)e[q] - st.x) * st.y * gg[q] + bb[q];
+      } else {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) x[q] += (float)e[q];
+      }
+    }
+    OutT o[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) o[q] = (OutT)actf(x[q]);
+    *reinterpret_cast<u32x4*>(C + (size_t)m * ldc + n) = *reinterpret_cast<const u32x4*>(o);
+    if constexpr (SOST) {
+      // statistics of the values as STORED (what a LayerNorm reading C would see)
+      float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const float y = (float)o[q];
+        s1 += y;
+        s2 += y * y;
+      }
+      float2* racc = reinterpret_cast<float2*>(const_cast<char*>(lnb) + LL::RACC);
+      atomicAdd(&racc[trow].x, s1);
+      atomicAdd(&racc[trow].y, s2);
+    }
+    (void)vcol;
+  };
   constexpr int NVEC = E::RC * E::NV;
   constexpr int PER = (NVEC + NT - 1) / NT;
 #ifdef RDB_EPI_NO_RES_PREFETCH
@@ -425,13 +552,7 @@ __device__ __forceinline__ void staged_epilogue(char* smem, const f32x4 (&acc)[T
           const f32x4 a = *reinterpret_cast<const f32x4*>(smem + r * E::ROWB + vcol * 32);
           const f32x4 b = *reinterpret_cast<const f32x4*>(smem + r * E::ROWB + vcol * 32 + 16);
           float x[8] = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
-          const T* e = reinterpret_cast<const T*>(&rpre[u]);
-#pragma unroll
-          for (int q = 0; q < 8; ++q) x[q] += (float)e[q];
-          OutT o[8];
-#pragma unroll
-          for (int q = 0; q < 8; ++q) o[q] = (OutT)actf(x[q]);
-          *reinterpret_cast<u32x4*>(C + (size_t)m * ldc + n) = *reinterpret_cast<const u32x4*>(o);
+          finish(x, rpre[u], c * E::RC + r, vcol, m, n);
         }
       }
       __syncthreads();
@@ -445,24 +566,17 @@ __device__ __forceinline__ void staged_epilogue(char* smem, const f32x4 (&acc)[T
       const int r = idx / E::NV, vcol = idx - r * E::NV;
       const int m = m0 + c * E::RC + r, n = n0 + vcol * 8;
       if (m < M && n < N) {
-        u32x4 rraw;
+        u32x4 rraw = {0u, 0u, 0u, 0u};
         if constexpr (HAS_RES) rraw = *reinterpret_cast<const u32x4*>(R + (size_t)m * ldr + n);
         const f32x4 a = *reinterpret_cast<const f32x4*>(smem + r * E::ROWB + vcol * 32);
         const f32x4 b = *reinterpret_cast<const f32x4*>(smem + r * E::ROWB + vcol * 32 + 16);
         float x[8] = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
-        if constexpr (HAS_RES) {
-          const T* e = reinterpret_cast<const T*>(&rraw);
-#pragma unroll
-          for (int q = 0; q < 8; ++q) x[q] += (float)e[q];
-        }
-        OutT o[8];
-#pragma unroll
-        for (int q = 0; q < 8; ++q) o[q] = (OutT)actf(x[q]);
-        *reinterpret_cast<u32x4*>(C + (size_t)m * ldc + n) = *reinterpret_cast<const u32x4*>(o);
+        finish(x, rraw, c * E::RC + r, vcol, m, n);
       }
     }
     __syncthreads();
   }
+  if constexpr (SOST) ln_store_partials<BM, BN, NT>(lnb, *ln, m0, M, tile_n);
 }
 
 // ---- GEMM + residual + LayerNorm epilogue (EPI_LNOUT) ---------------------------
@@ -630,7 +744,11 @@ __global__ void __launch_bounds__(64 * NW, NW == 4 ? 2 : 1)
 mfma_gemm_kernel(typename LoaderT<T, 1>::Params ap, const T* __restrict__ W, int ldw,
                  OutT* __restrict__ C, int ldc, const T* __restrict__ bias,
                  const T* __restrict__ R, int ldr, int M, int N, int K, float alpha, int act, LnEpi ln) {
-  constexpr bool LNA = (EPI & EPI_LNA) != 0, LNR = (EPI & EPI_LNR) != 0, OST = (EPI & EPI_STATS) != 0;
+  // STG: the staged-epilogue LayerNorm modes (operands in LDS, partial stats);
+  // the other flags are the direct-epilogue (legacy) modes
+  constexpr bool STG = (EPI & EPI_STG) != 0;
+  constexpr bool LNA = !STG && (EPI & EPI_LNA) != 0, LNR = !STG && (EPI & EPI_LNR) != 0;
+  constexpr bool OST = !STG && (EPI & EPI_STATS) != 0;
   constexpr bool SELF = (EPI & EPI_SELF) != 0;
   constexpr bool LNOUT = (EPI & EPI_LNOUT) != 0;
   static_assert(!SELF || (LNA && !OST), "SELF computes LNA's statistics; it writes o_stats itself");
@@ -653,7 +771,8 @@ mfma_gemm_kernel(typename LoaderT<T, 1>::Params ap, const T* __restrict__ W, int
   constexpr int kStages = (3 * kStage <= (NW == 4 ? 80 : 160) * 1024) ? 3 : 2;
   typedef typename MfmaOp<T>::frag frag;
 
-  __shared__ __attribute__((aligned(16))) char smem[kStages * kStage];
+  constexpr int LN_OFF = kStages * kStage;
+  __shared__ __attribute__((aligned(16))) char smem[LN_OFF + (STG ? LnLds<BM, BN>::BYTES : 0)];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -752,6 +871,7 @@ mfma_gemm_kernel(typename LoaderT<T, 1>::Params ap, const T* __restrict__ W, int
     }
   }
 
+  if constexpr (STG) ln_stage<T, EPI, BM, BN, NT>(smem + LN_OFF, ln, m0, n0, M, N);   // before the first DMA
   const int nk = (K + BK - 1) / BK;
   if constexpr (kStages == 2) {
     // Two LDS stages: the DMA of tile k+1 runs under the MFMAs of tile k; the
@@ -813,12 +933,14 @@ mfma_gemm_kernel(typename LoaderT<T, 1>::Params ap, const T* __restrict__ W, int
     return;
   }
   // ---- LDS-staged coalesced epilogue (plain modes; LN / SwiGLU keep the direct one) ----
-  if constexpr (EPI == 0 && sizeof(OutT) == 2) {
-    if (act != ACT_SWIGLU && staged_epilogue_ok<T, OutT, HAS_RES>(N, C, ldc, bias, R, ldr)) {
+  if constexpr ((EPI == 0 || STG) && sizeof(OutT) == 2) {
+    // (STG launches are host-checked for the staged epilogue's requirements)
+    if (STG || (act != ACT_SWIGLU && staged_epilogue_ok<T, OutT, HAS_RES>(N, C, ldc, bias, R, ldr))) {
       constexpr int SB = kStages * kStage;
       auto go = [&](auto actf) {
-        staged_epilogue<T, OutT, BM, BN, SB, NT, TM, TN, HAS_BIAS, HAS_RES>(smem, acc, wm * WM, wn * WN, m0, n0, M, N,
-                                                                            C, ldc, bias, R, ldr, alpha, actf);
+        staged_epilogue<T, OutT, BM, BN, SB, NT, TM, TN, HAS_BIAS, HAS_RES, decltype(actf), -1, EPI,
+                        STG ? LN_OFF : -1>(smem, acc, wm * WM, wn * WN, m0, n0, M, N, C, ldc, bias, R, ldr, alpha,
+                                           actf, &ln, tile_n);
       };
       switch (act) {
         case ACT_GELU: go([](float x) { return apply_act<ACT_GELU>(x); }); break;
@@ -1038,6 +1160,15 @@ inline bool ln_out_tile_ok(int cfg) {
   return bm * (bn * 4 + 16) + bm * 8 <= stages * stage;
 }
 
+// Tiles the staged-LayerNorm modes run (EPI_STG; launch_mfma_gemm_t): a
+// producer's partial-statistics count per row is ceil(N / BN) of its tile.
+constexpr int kStgTiles[] = {0, 9, 10, 12, 19, 21, 23, 24};
+inline int stg_tile_cfg(int cfg) {
+  for (int c : kStgTiles)
+    if (c == cfg) return cfg;
+  return 10;
+}
+
 // Heuristic: minimise (rounds of blocks over 256 CUs) x (tile work / tile efficiency).
 constexpr int kNumTiles4 = 13;  // tiles 0..12 are 4-wave (every loader); 13.. are 8-wave (dense only)
 inline int pick_tile_cfg(int M, int N, bool dense) {
@@ -1077,6 +1208,31 @@ void launch_mfma_gemm_t(const P& ap, const T* W, int ldw, OutT* C, int ldc, cons
   if constexpr (std::is_same<OutT, float>::value) {
     // f32 output is only used by small heads: one tile shape
     launch_one<T, OutT, LoaderT, HB, HR, 64, 64>(ap, W, ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act, s);
+  } else if constexpr ((EPI & EPI_STG) != 0) {
+    // staged-LayerNorm modes: the 4-wave tiles of the o-projection class and the
+    // ping-pong tiles of FFN-up / FFN-down (a subset keeps the build small);
+    // any other cfg runs 128x96
+    const T* A = static_cast<const T*>(ap.A);
+    switch (cfg) {
+      RDB_TILE(0, 128, 128, 2, 4)
+      RDB_TILE(9, 64, 96, 2, 4)
+      RDB_TILE(12, 128, 48, 4, 4)
+      case 19: launch_gemm_pp_ln<T, OutT, 8, 256, 128, 2, 2, 3, 64, 2, EPI>(A, ap.lda, W, ldw, C, ldc, bias, R, ldr, M,
+                                                                            N, K, alpha, act, s, ln);
+        return;
+      case 21: launch_gemm_pp_ln<T, OutT, 8, 128, 256, 1, 4, 3, 64, 2, EPI>(A, ap.lda, W, ldw, C, ldc, bias, R, ldr, M,
+                                                                            N, K, alpha, act, s, ln);
+        return;
+      case 23: launch_gemm_pp_ln<T, OutT, 8, 256, 128, 2, 2, 3, 32, 4, EPI>(A, ap.lda, W, ldw, C, ldc, bias, R, ldr, M,
+                                                                            N, K, alpha, act, s, ln);
+        return;
+      case 24: launch_gemm_pp_ln<T, OutT, 8, 256, 192, 2, 2, 3, 32, 2, EPI>(A, ap.lda, W, ldw, C, ldc, bias, R, ldr, M,
+                                                                            N, K, alpha, act, s, ln);
+        return;
+      default: break;
+    }
+    launch_one<T, OutT, LoaderT, HB, HR, 128, 96, 2, 4, EPI>(ap, W, ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act, s,
+                                                            ln);
   } else {
     // the ping-pong tiles (19..) take plain staged epilogues only: deferred-LN modes,
     // SwiGLU and unaligned / N % 8 != 0 outputs run the 8-wave 256x192 tile instead

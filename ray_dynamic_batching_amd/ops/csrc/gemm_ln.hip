@@ -25,7 +25,7 @@ void gemm_tn_ln(uintptr_t A, int lda, uintptr_t W, int ldw, uintptr_t C, int ldc
                 int ldr, int M, int N, int K, float alpha, int act, int mode, uintptr_t a_stats, int a_ld,
                 uintptr_t a_colsum, uintptr_t a_bias, uintptr_t r_stats, int r_ld, uintptr_t r_g, uintptr_t r_b,
                 uintptr_t o_stats, int o_ld, float a_inv_d, float r_inv_d, float eps, uintptr_t stream, int cfg,
-                uintptr_t panel, uintptr_t err) {
+                uintptr_t panel, uintptr_t err, int a_parts, int r_parts) {
   if (K % 8 != 0 || lda % 8 != 0 || ldw % 8 != 0) throw std::invalid_argument("gemm_tn_ln: K/lda/ldw % 8");
   if ((A | W) & 15) throw std::invalid_argument("gemm_tn_ln: A/W must be 16-byte aligned");
   if (N % 4 != 0 || ldc % 4 != 0) throw std::invalid_argument("gemm_tn_ln: N and ldc must be multiples of 4");
@@ -44,6 +44,8 @@ void gemm_tn_ln(uintptr_t A, int lda, uintptr_t W, int ldw, uintptr_t C, int ldc
   ln.a_inv_d = a_inv_d; ln.r_inv_d = r_inv_d; ln.eps = eps;
   ln.panel = reinterpret_cast<int*>(panel);
   ln.err = reinterpret_cast<int*>(err);
+  ln.a_parts = a_parts;
+  ln.r_parts = r_parts;
   DenseParams p{reinterpret_cast<const void*>(A), lda, M, K};
   auto w = reinterpret_cast<const bf16*>(W);
   auto b = reinterpret_cast<const bf16*>(bias);
@@ -53,6 +55,18 @@ void gemm_tn_ln(uintptr_t A, int lda, uintptr_t W, int ldw, uintptr_t C, int ldc
   auto need = [](bool ok, const char* what) {
     if (!ok) throw std::invalid_argument(what);
   };
+  if (mode & EPI_STG) {
+    // the staged epilogue's requirements (16-B rows, no SwiGLU) and the partial layouts
+    cfg = stg_tile_cfg(cfg);
+    need(N % 8 == 0 && ldc % 8 == 0 && (C & 15) == 0 && (!R || (ldr % 8 == 0 && (R & 15) == 0)),
+         "gemm_tn_ln: staged LN modes need N, ldc, ldr % 8 and 16-byte aligned C / residual");
+    need((a_stats & 7) == 0 && (r_stats & 7) == 0 && (o_stats & 7) == 0 && a_parts >= 1 && r_parts >= 1,
+         "gemm_tn_ln: staged LN statistics: 8-byte aligned, parts >= 1");
+    if (mode & EPI_STATS) {
+      const int parts = (N + kTileBN[cfg] - 1) / kTileBN[cfg];
+      need(o_ld >= 2 * parts, "gemm_tn_ln: out statistics row stride < 2 x N-tiles of the tile");
+    }
+  }
   switch (mode) {
     case EPI_LNA:
       need(a_stats && a_colsum && a_bias && !bias && !R, "gemm_tn_ln: LNA needs a_stats/a_colsum/a_bias, no bias/R");
@@ -100,11 +114,35 @@ void gemm_tn_ln(uintptr_t A, int lda, uintptr_t W, int ldw, uintptr_t C, int ldc
       launch_mfma_gemm_t<bf16, bf16, DenseLoader, false, false, EPI_LNA | EPI_SELF>(p, w, ldw, c, ldc, b, r, ldr, M, N,
                                                                                     K, alpha, act, s, cfg, ln);
       break;
+    case EPI_STG | EPI_LNA:
+      need(a_stats && a_colsum && a_bias && !bias && !R, "gemm_tn_ln: STG|LNA needs a_stats/a_colsum/a_bias, no bias/R");
+      launch_mfma_gemm_t<bf16, bf16, DenseLoader, false, false, EPI_STG | EPI_LNA>(p, w, ldw, c, ldc, b, r, ldr, M, N,
+                                                                                   K, alpha, act, s, cfg, ln);
+      break;
+    case EPI_STG | EPI_STATS:
+      need(o_stats && bias && R, "gemm_tn_ln: STG|STATS needs o_stats, bias and R");
+      launch_mfma_gemm_t<bf16, bf16, DenseLoader, true, true, EPI_STG | EPI_STATS>(p, w, ldw, c, ldc, b, r, ldr, M, N,
+                                                                                   K, alpha, act, s, cfg, ln);
+      break;
+    case EPI_STG | EPI_LNR | EPI_STATS:
+      need(o_stats && bias && R && r_stats && r_g && r_b, "gemm_tn_ln: STG|LNR|STATS needs o_stats, bias, R, r_*");
+      launch_mfma_gemm_t<bf16, bf16, DenseLoader, true, true, EPI_STG | EPI_LNR | EPI_STATS>(
+          p, w, ldw, c, ldc, b, r, ldr, M, N, K, alpha, act, s, cfg, ln);
+      break;
+    case EPI_STG | EPI_LNR:
+      need(bias && R && r_stats && r_g && r_b, "gemm_tn_ln: STG|LNR needs bias, R, r_*");
+      launch_mfma_gemm_t<bf16, bf16, DenseLoader, true, true, EPI_STG | EPI_LNR>(p, w, ldw, c, ldc, b, r, ldr, M, N,
+                                                                                 K, alpha, act, s, cfg, ln);
+      break;
     default:
       throw std::invalid_argument(
-          "gemm_tn_ln: mode must be LNA (1), STATS (4), LNR|STATS (6), LNR (2), LNA|SELF (9) or LNOUT (16)");
+          "gemm_tn_ln: mode must be LNA (1), STATS (4), LNR|STATS (6), LNR (2), LNA|SELF (9), LNOUT (16) or a "
+          "staged mode STG (32) | LNA, STATS, LNR|STATS, LNR");
   }
   RDB_HIP_CHECK(hipGetLastError());
 }
+
+int gemm_stg_cfg(int cfg) { return stg_tile_cfg(cfg); }
+int gemm_tile_bn(int cfg) { return cfg >= 0 && cfg < kNumTiles ? kTileBN[cfg] : -1; }
 
 }  // namespace rdb

@@ -82,12 +82,14 @@ struct PPGeom {
 // OCC = waves per SIMD the register budget must allow: 2 = one 8-wave block
 // per CU (<= 256 VGPRs), 4 = two co-resident blocks (<= 128 VGPRs; the tile's
 // LDS must then fit twice in 160 KiB)
+// EPI: 0 or an EPI_STG LayerNorm mode (gemm_core.h): its operands are staged in
+// LDS after the bias by the prologue and applied by the staged epilogue.
 template <typename T, typename OutT, int NW, int BM, int BN, int GM, int GN, int STAGES, bool HAS_BIAS, bool HAS_RES,
-          int BK_ = 64, int OCC = 2>
+          int BK_ = 64, int OCC = 2, int EPI = 0>
 __global__ void __launch_bounds__(64 * NW, OCC)
 gemm_pp_kernel(const T* __restrict__ A, int lda, const T* __restrict__ W, int ldw, OutT* __restrict__ C, int ldc,
                const T* __restrict__ bias, const T* __restrict__ R, int ldr, int M, int N, int K, float alpha,
-               int act) {
+               int act, LnEpi ln) {
   typedef PPGeom<NW, BM, BN, BK_> G;
   constexpr int BK = G::BK;
   constexpr int KS = BK / 32;                // MFMA k-steps per tile
@@ -103,7 +105,10 @@ gemm_pp_kernel(const T* __restrict__ A, int lda, const T* __restrict__ W, int ld
 
   // staging buffers, then the tile's bias as f32 (read by the epilogue)
   constexpr int BIAS_OFF = STAGES * G::STAGE_BYTES;
-  __shared__ __attribute__((aligned(16))) char smem[BIAS_OFF + (HAS_BIAS ? BN * 4 : 0)];
+  constexpr int LN_OFF = BIAS_OFF + (HAS_BIAS ? BN * 4 : 0);
+  constexpr int LN_BYTES = EPI ? LnLds<BM, BN>::BYTES : 0;
+  static_assert(EPI == 0 || (EPI & EPI_STG), "ping-pong tiles: plain or staged-LN epilogues");
+  __shared__ __attribute__((aligned(16))) char smem[LN_OFF + LN_BYTES];
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int grp = wid / GW, gw = wid % GW;
@@ -213,6 +218,7 @@ gemm_pp_kernel(const T* __restrict__ A, int lda, const T* __restrict__ W, int ld
       *reinterpret_cast<f32x4*>(smem + BIAS_OFF + q * 16) = f32x4{(float)e[0], (float)e[1], (float)e[2], (float)e[3]};
     }
   }
+  if constexpr (EPI != 0) ln_stage<T, EPI, BM, BN, G::NT>(smem + LN_OFF, ln, m0, n0, M, N);
   // prologue: tiles 0 .. STAGES-2 in flight, tile 0 retired and visible
 #pragma unroll
   for (int s = 0; s < STAGES - 1; ++s)
@@ -252,8 +258,9 @@ gemm_pp_kernel(const T* __restrict__ A, int lda, const T* __restrict__ W, int ld
   static_assert(sizeof(OutT) == 2, "ping-pong GEMM stores 16-bit outputs");
   constexpr int SB = STAGES * G::STAGE_BYTES;
   auto go = [&](auto actf) {
-    staged_epilogue<T, OutT, BM, BN, SB, G::NT, TM, TN, HAS_BIAS, HAS_RES, decltype(actf), BIAS_OFF>(
-        smem, acc, grp * GBM + wm * WM, wn * WN, m0, n0, M, N, C, ldc, bias, R, ldr, alpha, actf);
+    staged_epilogue<T, OutT, BM, BN, SB, G::NT, TM, TN, HAS_BIAS, HAS_RES, decltype(actf), BIAS_OFF, EPI,
+                    EPI ? LN_OFF : -1>(smem, acc, grp * GBM + wm * WM, wn * WN, m0, n0, M, N, C, ldc, bias, R, ldr,
+                                       alpha, actf, &ln, tile_n);
   };
   switch (act) {
     case ACT_GELU: go([](float x) { return apply_act<ACT_GELU>(x); }); break;
@@ -285,18 +292,30 @@ void launch_gemm_pp(const T* A, int lda, const T* W, int ldw, OutT* C, int ldc, 
                     int M, int N, int K, float alpha, int act, hipStream_t s) {
   const int nwg = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
   const dim3 grid(nwg), block(64 * NW);
+  const LnEpi ln{};
   if (bias && R)
     hipLaunchKernelGGL((gemm_pp_kernel<T, OutT, NW, BM, BN, GM, GN, STAGES, true, true, BK, OCC>), grid, block, 0, s, A, lda, W,
-                       ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act);
+                       ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act, ln);
   else if (bias)
     hipLaunchKernelGGL((gemm_pp_kernel<T, OutT, NW, BM, BN, GM, GN, STAGES, true, false, BK, OCC>), grid, block, 0, s, A, lda, W,
-                       ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act);
+                       ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act, ln);
   else if (R)
     hipLaunchKernelGGL((gemm_pp_kernel<T, OutT, NW, BM, BN, GM, GN, STAGES, false, true, BK, OCC>), grid, block, 0, s, A, lda, W,
-                       ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act);
+                       ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act, ln);
   else
     hipLaunchKernelGGL((gemm_pp_kernel<T, OutT, NW, BM, BN, GM, GN, STAGES, false, false, BK, OCC>), grid, block, 0, s, A, lda,
-                       W, ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act);
+                       W, ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act, ln);
+}
+
+// The staged-LayerNorm modes (EPI_STG | ...) on a ping-pong tile.  LNA: no bias
+// (folded), no residual; STATS with or without LNR: bias + residual.
+template <typename T, typename OutT, int NW, int BM, int BN, int GM, int GN, int STAGES, int BK, int OCC, int EPI>
+void launch_gemm_pp_ln(const T* A, int lda, const T* W, int ldw, OutT* C, int ldc, const T* bias, const T* R, int ldr,
+                       int M, int N, int K, float alpha, int act, hipStream_t s, const LnEpi& ln) {
+  const int nwg = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  constexpr bool RES = (EPI & (EPI_LNR | EPI_STATS)) != 0;
+  hipLaunchKernelGGL((gemm_pp_kernel<T, OutT, NW, BM, BN, GM, GN, STAGES, RES, RES, BK, OCC, EPI>), dim3(nwg),
+                     dim3(64 * NW), 0, s, A, lda, W, ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act, ln);
 }
 
 }  // namespace rdb

@@ -41,6 +41,8 @@ struct QkvLn {
   const float* bias_f;   // [H*192]
   float* stats_out;      // [B*S, 2] (sum, sum of squares) of X's rows, row stride 2; may be null
   float inv_d, eps;
+  const float* a_stats;  // LNA == 2: X's row statistics as partials [B*S][parts][2] (row stride a_ld floats)
+  int a_ld, a_parts;
 };
 
 // SEQ = 2 (S == 128 only): one block = TWO consecutive sequences of one head, a
@@ -50,7 +52,11 @@ struct QkvLn {
 // attention of the first sequence, 4..7 of the second.
 // OCC (> 0) overrides the waves-per-SIMD register budget (4 = two co-resident
 // 8-wave blocks per CU).
-template <typename T, int NW, int STAGES, bool LNA, int WGM_ = (NW == 8 ? 4 : 2), int SEQ = 1, int OCC = 0>
+// LNA: 0 = plain; 1 = folded LayerNorm, X's row statistics computed in the main
+// loop (frag_stats); 2 = folded LayerNorm, statistics given as the producer's
+// per-N-tile partials (ln.a_stats; gemm_core.h EPI_STG | EPI_STATS) -- no
+// statistics work in the main loop.
+template <typename T, int NW, int STAGES, int LNA, int WGM_ = (NW == 8 ? 4 : 2), int SEQ = 1, int OCC = 0>
 __global__ void __launch_bounds__(64 * NW, OCC > 0 ? OCC : (NW == 8 && (STAGES == 3 || SEQ == 2) ? 1 : 2))
 qkv_attn_kernel(DenseParams ap, const T* __restrict__ W, const T* __restrict__ bias, int S, int H,
                 const int* __restrict__ lens, T* __restrict__ out, int ld_out, float scale_log2e, QkvLn ln,
@@ -115,6 +121,30 @@ qkv_attn_kernel(DenseParams ap, const T* __restrict__ W, const T* __restrict__ b
   float st1[LNA ? TM : 1], st2[LNA ? TM : 1];
 #pragma unroll
   for (int j = 0; j < (LNA ? TM : 1); ++j) st1[j] = st2[j] = 0.f;
+  // LNA == 2: this lane's rows' partials, issued before the first DMA and summed
+  // behind it (the wait for them is the one the first stage needs anyway)
+  float2 xp[LNA == 2 ? TM * 8 : 1];
+  if constexpr (LNA == 2) {
+#pragma unroll
+    for (int j = 0; j < TM; ++j) {
+      const int m = m0 + wm * WM + j * 16 + fr;
+      const float* row = ln.a_stats + (size_t)(m < ap.M ? m : ap.M - 1) * ln.a_ld;
+#pragma unroll
+      for (int p = 0; p < 8; ++p)
+        xp[j * 8 + p] = p < ln.a_parts ? *reinterpret_cast<const float2*>(row + 2 * p) : float2{0.f, 0.f};
+    }
+  }
+  auto sum_partials = [&] {
+    if constexpr (LNA == 2) {
+#pragma unroll
+      for (int j = 0; j < TM; ++j)
+#pragma unroll
+        for (int p = 0; p < 8; ++p) {
+          st1[j] += xp[j * 8 + p].x;
+          st2[j] += xp[j * 8 + p].y;
+        }
+    }
+  };
   auto compute = [&](int buf) {
     const char* sa = smem + buf * kStage;
     const char* sw = sa + BM * BK * 2;
@@ -126,7 +156,7 @@ qkv_attn_kernel(DenseParams ap, const T* __restrict__ W, const T* __restrict__ b
       for (int i = 0; i < TN; ++i) wf[i] = *reinterpret_cast<const frag*>(sw + swz_off(wn * WN + i * 16 + fr, chunk));
 #pragma unroll
       for (int j = 0; j < TM; ++j) af[j] = *reinterpret_cast<const frag*>(sa + swz_off(wm * WM + j * 16 + fr, chunk));
-      if constexpr (LNA) {
+      if constexpr (LNA == 1) {
 #pragma unroll
         for (int j = 0; j < TM; ++j) frag_stats<T>(af[j], st1[j], st2[j]);   // k >= K reads as 0
       }
@@ -151,6 +181,7 @@ qkv_attn_kernel(DenseParams ap, const T* __restrict__ W, const T* __restrict__ b
   const int nk = (K + BK - 1) / BK;
   if constexpr (STAGES == 2) {
     stage(0, 0);
+    sum_partials();
     __syncthreads();
     for (int kt = 0; kt < nk; ++kt) {
       if (kt + 1 < nk) stage((kt + 1) & 1, (kt + 1) * BK);
@@ -164,6 +195,7 @@ qkv_attn_kernel(DenseParams ap, const T* __restrict__ W, const T* __restrict__ b
     static_assert(kLoads < 64, "vmcnt field");
     stage(0, 0);
     if (nk > 1) stage(1, BK);
+    sum_partials();
     int buf = 0;
     for (int kt = 0; kt < nk; ++kt) {
       if (kt + 1 < nk) __builtin_amdgcn_s_waitcnt(kWaitOne);
@@ -201,13 +233,15 @@ qkv_attn_kernel(DenseParams ap, const T* __restrict__ W, const T* __restrict__ b
 #pragma unroll
     for (int j = 0; j < TM; ++j) {
       float a = st1[j], q = st2[j];
-      a += __shfl_xor(a, 16, 64);
-      q += __shfl_xor(q, 16, 64);
-      a += __shfl_xor(a, 32, 64);
-      q += __shfl_xor(q, 32, 64);
+      if constexpr (LNA == 1) {   // the 4 lanes of a row each saw a quarter of its k
+        a += __shfl_xor(a, 16, 64);
+        q += __shfl_xor(q, 16, 64);
+        a += __shfl_xor(a, 32, 64);
+        q += __shfl_xor(q, 32, 64);
+      }
       ln_row_stats(float2{a, q}, ln.inv_d, ln.eps, mu[j], rs[j]);
       const int tok = wm * WM + j * 16 + fr;
-      if (ln.stats_out != nullptr && h == 0 && wn == 0 && fg == 0 && tok % 128 < S && m0 + tok < ap.M)
+      if (LNA == 1 && ln.stats_out != nullptr && h == 0 && wn == 0 && fg == 0 && tok % 128 < S && m0 + tok < ap.M)
         *reinterpret_cast<float2*>(ln.stats_out + (size_t)(m0 + tok) * 2) = float2{a, q};
     }
   }
@@ -350,7 +384,7 @@ qkv_attn_kernel(DenseParams ap, const T* __restrict__ W, const T* __restrict__ b
 // blocks share a CU, one block's softmax beside the other's projection MFMAs.
 constexpr int kNumQkvAttnCfgs = 5;
 
-template <typename T, bool LNA>
+template <typename T, int LNA>
 static void launch_qkv_attn(int cfg, const DenseParams& p, const T* W, const T* bias, int B, int S, int H,
                             const int* lens, T* out, int ld_out, float sl2e, const QkvLn& ln, hipStream_t s,
                             const int* kids, int pad) {
@@ -385,7 +419,8 @@ static void launch_qkv_attn(int cfg, const DenseParams& p, const T* W, const T* 
 // are f32 [H*192] (packed order), stats_out (optional) f32 [B*S, 2].
 void qkv_attn_fwd(int dtype, uintptr_t X, int ldx, uintptr_t Wp, uintptr_t bp, int B, int S, int H, int hidden,
                   uintptr_t lens, uintptr_t out, int ld_out, float scale, int cfg, uintptr_t stream,
-                  uintptr_t colsum, uintptr_t bias_f, uintptr_t stats_out, float eps, uintptr_t key_ids, int pad) {
+                  uintptr_t colsum, uintptr_t bias_f, uintptr_t stats_out, float eps, uintptr_t key_ids, int pad,
+                  uintptr_t a_stats, int a_ld, int a_parts) {
   if (S < 1 || S > 128) throw std::invalid_argument("qkv_attn: 1 <= S <= 128");
   if (hidden % 8 || ldx % 8 || ld_out % 4) throw std::invalid_argument("qkv_attn: hidden / ldx % 8, ld_out % 4");
   const bool lna = colsum != 0;
@@ -395,20 +430,23 @@ void qkv_attn_fwd(int dtype, uintptr_t X, int ldx, uintptr_t Wp, uintptr_t bp, i
   if (cfg == 4 && S != 128) cfg = 3;
   if (key_ids && lens) throw std::invalid_argument("qkv_attn: pass lens or key_ids, not both");
   if (key_ids & 3) throw std::invalid_argument("qkv_attn: key_ids must be int32-aligned");
+  if (a_stats && (!lna || stats_out || (a_stats & 7) || a_parts < 1 || a_parts > 8 || a_ld < 2 * a_parts))
+    throw std::invalid_argument("qkv_attn: partial statistics need the folded form, 1..8 parts, no stats_out");
   if (B <= 0 || H <= 0) return;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const DenseParams p{reinterpret_cast<const void*>(X), ldx, B * S, hidden};
   const float sl2e = scale * 1.4426950408889634f;
   const QkvLn ln{reinterpret_cast<const float*>(colsum), reinterpret_cast<const float*>(bias_f),
-                 reinterpret_cast<float*>(stats_out), 1.0f / hidden, eps};
+                 reinterpret_cast<float*>(stats_out), 1.0f / hidden, eps, reinterpret_cast<const float*>(a_stats),
+                 a_ld, a_parts};
 #define RDB_QA(T, L)                                                                                            \
   launch_qkv_attn<T, L>(cfg, p, reinterpret_cast<const T*>(Wp), reinterpret_cast<const T*>(bp), B, S, H,        \
                         reinterpret_cast<const int*>(lens), reinterpret_cast<T*>(out), ld_out, sl2e, ln, s,   \
                         reinterpret_cast<const int*>(key_ids), pad)
   if (dtype == 0) {
-    if (lna) RDB_QA(bf16, true); else RDB_QA(bf16, false);
+    if (lna && a_stats) RDB_QA(bf16, 2); else if (lna) RDB_QA(bf16, 1); else RDB_QA(bf16, 0);
   } else if (dtype == 1) {
-    if (lna) RDB_QA(f16, true); else RDB_QA(f16, false);
+    if (lna) RDB_QA(f16, 1); else RDB_QA(f16, 0);
   } else {
     throw std::invalid_argument("qkv_attn: dtype must be bf16 or f16");
   }
