@@ -961,6 +961,10 @@ def image_to_nhwc_ref(img_u8, Cp=8):
 # ---------------------------------------------------------------------------
 # Convolution family (NHWC f16)
 # ---------------------------------------------------------------------------
+# RDB_CONV1X1_GEMM=0 keeps 1x1 convolutions on the implicit-GEMM conv kernel
+_CONV1X1_GEMM = os.environ.get("RDB_CONV1X1_GEMM", "1") != "0"
+
+
 def conv2d_nhwc(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, stride: int = 1,
                 pad: int = 0, act: str = "none", residual: Optional[torch.Tensor] = None,
                 out: Optional[torch.Tensor] = None, tile_cfg: int = -1) -> torch.Tensor:
@@ -980,6 +984,13 @@ def conv2d_nhwc(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] =
     if residual is not None:
         _check(residual.shape == (N, P, Q, K) and residual.is_contiguous() and residual.dtype == torch.float16, "conv2d: bad residual")
     _check(_aligned(x) and _aligned(w), "conv2d: alignment")
+    if R == 1 and S == 1 and stride == 1 and pad == 0 and tile_cfg < 0 and _CONV1X1_GEMM and K % 8 == 0:
+        # a 1x1 / stride-1 convolution on NHWC IS the GEMM [N*H*W, C] x [K, C]^T:
+        # the dense path has the 8-wave and ping-pong tiles the implicit-GEMM
+        # loader does not (the bottleneck blocks' 1x1 convs are 2/3 of ResNet-50's convs)
+        linear(x.view(N * H * W, C), w.view(K, C), bias, act=act,
+               residual=None if residual is None else residual.view(N * P * Q, K), out=out.view(N * P * Q, K))
+        return out
     args = (x.data_ptr(), w.data_ptr(), _ptr(bias), _ptr(residual), out.data_ptr(), N, H, W, C, K, R, S,
             stride, pad, P, Q, ACT_CODE[act])
     fn = _ops().conv2d_nhwc
