@@ -91,27 +91,28 @@ class EfficientNetV2S(ImageClassifier):
         return convs, lins + ["classifier.1"]
 
     def _logits_hip(self, img):
+        ws = ops.splitk_workspace(img.device)      # split-K convolutions of this forward
         x = ops.image_to_nhwc(img, 8)
-        x = ops.conv2d_nhwc(x, *self.stem_p, stride=2, pad=1, act="silu")
+        x = ops.conv2d_nhwc(x, *self.stem_p, stride=2, pad=1, act="silu", workspace=ws)
         for blk in self.blocks:
             res = x if blk["res"] else None
             s = blk["stride"]
             if blk["kind"] == "fused":
                 if "conv" in blk:   # expand 1: conv + SiLU, residual added AFTER the activation
-                    y = ops.conv2d_nhwc(x, *blk["conv"], stride=s, pad=1, act="silu")
+                    y = ops.conv2d_nhwc(x, *blk["conv"], stride=s, pad=1, act="silu", workspace=ws)
                     x = y.add_(res) if res is not None else y
                 else:
-                    h = ops.conv2d_nhwc(x, *blk["expand"], stride=s, pad=1, act="silu")
-                    x = ops.conv2d_nhwc(h, *blk["project"], residual=res)
+                    h = ops.conv2d_nhwc(x, *blk["expand"], stride=s, pad=1, act="silu", workspace=ws)
+                    x = ops.conv2d_nhwc(h, *blk["project"], residual=res, workspace=ws)
             else:
-                h = ops.conv2d_nhwc(x, *blk["expand"], act="silu")
+                h = ops.conv2d_nhwc(x, *blk["expand"], act="silu", workspace=ws)
                 h = ops.dwconv_nhwc(h, *blk["dw_p"], stride=s, pad=1, act="silu")
                 z = ops.avgpool_nhwc(h)
                 z = ops.linear(z, *blk["se1"], act="silu")
                 z = ops.linear(z, *blk["se2"], act="sigmoid")
                 h = ops.se_scale(h, z)
-                x = ops.conv2d_nhwc(h, *blk["project"], residual=res)
-        x = ops.conv2d_nhwc(x, *self.head, act="silu")
+                x = ops.conv2d_nhwc(h, *blk["project"], residual=res, workspace=ws)
+        x = ops.conv2d_nhwc(x, *self.head, act="silu", workspace=ws)
         pooled = ops.avgpool_nhwc(x)
         return ops.linear(pooled, self.fc_w, self.fc_b, out_dtype=torch.float32)
 

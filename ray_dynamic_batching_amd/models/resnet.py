@@ -9,7 +9,8 @@ top-5 (probability, class id) as 10 float32 (softmax + top-k fused kernel --
 the Serve ResNet workload's softmax + argmax).
 
 Forward (all on gfx950 kernels, hipGraph-captured by the replica engine):
-  image_to_nhwc (normalise, C 3 -> 8) -> conv7x7/2 (+BN folded +ReLU) ->
+  image_to_s2d (normalise, 2x2 space-to-depth, C 12 -> 16) -> conv7x7/2 as a
+  4x4/1 conv on that tensor (+BN folded +ReLU) ->
   maxpool3x3/2 -> 16 bottlenecks [conv1x1+ReLU, conv3x3(/s)+ReLU,
   conv1x1 + (downsample conv) residual + ReLU fused in the epilogue] ->
   global avgpool -> FC GEMM (f32 logits) -> softmax_topk(5)
@@ -18,6 +19,7 @@ BatchNorm is folded into (W, b) at load time.
 from __future__ import annotations
 
 import math
+import os
 from typing import List
 
 import torch
@@ -55,6 +57,10 @@ class ResNet50:
         self.stem_w = torch.zeros(64, 7, 7, 8, device=self.device, dtype=dtype)   # C padded 3 -> 8
         self.stem_w[..., :3] = w
         self.stem_b = b
+        # the stem on the space-to-depth image: 4x4 / stride-1 conv, 256 reduction
+        # elements per output instead of 392 (RDB_RESNET_S2D=0: the 7x7 conv)
+        self.stem_s2d = os.environ.get("RDB_RESNET_S2D", "1") != "0"
+        self.stem_w_s2d = ops.stem_weight_s2d(self.stem_w)
         self.blocks: List[dict] = []
         cin = 64
         for width, n, stride in STAGES:
@@ -100,6 +106,7 @@ class ResNet50:
         self.stem_w.zero_()
         put(self.stem_w[..., :3], w)
         put(self.stem_b, b)
+        self.stem_w_s2d = ops.stem_weight_s2d(self.stem_w)
         bi = 0
         for si, (_, n, _) in enumerate(STAGES):
             for i in range(n):
@@ -152,15 +159,23 @@ class ResNet50:
         return self._logits_torch(img)
 
     def _logits_hip(self, img):
-        x = ops.image_to_nhwc(img, 8)
-        x = ops.conv2d_nhwc(x, self.stem_w, self.stem_b, stride=2, pad=3, act="relu")
+        # one split-K workspace per forward (its tile counters zeroed once; the
+        # convolutions of the forward run one after another on its stream)
+        ws = ops.splitk_workspace(img.device)
+        if self.stem_s2d and img.shape[1] % 2 == 0 and img.shape[2] % 2 == 0:
+            x = ops.image_to_s2d(img)
+            x = ops.conv2d_nhwc(x, self.stem_w_s2d, self.stem_b, stride=1, pad=2, act="relu",
+                                out_hw=(img.shape[1] // 2, img.shape[2] // 2), workspace=ws)
+        else:
+            x = ops.image_to_nhwc(img, 8)
+            x = ops.conv2d_nhwc(x, self.stem_w, self.stem_b, stride=2, pad=3, act="relu", workspace=ws)
         x = ops.maxpool_nhwc(x, 3, 2, 1)
         for blk in self.blocks:
             s = blk["stride"]
-            h = ops.conv2d_nhwc(x, blk["w1"], blk["b1"], act="relu")
-            h = ops.conv2d_nhwc(h, blk["w2"], blk["b2"], stride=s, pad=1, act="relu")
-            sc = ops.conv2d_nhwc(x, blk["wd"], blk["bd"], stride=s) if "wd" in blk else x
-            x = ops.conv2d_nhwc(h, blk["w3"], blk["b3"], act="relu", residual=sc)
+            h = ops.conv2d_nhwc(x, blk["w1"], blk["b1"], act="relu", workspace=ws)
+            h = ops.conv2d_nhwc(h, blk["w2"], blk["b2"], stride=s, pad=1, act="relu", workspace=ws)
+            sc = ops.conv2d_nhwc(x, blk["wd"], blk["bd"], stride=s, workspace=ws) if "wd" in blk else x
+            x = ops.conv2d_nhwc(h, blk["w3"], blk["b3"], act="relu", residual=sc, workspace=ws)
         pooled = ops.avgpool_nhwc(x)
         return ops.linear(pooled, self.fc_w, self.fc_b, out_dtype=torch.float32)
 

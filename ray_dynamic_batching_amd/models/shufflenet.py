@@ -105,26 +105,27 @@ class ShuffleNetV2(ImageClassifier):
 
     # -- HIP path: padded NHWC f16 -----------------------------------------
     def _logits_hip(self, img):
+        ws = ops.splitk_workspace(img.device)      # split-K convolutions of this forward
         x = ops.image_to_nhwc(img, 8)
-        x = ops.conv2d_nhwc(x, *self.stem_p, stride=2, pad=1, act="relu")
+        x = ops.conv2d_nhwc(x, *self.stem_p, stride=2, pad=1, act="relu", workspace=ws)
         x = ops.maxpool_nhwc(x, 3, 2, 1)
         x1 = x2 = None
         for u in self.units:
             hp = u["half_p"]
             if u["stride"] == 2:
                 a = ops.dwconv_nhwc(x, *u["dw1_p"], stride=2, pad=1)
-                a = ops.conv2d_nhwc(a, *u["pw1_p"], act="relu")
+                a = ops.conv2d_nhwc(a, *u["pw1_p"], act="relu", workspace=ws)
                 bsrc = x
             else:
                 a, bsrc = x1, x2
-            b = ops.conv2d_nhwc(bsrc, *u["pw2a_p"], act="relu")
+            b = ops.conv2d_nhwc(bsrc, *u["pw2a_p"], act="relu", workspace=ws)
             b = ops.dwconv_nhwc(b, *u["dw2_p"], stride=u["stride"], pad=1)
-            b = ops.conv2d_nhwc(b, *u["pw2b_p"], act="relu")
+            b = ops.conv2d_nhwc(b, *u["pw2b_p"], act="relu", workspace=ws)
             if u["last"]:
                 x = ops.shuffle_remap(a, b, u["half"], False, round8(2 * u["half"]))
             else:
                 x1, x2 = ops.shuffle_remap(a, b, u["half"], True, hp, hp)
-        x = ops.conv2d_nhwc(x, *self.conv5_p, act="relu")
+        x = ops.conv2d_nhwc(x, *self.conv5_p, act="relu", workspace=ws)
         pooled = ops.avgpool_nhwc(x)
         return ops.linear(pooled, self.fc_w, self.fc_b, out_dtype=torch.float32)
 

@@ -950,6 +950,42 @@ def image_to_nhwc(img_u8: torch.Tensor, Cp: int = 8) -> torch.Tensor:
     return out
 
 
+def image_to_s2d(img_u8: torch.Tensor) -> torch.Tensor:
+    """uint8 [N, H, W, 3] -> normalised f16 space-to-depth [N, H/2, W/2, 16]
+    (channel (dy*2+dx)*3 + c = pixel (2i+dy, 2j+dx) channel c; 12..15 zero)."""
+    _check(img_u8.is_cuda and img_u8.dtype == torch.uint8 and img_u8.is_contiguous() and img_u8.shape[-1] == 3,
+           "image_to_s2d: bad input")
+    N, H, W, _ = img_u8.shape
+    _check(H % 2 == 0 and W % 2 == 0, "image_to_s2d: H and W must be even")
+    out = torch.empty(N, H // 2, W // 2, 16, device=img_u8.device, dtype=torch.float16)
+    _ops().image_to_s2d(img_u8.data_ptr(), N, H, W, out.data_ptr(), _stream())
+    return out
+
+
+def image_to_s2d_ref(img_u8):
+    x = image_to_nhwc_ref(img_u8, 3).float()                       # [N, H, W, 3]
+    N, H, W, _ = x.shape
+    x = x.view(N, H // 2, 2, W // 2, 2, 3).permute(0, 1, 3, 2, 4, 5).reshape(N, H // 2, W // 2, 12)
+    return torch.cat([x, torch.zeros(N, H // 2, W // 2, 4, device=x.device)], -1).half()
+
+
+def stem_weight_s2d(w: torch.Tensor) -> torch.Tensor:
+    """7x7 stride-2 pad-3 conv weights [K, 7, 7, 3] -> the equivalent 4x4 stride-1
+    pad-2 conv on the space-to-depth input, [K, 4, 4, 16]: input row 2(p-2+bi)+dy
+    is tap r = 2*bi + dy - 1 of output row p (taps outside 0..6 are zero)."""
+    K = w.shape[0]
+    out = torch.zeros(K, 4, 4, 16, dtype=w.dtype, device=w.device)
+    for bi in range(4):
+        for bj in range(4):
+            for dy in range(2):
+                for dx in range(2):
+                    r, c = 2 * bi + dy - 1, 2 * bj + dx - 1
+                    if 0 <= r < 7 and 0 <= c < 7:
+                        ch = (dy * 2 + dx) * 3
+                        out[:, bi, bj, ch:ch + 3] = w[:, r, c, :3]
+    return out.contiguous()
+
+
 def image_to_nhwc_ref(img_u8, Cp=8):
     mean = torch.tensor([0.485, 0.456, 0.406], device=img_u8.device)
     std = torch.tensor([0.229, 0.224, 0.225], device=img_u8.device)
@@ -961,14 +997,66 @@ def image_to_nhwc_ref(img_u8, Cp=8):
 # ---------------------------------------------------------------------------
 # Convolution family (NHWC f16)
 # ---------------------------------------------------------------------------
-# RDB_CONV1X1_GEMM=0 keeps 1x1 convolutions on the implicit-GEMM conv kernel
+# RDB_CONV1X1_GEMM=0 keeps 1x1 convolutions off the dense `linear` tiles
 _CONV1X1_GEMM = os.environ.get("RDB_CONV1X1_GEMM", "1") != "0"
+# RDB_CONV_SPLITK=0: no split-K candidates
+_CONV_SPLITK = os.environ.get("RDB_CONV_SPLITK", "1") != "0"
+# Encoded conv tile choices (what the tuner / tile tables store):
+#   cfg                  4-wave tile cfg (0..12) of the implicit-GEMM conv kernel
+#   cfg | splits << 8    the same tile, split-K over `splits` workgroups per tile
+#   CONV_LINEAR | cfg    (1x1 / stride 1) the dense GEMM `linear` on tile cfg (0..25)
+CONV_LINEAR = 1 << 16
+SPLITK_HEADER = 65536                 # gemm_core.h kSplitKHeader (tile arrival counters)
+SPLITK_WS_BYTES = 40 << 20            # one forward's split-K workspace (ops.splitk_workspace)
+_SPLITS = (2, 3, 4, 6, 8)
+_TILE_BM = (128, 64, 128, 64, 128, 192, 256, 128, 128, 64, 128, 256, 128)   # gemm_core.h kTileBM/BN, 4-wave tiles
+_TILE_BN = (128, 128, 64, 64, 192, 128, 128, 256, 144, 96, 96, 144, 48)
+_tune_ws: Dict[int, torch.Tensor] = {}
+
+
+def splitk_workspace(device, nbytes: int = SPLITK_WS_BYTES) -> torch.Tensor:
+    """A split-K workspace: zeroed tile counters + f32 partial tiles.  Every
+    split-K launch leaves the counters zero again, so one workspace serves the
+    consecutive convolutions of a forward; two launches that may overlap (two
+    streams) need two workspaces."""
+    ws = torch.empty(nbytes, device=device, dtype=torch.uint8)
+    ws[:SPLITK_HEADER].zero_()
+    return ws
+
+
+def _conv_candidates(M: int, K_out: int, Kg: int, one_by_one: bool):
+    """Tile choices for a conv of output [M, K_out] over a Kg-long reduction:
+    every 4-wave tile; split-K where the tile grid leaves CUs idle (< 2 blocks
+    per CU) and each split keeps >= 4 K-steps; the dense GEMM tiles for 1x1."""
+    cands = list(range(NUM_CONV_TILE_CFGS))
+    nk = -(-Kg // 64)
+    if _CONV_SPLITK:
+        for c in range(NUM_CONV_TILE_CFGS):
+            tiles = -(-M // _TILE_BM[c]) * -(-K_out // _TILE_BN[c])
+            if tiles >= 512:
+                continue
+            for sp in _SPLITS:
+                kper = -(-nk // sp)
+                eff = -(-nk // kper)
+                if eff < 2 or kper < 4 or tiles * eff > 2048:
+                    continue
+                if SPLITK_HEADER + tiles * eff * _TILE_BM[c] * _TILE_BN[c] * 4 > SPLITK_WS_BYTES:
+                    continue
+                cands.append(c | (sp << 8))
+    if one_by_one and _CONV1X1_GEMM and K_out % 8 == 0:
+        cands += [CONV_LINEAR | c for c in range(NUM_TILE_CFGS)]
+    return cands
 
 
 def conv2d_nhwc(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, stride: int = 1,
                 pad: int = 0, act: str = "none", residual: Optional[torch.Tensor] = None,
-                out: Optional[torch.Tensor] = None, tile_cfg: int = -1) -> torch.Tensor:
-    """x [N, H, W, C] f16, w [K, R, S, C] f16 (BN folded), bias [K]; fused residual + act."""
+                out: Optional[torch.Tensor] = None, tile_cfg: int = -1, out_hw: Optional[tuple] = None,
+                workspace: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """x [N, H, W, C] f16, w [K, R, S, C] f16 (BN folded), bias [K]; fused residual + act.
+    ``out_hw`` = (P, Q) computes only the first P x Q outputs (an asymmetric pad:
+    the space-to-depth stem pads 2 on top / left and 1 on the bottom / right).
+    ``workspace`` (``splitk_workspace``): used when the chosen tile is split-K;
+    without one a split-K choice allocates its own (one extra memset)."""
     _check(x.is_cuda and x.dtype == torch.float16 and x.is_contiguous() and x.dim() == 4, "conv2d: bad x")
     _check(w.dtype == torch.float16 and w.is_contiguous() and w.dim() == 4, "conv2d: bad w")
     N, H, W, C = x.shape
@@ -976,6 +1064,9 @@ def conv2d_nhwc(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] =
     _check(C == C2 and C % 8 == 0, f"conv2d: channel mismatch/alignment {C} vs {C2}")
     P = (H + 2 * pad - R) // stride + 1
     Q = (W + 2 * pad - S) // stride + 1
+    if out_hw is not None:
+        _check(0 < out_hw[0] <= P and 0 < out_hw[1] <= Q, "conv2d: out_hw larger than the padded output")
+        P, Q = int(out_hw[0]), int(out_hw[1])
     if out is None:
         out = torch.empty(N, P, Q, K, device=x.device, dtype=torch.float16)
     _check(out.shape == (N, P, Q, K) and out.is_contiguous(), "conv2d: bad out")
@@ -984,20 +1075,38 @@ def conv2d_nhwc(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] =
     if residual is not None:
         _check(residual.shape == (N, P, Q, K) and residual.is_contiguous() and residual.dtype == torch.float16, "conv2d: bad residual")
     _check(_aligned(x) and _aligned(w), "conv2d: alignment")
-    if R == 1 and S == 1 and stride == 1 and pad == 0 and tile_cfg < 0 and _CONV1X1_GEMM and K % 8 == 0:
-        # a 1x1 / stride-1 convolution on NHWC IS the GEMM [N*H*W, C] x [K, C]^T:
-        # the dense path has the 8-wave and ping-pong tiles the implicit-GEMM
-        # loader does not (the bottleneck blocks' 1x1 convs are 2/3 of ResNet-50's convs)
-        linear(x.view(N * H * W, C), w.view(K, C), bias, act=act,
-               residual=None if residual is None else residual.view(N * P * Q, K), out=out.view(N * P * Q, K))
-        return out
+    M, Kg = N * P * Q, R * S * C
+    one_by_one = R == 1 and S == 1 and stride == 1 and pad == 0
+    fn = _ops().conv2d_nhwc
     args = (x.data_ptr(), w.data_ptr(), _ptr(bias), _ptr(residual), out.data_ptr(), N, H, W, C, K, R, S,
             stride, pad, P, Q, ACT_CODE[act])
-    fn = _ops().conv2d_nhwc
+
+    def launch(c: int, ws: Optional[torch.Tensor]) -> None:
+        if c >= CONV_LINEAR:
+            _ops().gemm_tn(DTYPE_CODE[torch.float16], DTYPE_CODE[torch.float16], x.data_ptr(), C, w.data_ptr(), C,
+                           out.data_ptr(), K, _ptr(bias), _ptr(residual), K if residual is not None else 0, M, K, C,
+                           1.0, ACT_CODE[act], _stream(), c - CONV_LINEAR)
+            return
+        if (c >> 8) > 1 and ws is None:
+            ws = splitk_workspace(x.device, max(SPLITK_HEADER,
+                                                int(_ops().conv_splitk_bytes(M, K, c & 255, c >> 8))))
+        fn(*args, _stream(), int(c), _ptr(ws), 0 if ws is None else ws.numel())
+
     if tile_cfg < 0:
-        key = ("conv", N, H, W, C, K, R, S, stride, pad, act, bias is not None, residual is not None)
-        tile_cfg = _tuned_cfg(key, lambda c: fn(*args, _stream(), c), range(NUM_CONV_TILE_CFGS))
-    fn(*args, _stream(), int(tile_cfg))
+        key = ("conv", N, H, W, C, K, R, S, stride, pad, act, bias is not None, residual is not None) + \
+            ((P, Q) if out_hw is not None else ())
+
+        def tune_launch(c: int) -> None:
+            # tuning launches may overlap on side streams: one workspace per stream
+            ws = None
+            if (c >> 8) > 1 and c < CONV_LINEAR:
+                sid = _stream()
+                ws = _tune_ws.get(sid)
+                if ws is None:
+                    ws = _tune_ws[sid] = splitk_workspace(x.device)
+            launch(c, ws)
+        tile_cfg = _tuned_cfg(key, tune_launch, _conv_candidates(M, K, Kg, one_by_one))
+    launch(int(tile_cfg), workspace)
     return out
 
 

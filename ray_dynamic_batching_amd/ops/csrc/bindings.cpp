@@ -44,9 +44,11 @@ void rope(uintptr_t qkv, int ld, int q_off, int k_off, int H, int Hkv, int D, in
           uintptr_t sin_t, int T, int pos_offset, uintptr_t stream);
 void gather_rows(uintptr_t src_ptrs, int n, int rows, int row_bytes, uintptr_t dst, uintptr_t stream);
 void image_to_nhwc(uintptr_t src, int N, int HW, int Cp, uintptr_t dst, uintptr_t stream);
+void image_to_s2d(uintptr_t src, int N, int H, int W, uintptr_t dst, uintptr_t stream);
 void conv2d_nhwc(uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t res, uintptr_t y, int N, int H,
                  int W, int C, int K, int R, int S, int stride, int pad, int P, int Q, int act,
-                 uintptr_t stream, int force_cfg);
+                 uintptr_t stream, int force_cfg, uintptr_t ws, size_t ws_bytes);
+size_t conv_splitk_bytes(int M, int N, int cfg, int splits);
 void maxpool_nhwc(uintptr_t x, uintptr_t y, int N, int H, int W, int C, int k, int stride, int pad,
                   int P, int Q, uintptr_t stream);
 void avgpool_nhwc(uintptr_t x, uintptr_t y, int N, int HW, int C, uintptr_t stream);
@@ -103,7 +105,9 @@ PYBIND11_MODULE(_rdb_ops, m) {
   m.def("rope", &rdb::rope, py::call_guard<py::gil_scoped_release>());
   m.def("gather_rows", &rdb::gather_rows, py::call_guard<py::gil_scoped_release>());
   m.def("image_to_nhwc", &rdb::image_to_nhwc, py::call_guard<py::gil_scoped_release>());
+  m.def("image_to_s2d", &rdb::image_to_s2d, py::call_guard<py::gil_scoped_release>());
   m.def("conv2d_nhwc", &rdb::conv2d_nhwc, py::call_guard<py::gil_scoped_release>());
+  m.def("conv_splitk_bytes", &rdb::conv_splitk_bytes);
   m.def("maxpool_nhwc", &rdb::maxpool_nhwc, py::call_guard<py::gil_scoped_release>());
   m.def("avgpool_nhwc", &rdb::avgpool_nhwc, py::call_guard<py::gil_scoped_release>());
   m.def("dwconv_nhwc", &rdb::dwconv_nhwc, py::call_guard<py::gil_scoped_release>());

@@ -11,26 +11,35 @@
 
 namespace rdb {
 
+// force_cfg = tile | (splits << 8): splits > 1 runs split-K on the workspace
+// `ws` (ws_bytes; zeroed counter header, see splitk_bytes) when it fits, else unsplit.
 void conv2d_nhwc(uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t res, uintptr_t y, int N, int H,
                  int W, int C, int K, int R, int S, int stride, int pad, int P, int Q, int act,
-                 uintptr_t stream, int force_cfg) {
+                 uintptr_t stream, int force_cfg, uintptr_t ws, size_t ws_bytes) {
   if (C % 8 != 0) throw std::invalid_argument("conv2d_nhwc: C must be a multiple of 8 (pad channels)");
   if ((x | w) & 15) throw std::invalid_argument("conv2d_nhwc: x/w must be 16-byte aligned");
+  if (P > (H + 2 * pad - R) / stride + 1 || Q > (W + 2 * pad - S) / stride + 1)
+    throw std::invalid_argument("conv2d_nhwc: P / Q larger than the padded output");
   const int M = N * P * Q, Kg = R * S * C;
   if (M <= 0 || K <= 0) return;
+  const int cfg = force_cfg < 0 ? -1 : (force_cfg & 255);
+  const int splits = force_cfg < 0 ? 1 : (force_cfg >> 8);
+  const LnEpi sk = splitk_epi(M, K, Kg, cfg, splits, reinterpret_cast<void*>(ws), ws_bytes);
   ConvParams p{reinterpret_cast<const void*>(x), N, H, W, C, R, S, stride, pad, P, Q, M, Kg};
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   if (R == 1 && S == 1 && stride == 1 && pad == 0) {
     // 1x1 stride-1 conv is a plain GEMM over the NHWC pixels.
     DenseParams d{reinterpret_cast<const void*>(x), C, M, C};
     launch_mfma_gemm<f16, f16, DenseLoader>(d, (const f16*)w, Kg, (f16*)y, K, (const f16*)bias,
-                                            (const f16*)res, K, M, K, Kg, 1.f, act, s, force_cfg);
+                                            (const f16*)res, K, M, K, Kg, 1.f, act, s, cfg, sk);
   } else {
     launch_mfma_gemm<f16, f16, Im2colLoader>(p, (const f16*)w, Kg, (f16*)y, K, (const f16*)bias,
-                                             (const f16*)res, K, M, K, Kg, 1.f, act, s, force_cfg);
+                                             (const f16*)res, K, M, K, Kg, 1.f, act, s, cfg, sk);
   }
   RDB_HIP_CHECK(hipGetLastError());
 }
+
+size_t conv_splitk_bytes(int M, int N, int cfg, int splits) { return splitk_bytes(M, N, cfg, splits); }
 
 // Depthwise RxR conv, NHWC f16, weights [R][R][C] (channel-contiguous), bias [C].
 // One thread = 8 channels of one output pixel.
@@ -124,30 +133,52 @@ void maxpool_nhwc(uintptr_t x, uintptr_t y, int N, int H, int W, int C, int k, i
   RDB_HIP_CHECK(hipGetLastError());
 }
 
-// Global average pool: one block per (n, 2048-channel slice); lanes own 8 channels.
+// Global average pool [N, HW, C] -> [N, C]: a block owns (n, 256 channels) --
+// 32 lanes x 8 channels per row slice, 8 slices of the HW positions -- and the
+// slices meet in LDS.  (One block per image with one thread per 8 channels left
+// 32 blocks for 256 CUs: 15.7 us at ResNet-50 bs32, profiles/pmc_resnet50_forward_r3.json.)
 __global__ void __launch_bounds__(256)
 avgpool_kernel(const f16* __restrict__ x, f16* __restrict__ y, int N, int HW, int C) {
+  constexpr int CG = 32, SL = 8;
+  __shared__ float part[SL][CG * 8 + 4];
   const int n = blockIdx.y;
-  const int c8 = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c8 * 8 >= C) return;
+  const int cl = threadIdx.x % CG, sl = threadIdx.x / CG;
+  const int c8 = blockIdx.x * CG + cl;
+  const bool on = c8 * 8 < C;
   float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  const f16* base = x + (size_t)n * HW * C + c8 * 8;
-  for (int i = 0; i < HW; ++i) {
-    const f16x8 v = *reinterpret_cast<const f16x8*>(base + (size_t)i * C);
+  if (on) {
+    const f16* base = x + (size_t)n * HW * C + c8 * 8;
+    int i = sl;
+#pragma unroll 1
+    for (; i + SL < HW; i += 2 * SL) {     // two independent 16-B loads in flight
+      const f16x8 a = *reinterpret_cast<const f16x8*>(base + (size_t)i * C);
+      const f16x8 b = *reinterpret_cast<const f16x8*>(base + (size_t)(i + SL) * C);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) acc[j] += (float)v[j];
+      for (int j = 0; j < 8; ++j) acc[j] += (float)a[j] + (float)b[j];
+    }
+    if (i < HW) {
+      const f16x8 a = *reinterpret_cast<const f16x8*>(base + (size_t)i * C);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += (float)a[j];
+    }
   }
-  f16x8 o;
-  const float inv = 1.f / HW;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) o[j] = (f16)(acc[j] * inv);
-  *reinterpret_cast<f16x8*>(y + (size_t)n * C + c8 * 8) = o;
+  for (int j = 0; j < 8; ++j) part[sl][cl * 8 + j] = acc[j];
+  __syncthreads();
+  // 256 threads finish 256 channels: thread t sums channel t over the slices
+  const int ch = blockIdx.x * CG * 8 + threadIdx.x;
+  if (ch < C) {
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < SL; ++k) s += part[k][threadIdx.x];
+    y[(size_t)n * C + ch] = (f16)(s / HW);
+  }
 }
 
 void avgpool_nhwc(uintptr_t x, uintptr_t y, int N, int HW, int C, uintptr_t stream) {
   if (C % 8 != 0) throw std::invalid_argument("avgpool_nhwc: C must be a multiple of 8");
-  if (N <= 0) return;
-  dim3 grid((C / 8 + 255) / 256, N);
+  if (N <= 0 || HW <= 0) return;
+  dim3 grid((C + 255) / 256, N);
   hipLaunchKernelGGL(avgpool_kernel, grid, dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
                      (const f16*)x, (f16*)y, N, HW, C);
   RDB_HIP_CHECK(hipGetLastError());

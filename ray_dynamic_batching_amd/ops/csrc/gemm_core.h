@@ -218,6 +218,12 @@ struct LnEpi {
   int* panel;             // LNOUT: zeroed arrival counters, one per row panel (tiles_m)
   int* err;               // LNOUT: set to 1 if a panel wait timed out (never hangs)
   int a_parts, r_parts;   // STG: partials per row in a_stats / r_stats (row stride a_ld / r_ld floats)
+  // split-K (plain epilogues, gridDim.y = splits > 1): split z runs K-steps
+  // [z * sk_kper, (z + 1) * sk_kper); the last split of a tile to arrive at its
+  // counter adds the others' f32 partials and runs the epilogue (no waiting)
+  float* sk_part;         // [tiles][splits][BM * BN] f32 partial tiles
+  int* sk_cnt;            // [tiles] arrival counters, zero between launches (the last arriver resets)
+  int sk_kper;
 };
 
 // (sum, sum of squares) of the 8 elements of an MFMA fragment, accumulated with
@@ -872,16 +878,19 @@ mfma_gemm_kernel(typename LoaderT<T, 1>::Params ap, const T* __restrict__ W, int
   }
 
   if constexpr (STG) ln_stage<T, EPI, BM, BN, NT>(smem + LN_OFF, ln, m0, n0, M, N);   // before the first DMA
-  const int nk = (K + BK - 1) / BK;
+  // split-K: this block's K-steps [kb, kb + nk) (host: every split non-empty)
+  const int nk_all = (K + BK - 1) / BK;
+  const int kb = EPI == 0 && gridDim.y > 1 ? (int)blockIdx.y * ln.sk_kper : 0;
+  const int nk = EPI == 0 && gridDim.y > 1 ? min(ln.sk_kper, nk_all - kb) : nk_all;
   if constexpr (kStages == 2) {
     // Two LDS stages: the DMA of tile k+1 runs under the MFMAs of tile k; the
     // __syncthreads() at the end of a step waits the issuing waves' DMA
     // (vmcnt(0)) and orders every wave's reads before the buffer is refilled.
-    stage(0, 0);
+    stage(0, kb * BK);
     __syncthreads();
     for (int kt = 0; kt < nk; ++kt) {
-      if (kt + 1 < nk) stage((kt + 1) & 1, (kt + 1) * BK);
-      compute(kt & 1, kt * BK);
+      if (kt + 1 < nk) stage((kt + 1) & 1, (kb + kt + 1) * BK);
+      compute(kt & 1, (kb + kt) * BK);
       __syncthreads();
     }
   } else {
@@ -896,8 +905,8 @@ mfma_gemm_kernel(typename LoaderT<T, 1>::Params ap, const T* __restrict__ W, int
     constexpr int kWaitOne = (kLoads & 15) | ((kLoads >> 4) << 14) | 0x70 | 0xF00;  // vmcnt(kLoads)
     constexpr int kWaitAll = 0x70 | 0xF00;                                             // vmcnt(0)
     static_assert(kLoads < 64, "vmcnt field is 6 bits");
-    stage(0, 0);
-    if (nk > 1) stage(1, BK);
+    stage(0, kb * BK);
+    if (nk > 1) stage(1, (kb + 1) * BK);
     int buf = 0;
     for (int kt = 0; kt < nk; ++kt) {
       if (kt + 1 < nk) __builtin_amdgcn_s_waitcnt(kWaitOne);
@@ -905,11 +914,55 @@ mfma_gemm_kernel(typename LoaderT<T, 1>::Params ap, const T* __restrict__ W, int
       asm volatile("" ::: "memory");
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
-      if (kt + 2 < nk) stage(buf == 0 ? 2 : buf - 1, (kt + 2) * BK);
-      compute(buf, kt * BK);
+      if (kt + 2 < nk) stage(buf == 0 ? 2 : buf - 1, (kb + kt + 2) * BK);
+      compute(buf, (kb + kt) * BK);
       buf = buf == 2 ? 0 : buf + 1;
     }
     __syncthreads();
+  }
+  if constexpr (EPI == 0) {
+    if (gridDim.y > 1) {
+      // ---- split-K hand-off (the gemm_sk.h protocol): partials are stored and
+      // loaded sc1; a storing block drains vmcnt, meets at a barrier, then one
+      // lane adds to the tile's counter (agent scope).  The last arriver --
+      // told by the counter -- resets it, folds the other splits in and goes on
+      // to the epilogue; every other block is done.  Nobody waits.
+      __shared__ int sk_flag;
+      const int splits = gridDim.y, z = blockIdx.y;
+      int* cnt = ln.sk_cnt + t;
+      const __amdgpu_buffer_rsrc_t psrc =
+          make_rsrc(ln.sk_part, (uint32_t)((size_t)nwg * splits * BM * BN * sizeof(float)));
+      auto slot_off = [&](int zz, int i, int j) {
+        return (uint32_t)(((((size_t)t * splits + zz) * (TN * TM) + i * TM + j) * NT + tid) * 16);
+      };
+      if (tid == 0) sk_flag = __hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == splits - 1;
+      __syncthreads();
+      bool last = sk_flag != 0;
+      __syncthreads();
+      if (!last) {
+#pragma unroll
+        for (int i = 0; i < TN; ++i)
+#pragma unroll
+          for (int j = 0; j < TM; ++j)
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i][j]), psrc, slot_off(z, i, j), 0, 16);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0)
+          sk_flag = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == splits - 1;
+        __syncthreads();
+        last = sk_flag != 0;
+      }
+      if (!last) return;
+      if (tid == 0) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      for (int zz = 0; zz < splits; ++zz) {
+        if (zz == z) continue;
+#pragma unroll
+        for (int i = 0; i < TN; ++i)
+#pragma unroll
+          for (int j = 0; j < TM; ++j)
+            acc[i][j] += __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(psrc, slot_off(zz, i, j), 0, 16));
+      }
+    }
   }
   if constexpr (SELF) {
 #pragma unroll
@@ -1191,8 +1244,15 @@ template <typename T, typename OutT, template <typename, int> class LoaderT, boo
 void launch_one(const P& ap, const T* W, int ldw, OutT* C, int ldc, const T* bias, const T* R, int ldr, int M,
                 int N, int K, float alpha, int act, hipStream_t s, const LnEpi& ln = LnEpi{}) {
   const int nwg = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
-  hipLaunchKernelGGL((mfma_gemm_kernel<T, OutT, BM, BN, LoaderT, HB, HR, WGM, NW, EPI>), dim3(nwg), dim3(64 * NW), 0,
-                     s, ap, W, ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act, ln);
+  int splits = 1;
+  if (EPI == 0 && ln.sk_kper > 0) {
+    // split-K: ceil(nk / kper) non-empty splits; the workspace must hold every
+    // (tile, split) partial and the tile counters (checked by splitk_fits)
+    const int nk = (K + 63) / 64;
+    splits = (nk + ln.sk_kper - 1) / ln.sk_kper;
+  }
+  hipLaunchKernelGGL((mfma_gemm_kernel<T, OutT, BM, BN, LoaderT, HB, HR, WGM, NW, EPI>), dim3(nwg, splits),
+                     dim3(64 * NW), 0, s, ap, W, ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act, ln);
 }
 
 template <typename T, typename OutT, template <typename, int> class LoaderT, bool HB, bool HR, int EPI = 0,
@@ -1296,19 +1356,49 @@ void launch_mfma_gemm_t(const P& ap, const T* W, int ldw, OutT* C, int ldc, cons
 #undef RDB_TILE
 }
 
+// Split-K workspace: tile arrival counters in the first 64 KiB (zeroed once;
+// every launch leaves them zero), then the f32 partial tiles.
+constexpr size_t kSplitKHeader = 65536;
+constexpr int kSplitKMaxTiles = (int)(kSplitKHeader / sizeof(int));
+inline size_t splitk_bytes(int M, int N, int cfg, int splits) {
+  const int bm = kTileBM[cfg], bn = kTileBN[cfg];
+  const size_t tiles = (size_t)((M + bm - 1) / bm) * ((N + bn - 1) / bn);
+  return kSplitKHeader + tiles * splits * bm * bn * sizeof(float);
+}
+// LnEpi carrying a split-K request, or none (splits < 2, no / too small
+// workspace, too many tiles, > 2^31 partial bytes): the launch then runs unsplit.
+inline LnEpi splitk_epi(int M, int N, int K, int cfg, int splits, void* ws, size_t ws_bytes) {
+  LnEpi e{};
+  if (splits < 2 || ws == nullptr || cfg < 0 || cfg >= kNumTiles4) return e;
+  const int nk = (K + 63) / 64;
+  const int kper = (nk + splits - 1) / splits;
+  const int eff = (nk + kper - 1) / kper;
+  const int bm = kTileBM[cfg], bn = kTileBN[cfg];
+  const long tiles = (long)((M + bm - 1) / bm) * ((N + bn - 1) / bn);
+  const size_t need = splitk_bytes(M, N, cfg, eff);
+  if (eff < 2 || tiles > kSplitKMaxTiles || need > ws_bytes || need - kSplitKHeader > (size_t(1) << 31)) return e;
+  e.sk_cnt = static_cast<int*>(ws);
+  e.sk_part = reinterpret_cast<float*>(static_cast<char*>(ws) + kSplitKHeader);
+  e.sk_kper = kper;
+  return e;
+}
+
 template <typename T, typename OutT, template <typename, int> class LoaderT, typename P>
 void launch_mfma_gemm(const P& ap, const T* W, int ldw, OutT* C, int ldc, const T* bias, const T* R,
-                      int ldr, int M, int N, int K, float alpha, int act, hipStream_t s, int cfg) {
+                      int ldr, int M, int N, int K, float alpha, int act, hipStream_t s, int cfg,
+                      const LnEpi& ln = LnEpi{}) {
   constexpr bool dense = std::is_same<LoaderT<T, 1>, DenseLoader<T, 1>>::value;
   if (cfg < 0 || cfg >= (dense ? kNumTiles : kNumTiles4)) cfg = pick_tile_cfg(M, N, dense);
+  // split-K runs on the 4-wave tiles (0..12) only: their kernel carries the hand-off
+  const LnEpi e = (ln.sk_kper > 0 && cfg < kNumTiles4 && act != ACT_SWIGLU) ? ln : LnEpi{};
   if (bias && R)
-    launch_mfma_gemm_t<T, OutT, LoaderT, true, true>(ap, W, ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act, s, cfg);
+    launch_mfma_gemm_t<T, OutT, LoaderT, true, true>(ap, W, ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act, s, cfg, e);
   else if (bias)
-    launch_mfma_gemm_t<T, OutT, LoaderT, true, false>(ap, W, ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act, s, cfg);
+    launch_mfma_gemm_t<T, OutT, LoaderT, true, false>(ap, W, ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act, s, cfg, e);
   else if (R)
-    launch_mfma_gemm_t<T, OutT, LoaderT, false, true>(ap, W, ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act, s, cfg);
+    launch_mfma_gemm_t<T, OutT, LoaderT, false, true>(ap, W, ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act, s, cfg, e);
   else
-    launch_mfma_gemm_t<T, OutT, LoaderT, false, false>(ap, W, ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act, s, cfg);
+    launch_mfma_gemm_t<T, OutT, LoaderT, false, false>(ap, W, ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act, s, cfg, e);
 }
 
 }  // namespace rdb

@@ -186,6 +186,53 @@ void image_to_nhwc(uintptr_t src, int N, int HW, int Cp, uintptr_t dst, uintptr_
   RDB_HIP_CHECK(hipGetLastError());
 }
 
+// uint8 HWC (RGB) -> normalised f16 SPACE-TO-DEPTH [N, H/2, W/2, 16]: channel
+// (dy*2 + dx)*3 + c of output pixel (i, j) is input pixel (2i+dy, 2j+dx) channel c,
+// channels 12..15 are zero.  A 7x7 stride-2 stem conv on the image is then a 4x4
+// stride-1 conv on this tensor (ResNet50.stem_w_s2d): 256 reduction elements per
+// output instead of 7*7*8 = 392 with the channel-padded layout.
+__global__ void image_to_s2d_kernel(const uint8_t* __restrict__ src, int N, int H, int W,
+                                    float m0, float m1, float m2, float s0, float s1, float s2,
+                                    f16* __restrict__ dst) {
+  const int P = H >> 1, Q = W >> 1;
+  const long total = (long)N * P * Q;
+  const float a[3] = {1.f / (255.f * s0), 1.f / (255.f * s1), 1.f / (255.f * s2)};
+  const float b[3] = {-m0 / s0, -m1 / s1, -m2 / s2};
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+    const int j = e % Q;
+    const long ni = e / Q;
+    const int i = ni % P;
+    const int n = ni / P;
+    f16x8 lo, hi;
+#pragma unroll
+    for (int dy = 0; dy < 2; ++dy) {
+      const uint8_t* r = src + (((size_t)n * H + 2 * i + dy) * W + 2 * j) * 3;
+#pragma unroll
+      for (int t = 0; t < 6; ++t) {            // (dx, c) = (t / 3, t % 3)
+        const int ch = dy * 6 + t;
+        const f16 v = (f16)(r[t] * a[t % 3] + b[t % 3]);
+        if (ch < 8) lo[ch] = v; else hi[ch - 8] = v;
+      }
+    }
+#pragma unroll
+    for (int c = 4; c < 8; ++c) hi[c] = (f16)0.f;
+    f16x8* d = reinterpret_cast<f16x8*>(dst + (size_t)e * 16);
+    d[0] = lo;
+    d[1] = hi;
+  }
+}
+
+void image_to_s2d(uintptr_t src, int N, int H, int W, uintptr_t dst, uintptr_t stream) {
+  if (N <= 0) return;
+  if ((H | W) & 1) throw std::invalid_argument("image_to_s2d: H and W must be even");
+  const long total = (long)N * (H / 2) * (W / 2);
+  int blocks = (int)((total + 255) / 256);
+  blocks = blocks > 8192 ? 8192 : blocks;
+  hipLaunchKernelGGL(image_to_s2d_kernel, dim3(blocks), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+                     (const uint8_t*)src, N, H, W, 0.485f, 0.456f, 0.406f, 0.229f, 0.224f, 0.225f, (f16*)dst);
+  RDB_HIP_CHECK(hipGetLastError());
+}
+
 // Per-sequence valid length = number of non-pad token ids (BERT key-padding
 // mask for the attention kernel): one wave per sequence, one launch.
 __global__ void __launch_bounds__(64) seq_lens_kernel(const int* __restrict__ ids, int S, int pad, int* __restrict__ lens) {

@@ -236,6 +236,70 @@ def test_conv2d(N, H, C, K, R, stride, pad):
     _close(y2, ops.conv2d_nhwc_ref(x, w, b, stride=stride, pad=pad, act="relu", residual=r), 2e-2, 2e-2)
 
 
+@pytest.mark.parametrize("N,H,C,K,R,stride,pad", [
+    (32, 7, 512, 512, 3, 1, 1), (32, 14, 256, 256, 3, 1, 1), (4, 14, 1024, 256, 1, 1, 0),
+    (2, 28, 128, 128, 3, 2, 1), (3, 7, 2048, 512, 1, 1, 0)])
+def test_conv2d_splitk(N, H, C, K, R, stride, pad):
+    """Split-K convolutions (tile | splits << 8; last-arriver hand-off) on one
+    shared workspace, back to back: every result matches the fp32 reference and
+    the workspace's tile counters are zero again afterwards."""
+    ops = _ops()
+    torch.manual_seed(11)
+    x = torch.randn(N, H, H, C, device="cuda", dtype=torch.float16)
+    w = torch.randn(K, R, R, C, device="cuda", dtype=torch.float16) * (R * R * C) ** -0.5
+    b = torch.randn(K, device="cuda", dtype=torch.float16) * 0.1
+    ref = ops.conv2d_nhwc_ref(x, w, b, stride=stride, pad=pad, act="relu")
+    r = torch.randn_like(ref)
+    ref_r = ops.conv2d_nhwc_ref(x, w, b, stride=stride, pad=pad, act="relu", residual=r)
+    ws = ops.splitk_workspace("cuda")
+    nk = -(-(R * R * C) // 64)
+    for cfg in (0, 3, 9, 12):
+        for sp in (2, 3, 8):
+            if -(-nk // -(-nk // sp)) < 2:
+                continue
+            c = cfg | (sp << 8)
+            _close(ops.conv2d_nhwc(x, w, b, stride=stride, pad=pad, act="relu", tile_cfg=c, workspace=ws), ref, 2e-2, 2e-2)
+            _close(ops.conv2d_nhwc(x, w, b, stride=stride, pad=pad, act="relu", residual=r, tile_cfg=c, workspace=ws),
+                   ref_r, 2e-2, 2e-2)
+    # without a workspace: a private one
+    _close(ops.conv2d_nhwc(x, w, b, stride=stride, pad=pad, act="relu", tile_cfg=0 | (2 << 8)), ref, 2e-2, 2e-2)
+    torch.cuda.synchronize()
+    assert int(ws[:ops.SPLITK_HEADER].view(torch.int32).abs().sum()) == 0
+    if R == 1 and stride == 1:
+        for c in (0, 10, 19, 23):
+            _close(ops.conv2d_nhwc(x, w, b, act="relu", residual=r, tile_cfg=ops.CONV_LINEAR | c), ref_r, 2e-2, 2e-2)
+
+
+def test_conv2d_splitk_graph_replay():
+    """Split-K inside a captured graph with the per-forward workspace idiom of
+    ResNet50._logits_hip, replayed with new inputs."""
+    ops = _ops()
+    torch.manual_seed(12)
+    x = torch.randn(32, 7, 7, 512, device="cuda", dtype=torch.float16)
+    w = torch.randn(512, 3, 3, 512, device="cuda", dtype=torch.float16) * (9 * 512) ** -0.5
+    b = torch.randn(512, device="cuda", dtype=torch.float16) * 0.1
+
+    def fwd():
+        ws = ops.splitk_workspace("cuda")
+        h = ops.conv2d_nhwc(x, w, b, pad=1, act="relu", tile_cfg=0 | (4 << 8), workspace=ws)
+        return ops.conv2d_nhwc(h, w, b, pad=1, act="relu", tile_cfg=9 | (3 << 8), workspace=ws)
+
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        fwd()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            y = fwd()
+    torch.cuda.synchronize()
+    for it in range(3):
+        x.copy_(torch.randn_like(x))
+        g.replay()
+        torch.cuda.synchronize()
+        h = ops.conv2d_nhwc_ref(x, w, b, pad=1, act="relu")
+        _close(y, ops.conv2d_nhwc_ref(h, w, b, pad=1, act="relu"), 3e-2, 3e-2)
+
+
 def test_pools_and_dwconv():
     ops = _ops()
     torch.manual_seed(9)
@@ -247,6 +311,32 @@ def test_pools_and_dwconv():
     for stride in (1, 2):
         _close(ops.dwconv_nhwc(x, w, b, stride=stride, pad=1, act="silu"),
                ops.dwconv_nhwc_ref(x, w, b, stride=stride, pad=1, act="silu"), 2e-2, 2e-2)
+
+
+@pytest.mark.parametrize("N,HW,C", [(32, 49, 2048), (3, 1, 8), (2, 17, 264), (1, 196, 1024)])
+def test_avgpool_shapes(N, HW, C):
+    ops = _ops()
+    torch.manual_seed(N + HW)
+    x = torch.randn(N, HW, 1, C, device="cuda", dtype=torch.float16)
+    _close(ops.avgpool_nhwc(x), ops.avgpool_nhwc_ref(x), 1e-3, 1e-2)
+
+
+def test_image_to_s2d_and_space_to_depth_stem():
+    """u8 image -> space-to-depth f16, and the 4x4 stride-1 stem conv on it (out
+    cut to 112 x 112) against the 7x7 stride-2 conv of the channel-padded image."""
+    ops = _ops()
+    img = torch.randint(0, 256, (3, 224, 224, 3), device="cuda", dtype=torch.uint8)
+    xs = ops.image_to_s2d(img)
+    _close(xs, ops.image_to_s2d_ref(img), 1e-2, 1e-2)
+    g = torch.Generator().manual_seed(3)
+    w = torch.zeros(64, 7, 7, 8, dtype=torch.float16)
+    w[..., :3] = (torch.randn(64, 7, 7, 3, generator=g) * (147 ** -0.5)).half()
+    w = w.cuda()
+    b = (torch.randn(64, generator=g) * 0.1).half().cuda()
+    ref = ops.conv2d_nhwc_ref(ops.image_to_nhwc(img, 8), w, b, stride=2, pad=3, act="relu")
+    y = ops.conv2d_nhwc(xs, ops.stem_weight_s2d(w), b, stride=1, pad=2, act="relu", out_hw=(112, 112))
+    assert y.shape == (3, 112, 112, 64)
+    _close(y, ref, 2e-2, 2e-2)
 
 
 def test_image_to_nhwc_and_gather():
