@@ -23,6 +23,8 @@ def main(argv=None):
     ap.add_argument("--act", default="none")
     ap.add_argument("--res", action="store_true")
     ap.add_argument("--bias", action="store_true")
+    ap.add_argument("--streamk", type=int, default=0, help="also time the stream-K kernel on this many workgroups")
+    ap.add_argument("--graph", type=int, default=1, help="1: time a captured graph of --iters calls (default)")
     a = ap.parse_args(argv)
     import torch
 
@@ -35,28 +37,45 @@ def main(argv=None):
     r = torch.randn(a.m, a.n, device="cuda", dtype=torch.bfloat16) if a.res else None
     cfgs = range(ops.NUM_TILE_CFGS) if a.cfg < 0 else [a.cfg]
     out = {}
-    for c in cfgs:
+
+    def timed(fn) -> float:
+        """us per call: eager loop, or (--graph, the default) one hipGraph of
+        --iters calls, so host launch cost never shows in short kernels."""
         for _ in range(5):
-            ops.linear(x, w, b, act=a.act, residual=r, tile_cfg=c)
+            fn()
         torch.cuda.synchronize()
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        s.record()
-        for _ in range(a.iters):
-            ops.linear(x, w, b, act=a.act, residual=r, tile_cfg=c)
-        e.record()
+        if a.graph:
+            g = torch.cuda.CUDAGraph()
+            st = torch.cuda.Stream()
+            st.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(st), torch.cuda.graph(g, stream=st):
+                for _ in range(a.iters):
+                    fn()
+            torch.cuda.synchronize()
+            g.replay()
+            torch.cuda.synchronize()
+            s.record()
+            g.replay()
+            e.record()
+        else:
+            s.record()
+            for _ in range(a.iters):
+                fn()
+            e.record()
         torch.cuda.synchronize()
-        us = s.elapsed_time(e) / a.iters * 1e3
+        return s.elapsed_time(e) / a.iters * 1e3
+
+    for c in cfgs:
+        us = timed(lambda: ops.linear(x, w, b, act=a.act, residual=r, tile_cfg=c))
         out[c] = dict(us=round(us, 2), tflops=round(2 * a.m * a.n * a.k / us / 1e6, 1))
-    t = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    for _ in range(5):
-        torch.nn.functional.linear(x, w, b)
-    torch.cuda.synchronize()
-    t[0].record()
-    for _ in range(a.iters):
-        torch.nn.functional.linear(x, w, b)
-    t[1].record()
-    torch.cuda.synchronize()
-    hb = t[0].elapsed_time(t[1]) / a.iters * 1e3
+    if a.streamk:
+        for tile in (0, 1):
+            ws = ops.streamk_workspace(x.device, a.streamk, tile)
+            us = timed(lambda: ops.linear_streamk(x, w, b, act=a.act, residual=r, workspace=ws, grid=a.streamk,
+                                                  tile=tile))
+            out[f"streamk_t{tile}_g{a.streamk}"] = dict(us=round(us, 2), tflops=round(2 * a.m * a.n * a.k / us / 1e6, 1))
+    hb = timed(lambda: torch.nn.functional.linear(x, w, b))
     print(json.dumps(dict(shape=[a.m, a.n, a.k], ours=out, hipblaslt_us=round(hb, 2),
                           hipblaslt_tflops=round(2 * a.m * a.n * a.k / hb / 1e6, 1))))
 

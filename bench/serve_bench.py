@@ -32,6 +32,7 @@ def main(argv=None):
     ap.add_argument("--max-wait-ms", type=float, default=5.0)
     ap.add_argument("--backend", default="hip")
     ap.add_argument("--pipeline-depth", type=int, default=2)
+    ap.add_argument("--compute-streams", type=int, default=1, help="batches executing concurrently on the GPU")
     ap.add_argument("--json-out", default="")
     a = ap.parse_args(argv)
 
@@ -58,7 +59,7 @@ def main(argv=None):
     j.configure_queue(0, 0, 0, cap, 0.0, True)
     runner = EngineRunner(name, 0, [SessionSpec(model=m, queue=0, max_batch=a.max_batch,
                                                 max_wait_s=a.max_wait_ms / 1e3)],
-                          pipeline_depth=a.pipeline_depth).build()
+                          pipeline_depth=a.pipeline_depth, compute_streams=a.compute_streams).build()
     runner.start()
     points = []
     try:
@@ -90,6 +91,7 @@ def main(argv=None):
         runner.stop()
         j.close()
     out = {"model": a.model, "backend": a.backend, "max_batch": a.max_batch, "max_wait_ms": a.max_wait_ms,
+           "pipeline_depth": a.pipeline_depth, "compute_streams": a.compute_streams,
            "tile_table": os.path.basename(os.environ.get("RDB_TUNE_FILE", "")) or "tuned at start-up",
            "points": points}
     if a.json_out:

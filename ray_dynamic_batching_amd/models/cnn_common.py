@@ -150,9 +150,8 @@ class ImageClassifier:
         """img uint8 [B, H, W, 3] -> [B, 2k] f32 = (top-k probs, top-k class ids)."""
         logits = self.logits(img)
         if self.backend == "hip":
-            p, i = ops.softmax_topk(logits, self.topk)
-        else:
-            p, i = ops.softmax_topk_ref(logits, self.topk)
+            return ops.softmax_topk_packed(logits, self.topk)
+        p, i = ops.softmax_topk_ref(logits, self.topk)
         return torch.cat([p, i.float()], dim=1).contiguous()
 
     def logits(self, img: torch.Tensor) -> torch.Tensor:

@@ -148,9 +148,8 @@ class ResNet50:
         """img uint8 [B, H, W, 3] -> [B, 2k] f32 = (top-k probs, top-k class ids)."""
         logits = self.logits(img)
         if self.backend == "hip":
-            p, i = ops.softmax_topk(logits, self.topk)
-        else:
-            p, i = ops.softmax_topk_ref(logits, self.topk)
+            return ops.softmax_topk_packed(logits, self.topk)   # [k probs | k ids] written by the kernel
+        p, i = ops.softmax_topk_ref(logits, self.topk)
         return torch.cat([p, i.float()], dim=1).contiguous()
 
     def logits(self, img: torch.Tensor) -> torch.Tensor:
@@ -159,11 +158,12 @@ class ResNet50:
         return self._logits_torch(img)
 
     def _logits_hip(self, img):
-        # one split-K workspace per forward (its tile counters zeroed once; the
-        # convolutions of the forward run one after another on its stream)
-        ws = ops.splitk_workspace(img.device)
-        if self.stem_s2d and img.shape[1] % 2 == 0 and img.shape[2] % 2 == 0:
-            x = ops.image_to_s2d(img)
+        # one split-K workspace per forward (its tile counters zeroed once, by the
+        # first kernel; the convolutions of the forward run one after another on its stream)
+        s2d = self.stem_s2d and img.shape[1] % 2 == 0 and img.shape[2] % 4 == 0
+        ws = ops.splitk_workspace(img.device, zeroed=not s2d)
+        if s2d:
+            x = ops.image_to_s2d(img, zero=ws)          # also zeroes the workspace's counters
             x = ops.conv2d_nhwc(x, self.stem_w_s2d, self.stem_b, stride=1, pad=2, act="relu",
                                 out_hw=(img.shape[1] // 2, img.shape[2] // 2), workspace=ws)
         else:

@@ -101,7 +101,9 @@ class ViT:
     @torch.no_grad()
     def forward(self, img):
         logits = self._logits_hip(img) if self.backend == "hip" else self._logits_torch(img)
-        p, i = (ops.softmax_topk if self.backend == "hip" else ops.softmax_topk_ref)(logits, self.topk)
+        if self.backend == "hip":
+            return ops.softmax_topk_packed(logits, self.topk)
+        p, i = ops.softmax_topk_ref(logits, self.topk)
         return torch.cat([p, i.float()], dim=1).contiguous()
 
     def logits(self, img):

@@ -899,6 +899,18 @@ def softmax_topk(logits: torch.Tensor, k: int) -> Tuple[torch.Tensor, torch.Tens
     return probs, idx
 
 
+def softmax_topk_packed(logits: torch.Tensor, k: int) -> torch.Tensor:
+    """softmax + top-k written as the serving output row [k probs | k class ids
+    as f32] ([B, 2k]) by the kernel itself (no cat / cast kernels)."""
+    _check(logits.is_cuda and logits.dtype == torch.float32 and logits.dim() == 2 and logits.is_contiguous(),
+           "softmax_topk: logits must be contiguous f32 [B, C]")
+    B, C = logits.shape
+    _check(C <= 4096 and 1 <= k <= min(16, C), "softmax_topk: C <= 4096 and 1 <= k <= 16")
+    out = torch.empty(B, 2 * k, device=logits.device, dtype=torch.float32)
+    _ops().softmax_topk(logits.data_ptr(), B, C, k, out.data_ptr(), 0, _stream())
+    return out
+
+
 def softmax_topk_ref(logits, k):
     p = torch.softmax(logits.float(), dim=-1)
     v, i = torch.topk(p, k, dim=-1)
@@ -950,15 +962,22 @@ def image_to_nhwc(img_u8: torch.Tensor, Cp: int = 8) -> torch.Tensor:
     return out
 
 
-def image_to_s2d(img_u8: torch.Tensor) -> torch.Tensor:
+def image_to_s2d(img_u8: torch.Tensor, zero: Optional[torch.Tensor] = None) -> torch.Tensor:
     """uint8 [N, H, W, 3] -> normalised f16 space-to-depth [N, H/2, W/2, 16]
-    (channel (dy*2+dx)*3 + c = pixel (2i+dy, 2j+dx) channel c; 12..15 zero)."""
+    (channel (dy*2+dx)*3 + c = pixel (2i+dy, 2j+dx) channel c; 12..15 zero).
+    ``zero``: a split-K workspace (``splitk_workspace(..., zeroed=False)``) whose
+    counter header the same kernel zeroes -- no separate memset per forward."""
     _check(img_u8.is_cuda and img_u8.dtype == torch.uint8 and img_u8.is_contiguous() and img_u8.shape[-1] == 3,
            "image_to_s2d: bad input")
     N, H, W, _ = img_u8.shape
-    _check(H % 2 == 0 and W % 2 == 0, "image_to_s2d: H and W must be even")
+    _check(H % 2 == 0 and W % 4 == 0, "image_to_s2d: H must be even and W a multiple of 4")
     out = torch.empty(N, H // 2, W // 2, 16, device=img_u8.device, dtype=torch.float16)
-    _ops().image_to_s2d(img_u8.data_ptr(), N, H, W, out.data_ptr(), _stream())
+    zb = 0
+    if zero is not None:
+        _check(zero.is_cuda and zero.dtype == torch.uint8 and zero.numel() >= SPLITK_HEADER and _aligned(zero),
+               "image_to_s2d: zero must be a split-K workspace")
+        zb = SPLITK_HEADER
+    _ops().image_to_s2d(img_u8.data_ptr(), N, H, W, out.data_ptr(), _ptr(zero), zb, _stream())
     return out
 
 
@@ -1014,13 +1033,15 @@ _TILE_BN = (128, 128, 64, 64, 192, 128, 128, 256, 144, 96, 96, 144, 48)
 _tune_ws: Dict[int, torch.Tensor] = {}
 
 
-def splitk_workspace(device, nbytes: int = SPLITK_WS_BYTES) -> torch.Tensor:
+def splitk_workspace(device, nbytes: int = SPLITK_WS_BYTES, zeroed: bool = True) -> torch.Tensor:
     """A split-K workspace: zeroed tile counters + f32 partial tiles.  Every
     split-K launch leaves the counters zero again, so one workspace serves the
     consecutive convolutions of a forward; two launches that may overlap (two
-    streams) need two workspaces."""
+    streams) need two workspaces.  ``zeroed=False``: the caller zeroes the
+    counter header itself before the first split-K launch (``image_to_s2d(zero=)``)."""
     ws = torch.empty(nbytes, device=device, dtype=torch.uint8)
-    ws[:SPLITK_HEADER].zero_()
+    if zeroed:
+        ws[:SPLITK_HEADER].zero_()
     return ws
 
 

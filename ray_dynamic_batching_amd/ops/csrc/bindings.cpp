@@ -44,7 +44,7 @@ void rope(uintptr_t qkv, int ld, int q_off, int k_off, int H, int Hkv, int D, in
           uintptr_t sin_t, int T, int pos_offset, uintptr_t stream);
 void gather_rows(uintptr_t src_ptrs, int n, int rows, int row_bytes, uintptr_t dst, uintptr_t stream);
 void image_to_nhwc(uintptr_t src, int N, int HW, int Cp, uintptr_t dst, uintptr_t stream);
-void image_to_s2d(uintptr_t src, int N, int H, int W, uintptr_t dst, uintptr_t stream);
+void image_to_s2d(uintptr_t src, int N, int H, int W, uintptr_t dst, uintptr_t zero, long zero_bytes, uintptr_t stream);
 void conv2d_nhwc(uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t res, uintptr_t y, int N, int H,
                  int W, int C, int K, int R, int S, int stride, int pad, int P, int Q, int act,
                  uintptr_t stream, int force_cfg, uintptr_t ws, size_t ws_bytes);

@@ -126,6 +126,7 @@ struct DenseLoader {
       rowoff[i] = gm < p.M ? (uint32_t)((size_t)gm * p.lda * sizeof(T)) : kOOB;
     }
   }
+  __device__ __forceinline__ void prep(int) {}
   __device__ __forceinline__ uint32_t offset(int i, int k0) const {
     const int gk = k0 + chunk[i] * 8;
     return (gk < K && rowoff[i] != kOOB) ? rowoff[i] + (uint32_t)(gk * sizeof(T)) : kOOB;
@@ -143,9 +144,16 @@ struct Im2colLoader {
   __amdgpu_buffer_rsrc_t rsrc;
   uint32_t imgoff[NCH];
   int h0[NCH], w0[NCH], chunk[NCH];
+  int pix[NCH];        // fast path: (h0 * W + w0) * C + chunk * 8 (elements from the image base)
   int K, C, S, H, W;
+  // C % 64 == 0 (every ResNet conv but the stem): a 64-deep K step lies inside
+  // one filter tap, so (r, s, c0) are block-uniform -- decomposed ONCE per K
+  // step by prep() instead of two integer divisions per lane and chunk
+  bool fast;
+  int ur, us, uoff;
   __device__ __forceinline__ void init(const Params& p, int tid, int m0) {
     K = p.K; C = p.C; S = p.S; H = p.H; W = p.W;
+    fast = (p.C & 63) == 0;
     rsrc = make_rsrc(p.x, (uint32_t)((size_t)p.N * p.H * p.W * p.C * sizeof(T)));
 #pragma unroll
     for (int i = 0; i < NCH; ++i) {
@@ -158,10 +166,24 @@ struct Im2colLoader {
       const int pp = rem / p.Q, qq = rem - pp * p.Q;
       h0[i] = gm < p.M ? pp * p.stride - p.pad : -(1 << 20);
       w0[i] = qq * p.stride - p.pad;
+      pix[i] = gm < p.M ? ((pp * p.stride - p.pad) * p.W + w0[i]) * p.C + chunk[i] * 8 : 0;
       imgoff[i] = (uint32_t)((size_t)n * p.H * p.W * p.C * sizeof(T));
     }
   }
+  __device__ __forceinline__ void prep(int k0) {
+    if (fast) {
+      const int rs = k0 / C, c0 = k0 - rs * C;
+      ur = rs / S;
+      us = rs - ur * S;
+      uoff = (ur * W + us) * C + c0;
+    }
+  }
   __device__ __forceinline__ uint32_t offset(int i, int k0) const {
+    if (fast) {
+      const int h = h0[i] + ur, w = w0[i] + us;
+      const bool ok = k0 < K && (unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W;
+      return ok ? imgoff[i] + (uint32_t)((pix[i] + uoff) * (int)sizeof(T)) : kOOB;
+    }
     const int gk = k0 + chunk[i] * 8;
     const int rs = gk / C;
     const int cc = gk - rs * C;
@@ -813,6 +835,7 @@ mfma_gemm_kernel(typename LoaderT<T, 1>::Params ap, const T* __restrict__ W, int
   const int wid_u = __builtin_amdgcn_readfirstlane(wid);
   auto stage = [&](int buf, int k0) {
     char* base = smem + buf * kStage;
+    la.prep(k0);
 #pragma unroll
     for (int i = 0; i < A_CH; ++i) dma16(la.rsrc, base + (wid_u * A_CH + i) * 1024, la.offset(i, k0));
 #pragma unroll

@@ -8,6 +8,7 @@
 //                      the H2D step of the replica engine, run on a side stream.
 //   * image_to_nhwc  - uint8 HWC images -> normalised f16 NHWC model input.
 #include "common.h"
+#include <algorithm>
 #include <stdexcept>
 
 namespace rdb {
@@ -63,8 +64,13 @@ softmax_topk_kernel(const float* __restrict__ x, int rows, int C, int k, float* 
       if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
     }
     if (lane == 0) {
-      probs[(size_t)row * k + t] = __expf(best - mx) * inv;
-      idx[(size_t)row * k + t] = bi < C ? bi : -1;
+      if (idx != nullptr) {
+        probs[(size_t)row * k + t] = __expf(best - mx) * inv;
+        idx[(size_t)row * k + t] = bi < C ? bi : -1;
+      } else {   // packed serving output: row = [k probabilities | k class ids as f32]
+        probs[(size_t)row * 2 * k + t] = __expf(best - mx) * inv;
+        probs[(size_t)row * 2 * k + k + t] = (float)(bi < C ? bi : -1);
+      }
     }
 #pragma unroll
     for (int e = 0; e < NV * 4; ++e)
@@ -190,46 +196,68 @@ void image_to_nhwc(uintptr_t src, int N, int HW, int Cp, uintptr_t dst, uintptr_
 // (dy*2 + dx)*3 + c of output pixel (i, j) is input pixel (2i+dy, 2j+dx) channel c,
 // channels 12..15 are zero.  A 7x7 stride-2 stem conv on the image is then a 4x4
 // stride-1 conv on this tensor (ResNet50.stem_w_s2d): 256 reduction elements per
-// output instead of 7*7*8 = 392 with the channel-padded layout.
+// output instead of 7*7*8 = 392 with the channel-padded layout.  Optionally
+// zeroes `zero_bytes` at `zero` (the forward's split-K counters) on the side.
 __global__ void image_to_s2d_kernel(const uint8_t* __restrict__ src, int N, int H, int W,
                                     float m0, float m1, float m2, float s0, float s1, float s2,
-                                    f16* __restrict__ dst) {
-  const int P = H >> 1, Q = W >> 1;
-  const long total = (long)N * P * Q;
+                                    f16* __restrict__ dst, u32x4* __restrict__ zero, int zero_n) {
+  // side job: zero a split-K counter header for the forward this kernel starts
+  {
+    const long z = blockIdx.x * (long)blockDim.x + threadIdx.x;
+    if (z < zero_n) zero[z] = u32x4{0u, 0u, 0u, 0u};
+  }
+  const int P = H >> 1, Q2 = W >> 2;          // a thread makes output pixels (i, 2j) and (i, 2j + 1)
+  const long total = (long)N * P * Q2;
   const float a[3] = {1.f / (255.f * s0), 1.f / (255.f * s1), 1.f / (255.f * s2)};
   const float b[3] = {-m0 / s0, -m1 / s1, -m2 / s2};
   for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
-    const int j = e % Q;
-    const long ni = e / Q;
+    const int j = e % Q2;
+    const long ni = e / Q2;
     const int i = ni % P;
     const int n = ni / P;
-    f16x8 lo, hi;
+    // 12 input bytes per row (4 pixels x RGB), three aligned dword loads (W % 4 == 0)
+    uint32_t raw[2][3];
 #pragma unroll
     for (int dy = 0; dy < 2; ++dy) {
-      const uint8_t* r = src + (((size_t)n * H + 2 * i + dy) * W + 2 * j) * 3;
+      const uint32_t* r = reinterpret_cast<const uint32_t*>(src + (((size_t)n * H + 2 * i + dy) * W + 4 * j) * 3);
 #pragma unroll
-      for (int t = 0; t < 6; ++t) {            // (dx, c) = (t / 3, t % 3)
-        const int ch = dy * 6 + t;
-        const f16 v = (f16)(r[t] * a[t % 3] + b[t % 3]);
-        if (ch < 8) lo[ch] = v; else hi[ch - 8] = v;
-      }
+      for (int t = 0; t < 3; ++t) raw[dy][t] = r[t];
     }
+    f16x8 o[4];   // pixel 2j: o[0], o[1]; pixel 2j + 1: o[2], o[3]
 #pragma unroll
-    for (int c = 4; c < 8; ++c) hi[c] = (f16)0.f;
-    f16x8* d = reinterpret_cast<f16x8*>(dst + (size_t)e * 16);
-    d[0] = lo;
-    d[1] = hi;
+    for (int px = 0; px < 2; ++px) {
+#pragma unroll
+      for (int dy = 0; dy < 2; ++dy) {
+#pragma unroll
+        for (int t = 0; t < 6; ++t) {           // (dx, c) = (t / 3, t % 3): byte 6 px + t of the row
+          const int byte = 6 * px + t;
+          const float u = (float)((raw[dy][byte >> 2] >> (8 * (byte & 3))) & 0xffu);
+          const int ch = dy * 6 + t;
+          o[2 * px + (ch >> 3)][ch & 7] = (f16)(u * a[t % 3] + b[t % 3]);
+        }
+      }
+#pragma unroll
+      for (int c = 4; c < 8; ++c) o[2 * px + 1][c] = (f16)0.f;
+    }
+    f16x8* d = reinterpret_cast<f16x8*>(dst + (size_t)(ni * (W >> 1) + 2 * j) * 16);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) d[q] = o[q];
   }
 }
 
-void image_to_s2d(uintptr_t src, int N, int H, int W, uintptr_t dst, uintptr_t stream) {
+void image_to_s2d(uintptr_t src, int N, int H, int W, uintptr_t dst, uintptr_t zero, long zero_bytes,
+                  uintptr_t stream) {
   if (N <= 0) return;
-  if ((H | W) & 1) throw std::invalid_argument("image_to_s2d: H and W must be even");
-  const long total = (long)N * (H / 2) * (W / 2);
-  int blocks = (int)((total + 255) / 256);
-  blocks = blocks > 8192 ? 8192 : blocks;
-  hipLaunchKernelGGL(image_to_s2d_kernel, dim3(blocks), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
-                     (const uint8_t*)src, N, H, W, 0.485f, 0.456f, 0.406f, 0.229f, 0.224f, 0.225f, (f16*)dst);
+  if ((H & 1) || (W & 3)) throw std::invalid_argument("image_to_s2d: H must be even and W a multiple of 4");
+  if ((src & 3) || (dst & 15) || (zero & 15) || (zero_bytes & 15))
+    throw std::invalid_argument("image_to_s2d: src 4-byte, dst / zero 16-byte aligned; zero_bytes % 16 == 0");
+  const long total = (long)N * (H / 2) * (W / 4);
+  const long zn = zero ? zero_bytes / 16 : 0;
+  long blocks = (std::max(total, zn) + 255) / 256;
+  blocks = blocks > 8192 ? std::max<long>(8192, (zn + 255) / 256) : blocks;
+  hipLaunchKernelGGL(image_to_s2d_kernel, dim3((unsigned)blocks), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+                     (const uint8_t*)src, N, H, W, 0.485f, 0.456f, 0.406f, 0.229f, 0.224f, 0.225f, (f16*)dst,
+                     (u32x4*)zero, (int)zn);
   RDB_HIP_CHECK(hipGetLastError());
 }
 

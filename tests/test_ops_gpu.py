@@ -201,6 +201,9 @@ def test_softmax_topk(C, k):
     pr, ir = ops.softmax_topk_ref(x, k)
     assert torch.equal(i, ir)
     _close(p, pr, 1e-5, 1e-4)
+    packed = ops.softmax_topk_packed(x, k)          # the serving row [k probs | k ids as f32]
+    assert packed.shape == (37, 2 * k)
+    assert torch.equal(packed[:, :k], p) and torch.equal(packed[:, k:], i.float())
     # ties: small integers, many equal maxima -> lowest column wins, like torch.topk on sorted ties
     xt = torch.randint(0, 3, (8, C), device="cuda").float()
     pt, it = ops.softmax_topk(xt, k)
@@ -326,8 +329,13 @@ def test_image_to_s2d_and_space_to_depth_stem():
     cut to 112 x 112) against the 7x7 stride-2 conv of the channel-padded image."""
     ops = _ops()
     img = torch.randint(0, 256, (3, 224, 224, 3), device="cuda", dtype=torch.uint8)
-    xs = ops.image_to_s2d(img)
+    ws = ops.splitk_workspace("cuda", zeroed=False)
+    ws[:ops.SPLITK_HEADER].fill_(0xFF)
+    xs = ops.image_to_s2d(img, zero=ws)             # the side job zeroes the split-K counters
     _close(xs, ops.image_to_s2d_ref(img), 1e-2, 1e-2)
+    assert int(ws[:ops.SPLITK_HEADER].sum()) == 0
+    img2 = torch.randint(0, 256, (2, 36, 20, 3), device="cuda", dtype=torch.uint8)   # a small odd-shaped batch
+    _close(ops.image_to_s2d(img2), ops.image_to_s2d_ref(img2), 1e-2, 1e-2)
     g = torch.Generator().manual_seed(3)
     w = torch.zeros(64, 7, 7, 8, dtype=torch.float16)
     w[..., :3] = (torch.randn(64, 7, 7, 3, generator=g) * (147 ** -0.5)).half()
