@@ -1,7 +1,8 @@
 """Single-GPU serving curves through the native replica engine:
 req/s vs p50/p99 latency for any servable model of the zoo.
 
-BASELINE config 2 (ResNet-50 fp16, 1 GPU, dyn-batch <= 32 / 5 ms, Poisson):
+BASELINE config 2 (ResNet-50 fp16, 1 GPU, dyn-batch <= 32 / 5 ms, Poisson; one
+replica engine running two batches at a time on two compute streams, like bench.py):
     python bench/serve_bench.py --model resnet50 --rates 2000,4000,8000,12000
 Closed-loop saturation throughput:
     python bench/serve_bench.py --model bert-base --closed 96
@@ -31,8 +32,8 @@ def main(argv=None):
     ap.add_argument("--max-batch", type=int, default=32)
     ap.add_argument("--max-wait-ms", type=float, default=5.0)
     ap.add_argument("--backend", default="hip")
-    ap.add_argument("--pipeline-depth", type=int, default=2)
-    ap.add_argument("--compute-streams", type=int, default=1, help="batches executing concurrently on the GPU")
+    ap.add_argument("--pipeline-depth", type=int, default=4)
+    ap.add_argument("--compute-streams", type=int, default=2, help="batches executing concurrently on the GPU")
     ap.add_argument("--json-out", default="")
     a = ap.parse_args(argv)
 
@@ -46,8 +47,11 @@ def main(argv=None):
     torch.cuda.set_device(0)
     # replay the tile table shipped for this (model, max batch, depth) when there is one
     # (ops/tuned/README.md); RDB_TUNE_FILE set by the caller wins
-    shipped = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "ray_dynamic_batching_amd",
-                           "ops", "tuned", f"mi355x_{a.model}_B{a.max_batch}_d{a.pipeline_depth}.json")
+    tuned = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "ray_dynamic_batching_amd",
+                         "ops", "tuned")
+    shipped = os.path.join(tuned, f"mi355x_{a.model}_B{a.max_batch}_cs{a.compute_streams}_d{a.pipeline_depth}.json")
+    if not os.path.exists(shipped) and a.compute_streams == 1:
+        shipped = os.path.join(tuned, f"mi355x_{a.model}_B{a.max_batch}_d{a.pipeline_depth}.json")   # round-3 name
     if a.backend == "hip" and "RDB_TUNE_FILE" not in os.environ and os.path.exists(shipped):
         os.environ["RDB_TUNE_FILE"] = shipped
     m = models.create(a.model, device="cuda", backend=a.backend)
