@@ -35,7 +35,7 @@ def main(argv=None):
     w = torch.randn(a.n, a.k, device="cuda", dtype=torch.bfloat16) * 0.05
     b = torch.randn(a.n, device="cuda", dtype=torch.bfloat16) if a.bias else None
     r = torch.randn(a.m, a.n, device="cuda", dtype=torch.bfloat16) if a.res else None
-    cfgs = range(ops.NUM_TILE_CFGS) if a.cfg < 0 else [a.cfg]
+    cfgs = (list(range(ops.NUM_TILE_CFGS)) + [c | ops.DEEP for c in ops._DEEP_TILES]) if a.cfg < 0 else [a.cfg]
     out = {}
 
     def timed(fn) -> float:

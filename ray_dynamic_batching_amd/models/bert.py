@@ -398,8 +398,9 @@ class BertForSequenceClassification:
             lnr = None if xst is None else (xst, xg, xb, D, eps)
             a, ast = ops.linear_ln_staged(ctx, L["w_o"], L["b_o"], residual=x, lnr=lnr, pstats=True)
             inter = ops.linear_ln_staged(a, d["w_i"], act="gelu", lna=(ast, d["cs_i"], d["b_i"], D, eps))
+            # its partials feed the next layer's fused QKV+attention (at most 8 per row)
             o, ost = ops.linear_ln_staged(inter, L["w_out"], L["b_out"], residual=a,
-                                          lnr=(ast, L["ln1_g"], L["ln1_b"], D, eps), pstats=True)
+                                          lnr=(ast, L["ln1_g"], L["ln1_b"], D, eps), pstats=True, max_parts=8)
             x, xst, xg, xb = o, ost, L["ln2_g"], L["ln2_b"]
         if h is None:
             h = ops.layer_norm(x, xg, xb, eps) if xst is not None else x

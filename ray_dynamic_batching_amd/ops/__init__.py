@@ -193,6 +193,16 @@ def _tuned_cfg(key: tuple, launch: Callable[[int], None], candidates=range(NUM_T
 # ---------------------------------------------------------------------------
 # GEMM (+ fused bias / activation / residual epilogue)
 # ---------------------------------------------------------------------------
+def _gemm_candidates(M: int, N: int, K: int):
+    """Dense GEMM tile choices: every tile cfg, plus the DEEP variants of the
+    4-wave tiles whose grid is about one block per CU (``DEEP`` flag)."""
+    cands = list(range(NUM_TILE_CFGS))
+    if _GEMM_DEEP and K >= 256:
+        cands += [c | DEEP for c in _DEEP_TILES
+                  if -(-M // _TILE_BM[c]) * -(-N // _TILE_BN[c]) <= _DEEP_MAX_BLOCKS]
+    return cands
+
+
 def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, act: str = "none",
            residual: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None,
            out_dtype: Optional[torch.dtype] = None, alpha: float = 1.0, tile_cfg: int = -1) -> torch.Tensor:
@@ -237,7 +247,8 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
     skinny = M <= SKINNY_MAX_M and K % 32 == 0 and act != "swiglu"   # C++ routes these to the skinny-M kernel
     if tile_cfg < 0 and od != torch.float32 and not skinny:
         key = ("gemm", x.dtype, M, N, K, lda, act, bias is not None, residual is not None)
-        tile_cfg = _tuned_cfg(key, lambda c: fn(*args, _stream(), c))
+        tile_cfg = _tuned_cfg(key, lambda c: fn(*args, _stream(), c),
+                              _gemm_candidates(M, N, K) if act != "swiglu" else range(NUM_TILE_CFGS))
     fn(*args, _stream(), int(tile_cfg))
     return out
 
@@ -303,7 +314,7 @@ def _stats_ld(st: torch.Tensor, M: int, what: str) -> int:
 def linear_ln_staged(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, act: str = "none",
                      residual: Optional[torch.Tensor] = None, lna: Optional[tuple] = None,
                      lnr: Optional[tuple] = None, pstats: bool = False, out: Optional[torch.Tensor] = None,
-                     tile_cfg: int = -1):
+                     tile_cfg: int = -1, max_parts: int = _PSTATS_MAX):
     """The deferred-LayerNorm GEMM on the STAGED epilogue with partial statistics
     (gemm_core.h EPI_STG; ping-pong and 4-wave tiles):
 
@@ -315,7 +326,9 @@ def linear_ln_staged(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tens
       ``stats``), added as LayerNorm(residual).
     * ``pstats=True``: also returns this GEMM's output statistics as partials
       [M, P, 2] (P = N-tiles of the tile it ran): ``(out, stats)``.  No zeroing,
-      no atomics: each N-tile writes its own partial.
+      no atomics: each N-tile writes its own partial.  ``max_parts``: only tiles
+      with at most that many N-tiles (a consumer's limit, e.g. 8 for
+      ``qkv_attention(a_stats=...)``).
     """
     _check(x.is_cuda and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16, "linear_ln_staged: bf16 on the GPU")
     _check(w.dim() == 2 and w.is_contiguous(), "linear_ln_staged: w must be a contiguous [N, K] matrix")
@@ -369,10 +382,18 @@ def linear_ln_staged(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tens
            _ptr(o_buf), 2 * _PSTATS_MAX if pstats else 0, float(a_inv), float(r_inv), float(eps), _stream(), c,
            0, 0, a_parts, r_parts)
 
+    def parts(c):
+        return -(-N // int(_ops().gemm_tile_bn(int(_ops().gemm_stg_cfg(int(c))))))
+
+    cands = [c for c in STG_TILE_CFGS if not pstats or parts(c) <= max_parts]
+    _check(len(cands) > 0, f"linear_ln_staged: no tile writes <= {max_parts} partials for N = {N}")
     if tile_cfg < 0:
-        key = ("gemm_stg", x.dtype, M, N, K, lda, act, mode, a_parts, r_parts)
-        tile_cfg = _tuned_cfg(key, launch, STG_TILE_CFGS)
+        key = ("gemm_stg", x.dtype, M, N, K, lda, act, mode, a_parts, r_parts) + \
+            ((max_parts,) if pstats and max_parts < _PSTATS_MAX else ())
+        tile_cfg = _tuned_cfg(key, launch, cands)
     tile_cfg = int(_ops().gemm_stg_cfg(int(tile_cfg)))
+    if tile_cfg not in cands:
+        tile_cfg = int(_ops().gemm_stg_cfg(int(cands[0])))
     launch(tile_cfg)
     if not pstats:
         return out
@@ -1020,11 +1041,17 @@ def image_to_nhwc_ref(img_u8, Cp=8):
 _CONV1X1_GEMM = os.environ.get("RDB_CONV1X1_GEMM", "1") != "0"
 # RDB_CONV_SPLITK=0: no split-K candidates
 _CONV_SPLITK = os.environ.get("RDB_CONV_SPLITK", "1") != "0"
+# RDB_GEMM_DEEP=0: no DEEP (one block per CU, many LDS stages) tile candidates
+_GEMM_DEEP = os.environ.get("RDB_GEMM_DEEP", "1") != "0"
 # Encoded conv tile choices (what the tuner / tile tables store):
 #   cfg                  4-wave tile cfg (0..12) of the implicit-GEMM conv kernel
 #   cfg | splits << 8    the same tile, split-K over `splits` workgroups per tile
 #   CONV_LINEAR | cfg    (1x1 / stride 1) the dense GEMM `linear` on tile cfg (0..25)
+#   ... | DEEP           tiles 0, 1, 2, 3, 9, 10 with one block per CU and up to 8 LDS stages
 CONV_LINEAR = 1 << 16
+DEEP = 1 << 12                        # gemm_core.h kDeepFlag: one block per CU, up to 8 LDS stages
+_DEEP_TILES = (0, 1, 2, 3, 9, 10)
+_DEEP_MAX_BLOCKS = 320                # DEEP candidates only where the grid is ~one block per CU
 SPLITK_HEADER = 65536                 # gemm_core.h kSplitKHeader (tile arrival counters)
 SPLITK_WS_BYTES = 40 << 20            # one forward's split-K workspace (ops.splitk_workspace)
 _SPLITS = (2, 3, 4, 6, 8)
@@ -1051,9 +1078,15 @@ def _conv_candidates(M: int, K_out: int, Kg: int, one_by_one: bool):
     per CU) and each split keeps >= 4 K-steps; the dense GEMM tiles for 1x1."""
     cands = list(range(NUM_CONV_TILE_CFGS))
     nk = -(-Kg // 64)
+
+    def tiles_of(c):
+        return -(-M // _TILE_BM[c]) * -(-K_out // _TILE_BN[c])
+
+    if _GEMM_DEEP:
+        cands += [c | DEEP for c in _DEEP_TILES if tiles_of(c) <= _DEEP_MAX_BLOCKS and nk >= 4]
     if _CONV_SPLITK:
         for c in range(NUM_CONV_TILE_CFGS):
-            tiles = -(-M // _TILE_BM[c]) * -(-K_out // _TILE_BN[c])
+            tiles = tiles_of(c)
             if tiles >= 512:
                 continue
             for sp in _SPLITS:
@@ -1064,8 +1097,10 @@ def _conv_candidates(M: int, K_out: int, Kg: int, one_by_one: bool):
                 if SPLITK_HEADER + tiles * eff * _TILE_BM[c] * _TILE_BN[c] * 4 > SPLITK_WS_BYTES:
                     continue
                 cands.append(c | (sp << 8))
+                if _GEMM_DEEP and c in _DEEP_TILES and tiles * eff <= _DEEP_MAX_BLOCKS and kper >= 4:
+                    cands.append(c | (sp << 8) | DEEP)
     if one_by_one and _CONV1X1_GEMM and K_out % 8 == 0:
-        cands += [CONV_LINEAR | c for c in range(NUM_TILE_CFGS)]
+        cands += [CONV_LINEAR | c for c in _gemm_candidates(M, K_out, Kg)]
     return cands
 
 

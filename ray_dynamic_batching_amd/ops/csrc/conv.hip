@@ -11,7 +11,7 @@
 
 namespace rdb {
 
-// force_cfg = tile | (splits << 8): splits > 1 runs split-K on the workspace
+// force_cfg = tile | (splits << 8) [| kDeepFlag]: splits > 1 runs split-K on the workspace
 // `ws` (ws_bytes; zeroed counter header, see splitk_bytes) when it fits, else unsplit.
 void conv2d_nhwc(uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t res, uintptr_t y, int N, int H,
                  int W, int C, int K, int R, int S, int stride, int pad, int P, int Q, int act,
@@ -22,9 +22,10 @@ void conv2d_nhwc(uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t res, uintpt
     throw std::invalid_argument("conv2d_nhwc: P / Q larger than the padded output");
   const int M = N * P * Q, Kg = R * S * C;
   if (M <= 0 || K <= 0) return;
-  const int cfg = force_cfg < 0 ? -1 : (force_cfg & 255);
-  const int splits = force_cfg < 0 ? 1 : (force_cfg >> 8);
-  const LnEpi sk = splitk_epi(M, K, Kg, cfg, splits, reinterpret_cast<void*>(ws), ws_bytes);
+  const int tile = force_cfg < 0 ? -1 : (force_cfg & 255);
+  const int splits = force_cfg < 0 ? 1 : ((force_cfg >> 8) & 15);
+  const int cfg = force_cfg < 0 ? -1 : (tile | (force_cfg & kDeepFlag));
+  const LnEpi sk = splitk_epi(M, K, Kg, tile, splits, reinterpret_cast<void*>(ws), ws_bytes);
   ConvParams p{reinterpret_cast<const void*>(x), N, H, W, C, R, S, stride, pad, P, Q, M, Kg};
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   if (R == 1 && S == 1 && stride == 1 && pad == 0) {

@@ -767,8 +767,8 @@ __device__ __forceinline__ bool staged_epilogue_ok(int N, const OutT* C, int ldc
 // which is what the L2-bandwidth-bound BERT shapes need (FFN2 at 128x48 moves
 // ~14 TB/s through L2 for 0.5 PF).
 template <typename T, typename OutT, int BM, int BN, template <typename, int> class LoaderT, bool HAS_BIAS,
-          bool HAS_RES, int WGM = 2, int NW = 4, int EPI = 0>
-__global__ void __launch_bounds__(64 * NW, NW == 4 ? 2 : 1)
+          bool HAS_RES, int WGM = 2, int NW = 4, int EPI = 0, int DEEP = 0>
+__global__ void __launch_bounds__(64 * NW, (NW == 4 && !DEEP) ? 2 : 1)
 mfma_gemm_kernel(typename LoaderT<T, 1>::Params ap, const T* __restrict__ W, int ldw,
                  OutT* __restrict__ C, int ldc, const T* __restrict__ bias,
                  const T* __restrict__ R, int ldr, int M, int N, int K, float alpha, int act, LnEpi ln) {
@@ -795,8 +795,14 @@ mfma_gemm_kernel(typename LoaderT<T, 1>::Params ap, const T* __restrict__ W, int
   constexpr int BNP = W_CH * 8 * NW;
   constexpr int kStage = (BM + BNP) * BK * 2;  // bytes per LDS stage (A tile, then W tile)
   // Three LDS stages (two K-tiles in flight across each barrier) whenever they
-  // still fit two blocks per CU; the big tiles keep two stages.
-  constexpr int kStages = (3 * kStage <= (NW == 4 ? 80 : 160) * 1024) ? 3 : 2;
+  // still fit two blocks per CU; the big tiles keep two stages.  DEEP: one
+  // block per CU with up to 8 stages in ~150 KiB of LDS -- for grids of at most
+  // ~one tile per CU, where a lone block otherwise waits out the DMA latency
+  // every K step (a 128x128 tile has 2 stages: 1.75 us per K step measured on
+  // the ResNet-50 layer-3 convolutions, ~10 % MFMA busy)
+  constexpr int kStages = DEEP ? ((152 * 1024) / kStage < 8 ? (152 * 1024) / kStage : 8)
+                               : ((3 * kStage <= (NW == 4 ? 80 : 160) * 1024) ? 3 : 2);
+  static_assert(kStages >= 2, "LDS stages");
   typedef typename MfmaOp<T>::frag frag;
 
   constexpr int LN_OFF = kStages * kStage;
@@ -924,22 +930,26 @@ mfma_gemm_kernel(typename LoaderT<T, 1>::Params ap, const T* __restrict__ W, int
     // makes every wave's pieces of tile k visible.  Buffer (k+2)%3 was last
     // read by compute(k-1), which every wave finished before this barrier, so
     // it is refilled right after it (WAR-safe).
+    // (kStages > 3, DEEP: kStages - 1 tiles in flight, the same protocol)
     constexpr int kLoads = A_CH + W_CH;                  // DMA instructions per wave per stage
-    constexpr int kWaitOne = (kLoads & 15) | ((kLoads >> 4) << 14) | 0x70 | 0xF00;  // vmcnt(kLoads)
-    constexpr int kWaitAll = 0x70 | 0xF00;                                             // vmcnt(0)
-    static_assert(kLoads < 64, "vmcnt field is 6 bits");
-    stage(0, kb * BK);
-    if (nk > 1) stage(1, (kb + 1) * BK);
+    constexpr int kPend = kLoads * (kStages - 2);        // younger tiles' DMAs left pending
+    constexpr int kWaitPend = (kPend & 15) | ((kPend >> 4) << 14) | 0x70 | 0xF00;   // vmcnt(kPend)
+    constexpr int kWaitAll = 0x70 | 0xF00;                                           // vmcnt(0)
+    static_assert(kPend < 64, "vmcnt field is 6 bits");
+#pragma unroll
+    for (int p = 0; p < kStages - 1; ++p)
+      if (p < nk) stage(p, (kb + p) * BK);
     int buf = 0;
     for (int kt = 0; kt < nk; ++kt) {
-      if (kt + 1 < nk) __builtin_amdgcn_s_waitcnt(kWaitOne);
-      else __builtin_amdgcn_s_waitcnt(kWaitAll);
+      if (kt + kStages - 2 < nk) __builtin_amdgcn_s_waitcnt(kWaitPend);
+      else __builtin_amdgcn_s_waitcnt(kWaitAll);       // the tail: fewer younger tiles in flight
       asm volatile("" ::: "memory");
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
-      if (kt + 2 < nk) stage(buf == 0 ? 2 : buf - 1, (kb + kt + 2) * BK);
+      if (kt + kStages - 1 < nk)
+        stage(buf == 0 ? kStages - 1 : buf - 1, (kb + kt + kStages - 1) * BK);
       compute(buf, (kb + kt) * BK);
-      buf = buf == 2 ? 0 : buf + 1;
+      buf = buf == kStages - 1 ? 0 : buf + 1;
     }
     __syncthreads();
   }
@@ -1213,6 +1223,9 @@ constexpr int kNumTiles = 26;
 //                                 0    1    2    3    4    5    6    7    8    9   10   11   12 | 8-wave: 13   14   15   16   17   18 | pp: 19   20   21   22   23   24   25
 constexpr int kTileBM[kNumTiles] = {128, 64, 128, 64, 128, 192, 256, 128, 128, 64, 128, 256, 128, 256, 128, 256, 256, 128, 256, 256, 256, 128, 256, 256, 256, 256};
 constexpr int kTileBN[kNumTiles] = {128, 128, 64, 64, 192, 128, 128, 256, 144, 96, 96, 144, 48, 128, 256, 192, 144, 96, 96, 128, 144, 256, 256, 128, 192, 192};
+// tile cfg flag: the DEEP (one block per CU, up to 8 LDS stages) variant of
+// 4-wave tiles 0, 1, 2, 3, 9, 10 (plain epilogues); other tiles ignore it
+constexpr int kDeepFlag = 1 << 12;
 constexpr int kTileWGM[kNumTiles] = {2, 2, 2, 2, 2, 2, 2, 2, 4, 2, 2, 4, 4, 4, 2, 4, 8, 4, 8, 4, 8, 2, 4, 4, 4, 4};
 constexpr int kTileNW[kNumTiles] = {4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 8, 8, 8, 8, 8, 8, 8, 8, 8, 8, 8, 8, 8};
 
@@ -1263,7 +1276,7 @@ inline int pick_tile_cfg(int M, int N, bool dense) {
 }
 
 template <typename T, typename OutT, template <typename, int> class LoaderT, bool HB, bool HR, int BM, int BN,
-          int WGM = 2, int NW = 4, int EPI = 0, typename P>
+          int WGM = 2, int NW = 4, int EPI = 0, int DEEP = 0, typename P>
 void launch_one(const P& ap, const T* W, int ldw, OutT* C, int ldc, const T* bias, const T* R, int ldr, int M,
                 int N, int K, float alpha, int act, hipStream_t s, const LnEpi& ln = LnEpi{}) {
   const int nwg = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
@@ -1274,7 +1287,7 @@ void launch_one(const P& ap, const T* W, int ldw, OutT* C, int ldc, const T* bia
     const int nk = (K + 63) / 64;
     splits = (nk + ln.sk_kper - 1) / ln.sk_kper;
   }
-  hipLaunchKernelGGL((mfma_gemm_kernel<T, OutT, BM, BN, LoaderT, HB, HR, WGM, NW, EPI>), dim3(nwg, splits),
+  hipLaunchKernelGGL((mfma_gemm_kernel<T, OutT, BM, BN, LoaderT, HB, HR, WGM, NW, EPI, DEEP>), dim3(nwg, splits),
                      dim3(64 * NW), 0, s, ap, W, ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act, ln);
 }
 
@@ -1283,6 +1296,9 @@ template <typename T, typename OutT, template <typename, int> class LoaderT, boo
 void launch_mfma_gemm_t(const P& ap, const T* W, int ldw, OutT* C, int ldc, const T* bias, const T* R,
                         int ldr, int M, int N, int K, float alpha, int act, hipStream_t s, int cfg,
                         const LnEpi& ln = LnEpi{}) {
+  const bool deep = cfg >= 0 && (cfg & kDeepFlag) != 0;
+  (void)deep;
+  if (cfg >= 0) cfg &= 0xFF;
 #define RDB_TILE(IDX, BM_, BN_, WGM_, NW_)                                                                    \
   case IDX:                                                                                                  \
     launch_one<T, OutT, LoaderT, HB, HR, BM_, BN_, WGM_, NW_, EPI>(ap, W, ldw, C, ldc, bias, R, ldr, M, N, K, \
@@ -1320,6 +1336,25 @@ void launch_mfma_gemm_t(const P& ap, const T* W, int ldw, OutT* C, int ldc, cons
     // the ping-pong tiles (19..) take plain staged epilogues only: deferred-LN modes,
     // SwiGLU and unaligned / N % 8 != 0 outputs run the 8-wave 256x192 tile instead
     if (cfg >= 19 && (EPI != 0 || !gemm_pp_ok(N, ldc, ldr, C, bias, R, act))) cfg = 15;
+    if constexpr (EPI == 0 && sizeof(OutT) == 2) {
+      if (deep) {
+#define RDB_TILE_DEEP(IDX, BM_, BN_)                                                                             \
+  case IDX:                                                                                                      \
+    launch_one<T, OutT, LoaderT, HB, HR, BM_, BN_, 2, 4, 0, 1>(ap, W, ldw, C, ldc, bias, R, ldr, M, N, K, alpha, \
+                                                              act, s, ln);                                       \
+    return;
+        switch (cfg) {
+          RDB_TILE_DEEP(0, 128, 128)
+          RDB_TILE_DEEP(1, 64, 128)
+          RDB_TILE_DEEP(2, 128, 64)
+          RDB_TILE_DEEP(3, 64, 64)
+          RDB_TILE_DEEP(9, 64, 96)
+          RDB_TILE_DEEP(10, 128, 96)
+          default: break;
+        }
+#undef RDB_TILE_DEEP
+      }
+    }
     switch (cfg) {
       RDB_TILE(0, 128, 128, 2, 4)
       RDB_TILE(1, 64, 128, 2, 4)
@@ -1411,9 +1446,12 @@ void launch_mfma_gemm(const P& ap, const T* W, int ldw, OutT* C, int ldc, const 
                       int ldr, int M, int N, int K, float alpha, int act, hipStream_t s, int cfg,
                       const LnEpi& ln = LnEpi{}) {
   constexpr bool dense = std::is_same<LoaderT<T, 1>, DenseLoader<T, 1>>::value;
+  const int deep = (cfg >= 0 && (cfg & kDeepFlag) != 0) ? kDeepFlag : 0;
+  if (cfg >= 0) cfg &= 0xFF;
   if (cfg < 0 || cfg >= (dense ? kNumTiles : kNumTiles4)) cfg = pick_tile_cfg(M, N, dense);
   // split-K runs on the 4-wave tiles (0..12) only: their kernel carries the hand-off
   const LnEpi e = (ln.sk_kper > 0 && cfg < kNumTiles4 && act != ACT_SWIGLU) ? ln : LnEpi{};
+  cfg |= deep;
   if (bias && R)
     launch_mfma_gemm_t<T, OutT, LoaderT, true, true>(ap, W, ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act, s, cfg, e);
   else if (bias)

@@ -264,6 +264,12 @@ def test_conv2d_splitk(N, H, C, K, R, stride, pad):
             _close(ops.conv2d_nhwc(x, w, b, stride=stride, pad=pad, act="relu", tile_cfg=c, workspace=ws), ref, 2e-2, 2e-2)
             _close(ops.conv2d_nhwc(x, w, b, stride=stride, pad=pad, act="relu", residual=r, tile_cfg=c, workspace=ws),
                    ref_r, 2e-2, 2e-2)
+    # DEEP tiles (one block per CU, up to 8 LDS stages), alone and split
+    for c in (0 | ops.DEEP, 1 | ops.DEEP, 10 | ops.DEEP, 3 | (2 << 8) | ops.DEEP, 0 | (3 << 8) | ops.DEEP):
+        if (c >> 8) & 15 and -(-nk // -(-nk // ((c >> 8) & 15))) < 2:
+            continue
+        _close(ops.conv2d_nhwc(x, w, b, stride=stride, pad=pad, act="relu", residual=r, tile_cfg=c, workspace=ws),
+               ref_r, 2e-2, 2e-2)
     # without a workspace: a private one
     _close(ops.conv2d_nhwc(x, w, b, stride=stride, pad=pad, act="relu", tile_cfg=0 | (2 << 8)), ref, 2e-2, 2e-2)
     torch.cuda.synchronize()
@@ -271,6 +277,23 @@ def test_conv2d_splitk(N, H, C, K, R, stride, pad):
     if R == 1 and stride == 1:
         for c in (0, 10, 19, 23):
             _close(ops.conv2d_nhwc(x, w, b, act="relu", residual=r, tile_cfg=ops.CONV_LINEAR | c), ref_r, 2e-2, 2e-2)
+
+
+@pytest.mark.parametrize("M,N,K", [(4096, 768, 768), (512, 768, 3072), (1000, 520, 1160)])
+def test_linear_deep_tiles(M, N, K):
+    """The DEEP 4-wave tiles (kStages up to 8, one block per CU; K tails and
+    ragged M / N edges included) against the fp32 reference."""
+    ops = _ops()
+    torch.manual_seed(M + K)
+    x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    w = torch.randn(N, K, device="cuda", dtype=torch.bfloat16) * K ** -0.5
+    b = torch.randn(N, device="cuda", dtype=torch.bfloat16) * 0.1
+    r = torch.randn(M, N, device="cuda", dtype=torch.bfloat16)
+    ref = torch.nn.functional.gelu(x.float() @ w.float().t() + b.float())
+    ref_r = x.float() @ w.float().t() + b.float() + r.float()
+    for c in (0, 1, 2, 3, 9, 10):
+        _close(ops.linear(x, w, b, act="gelu", tile_cfg=c | ops.DEEP), ref, 2e-2, 2e-2)
+        _close(ops.linear(x, w, b, residual=r, tile_cfg=c | ops.DEEP), ref_r, 2e-2, 2e-2)
 
 
 def test_conv2d_splitk_graph_replay():
