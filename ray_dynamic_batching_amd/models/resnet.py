@@ -60,6 +60,8 @@ class ResNet50:
         # the stem on the space-to-depth image: 4x4 / stride-1 conv, 256 reduction
         # elements per output instead of 392 (RDB_RESNET_S2D=0: the 7x7 conv)
         self.stem_s2d = os.environ.get("RDB_RESNET_S2D", "1") != "0"
+        # ... and fused with the max-pool and the image conversion (RDB_RESNET_STEM_FUSED=0: three kernels)
+        self.stem_fused = os.environ.get("RDB_RESNET_STEM_FUSED", "1") != "0"
         self.stem_w_s2d = ops.stem_weight_s2d(self.stem_w)
         self.blocks: List[dict] = []
         cin = 64
@@ -161,15 +163,21 @@ class ResNet50:
         # one split-K workspace per forward (its tile counters zeroed once, by the
         # first kernel; the convolutions of the forward run one after another on its stream)
         s2d = self.stem_s2d and img.shape[1] % 2 == 0 and img.shape[2] % 4 == 0
+        fused = s2d and self.stem_fused and img.shape[1] % 32 == 0 and img.shape[2] % 32 == 0
         ws = ops.splitk_workspace(img.device, zeroed=not s2d)
-        if s2d:
-            x = ops.image_to_s2d(img, zero=ws)          # also zeroes the workspace's counters
-            x = ops.conv2d_nhwc(x, self.stem_w_s2d, self.stem_b, stride=1, pad=2, act="relu",
-                                out_hw=(img.shape[1] // 2, img.shape[2] // 2), workspace=ws)
+        if fused:
+            # image -> space-to-depth -> stem conv -> ReLU -> max-pool in one kernel
+            # (the 112x112x64 stem activation never reaches HBM); also zeroes ws
+            x = ops.stem_s2d_pool(img, self.stem_w_s2d, self.stem_b, zero=ws)
         else:
-            x = ops.image_to_nhwc(img, 8)
-            x = ops.conv2d_nhwc(x, self.stem_w, self.stem_b, stride=2, pad=3, act="relu", workspace=ws)
-        x = ops.maxpool_nhwc(x, 3, 2, 1)
+            if s2d:
+                x = ops.image_to_s2d(img, zero=ws)          # also zeroes the workspace's counters
+                x = ops.conv2d_nhwc(x, self.stem_w_s2d, self.stem_b, stride=1, pad=2, act="relu",
+                                    out_hw=(img.shape[1] // 2, img.shape[2] // 2), workspace=ws)
+            else:
+                x = ops.image_to_nhwc(img, 8)
+                x = ops.conv2d_nhwc(x, self.stem_w, self.stem_b, stride=2, pad=3, act="relu", workspace=ws)
+            x = ops.maxpool_nhwc(x, 3, 2, 1)
         for blk in self.blocks:
             s = blk["stride"]
             h = ops.conv2d_nhwc(x, blk["w1"], blk["b1"], act="relu", workspace=ws)

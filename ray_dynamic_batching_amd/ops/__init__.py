@@ -1002,6 +1002,30 @@ def image_to_s2d(img_u8: torch.Tensor, zero: Optional[torch.Tensor] = None) -> t
     return out
 
 
+def stem_s2d_pool(img_u8: torch.Tensor, w_s2d: torch.Tensor, bias: torch.Tensor,
+                  zero: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """The ResNet stem in one kernel (ops/csrc/cnn_stem.hip): uint8 [N, H, W, 3]
+    -> normalise -> space-to-depth -> 4x4 conv with ``w_s2d`` [64, 4, 4, 16]
+    (``stem_weight_s2d``) + bias + ReLU -> 3x3 / stride-2 max-pool (pad 1) ->
+    f16 [N, H/4, W/4, 64].  H, W multiples of 32.  ``zero``: a split-K workspace
+    whose counter header the kernel zeroes on the side."""
+    _check(img_u8.is_cuda and img_u8.dtype == torch.uint8 and img_u8.is_contiguous() and img_u8.shape[-1] == 3,
+           "stem_s2d_pool: bad image")
+    N, H, W, _ = img_u8.shape
+    _check(H % 32 == 0 and W % 32 == 0, "stem_s2d_pool: H and W must be multiples of 32")
+    _check(w_s2d.shape == (64, 4, 4, 16) and w_s2d.dtype == torch.float16 and w_s2d.is_contiguous()
+           and bias.numel() == 64 and bias.dtype == torch.float16 and _aligned(w_s2d), "stem_s2d_pool: bad weights")
+    out = torch.empty(N, H // 4, W // 4, 64, device=img_u8.device, dtype=torch.float16)
+    zb = 0
+    if zero is not None:
+        _check(zero.is_cuda and zero.dtype == torch.uint8 and zero.numel() >= SPLITK_HEADER and _aligned(zero),
+               "stem_s2d_pool: zero must be a split-K workspace")
+        zb = SPLITK_HEADER
+    _ops().stem_s2d_pool(img_u8.data_ptr(), N, H, W, w_s2d.data_ptr(), bias.data_ptr(), out.data_ptr(), _ptr(zero),
+                         zb, _stream())
+    return out
+
+
 def image_to_s2d_ref(img_u8):
     x = image_to_nhwc_ref(img_u8, 3).float()                       # [N, H, W, 3]
     N, H, W, _ = x.shape

@@ -45,6 +45,8 @@ void rope(uintptr_t qkv, int ld, int q_off, int k_off, int H, int Hkv, int D, in
 void gather_rows(uintptr_t src_ptrs, int n, int rows, int row_bytes, uintptr_t dst, uintptr_t stream);
 void image_to_nhwc(uintptr_t src, int N, int HW, int Cp, uintptr_t dst, uintptr_t stream);
 void image_to_s2d(uintptr_t src, int N, int H, int W, uintptr_t dst, uintptr_t zero, long zero_bytes, uintptr_t stream);
+void stem_s2d_pool(uintptr_t img, int N, int H, int W, uintptr_t w, uintptr_t bias, uintptr_t out, uintptr_t zero,
+                   long zero_bytes, uintptr_t stream);
 void conv2d_nhwc(uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t res, uintptr_t y, int N, int H,
                  int W, int C, int K, int R, int S, int stride, int pad, int P, int Q, int act,
                  uintptr_t stream, int force_cfg, uintptr_t ws, size_t ws_bytes);
@@ -106,6 +108,7 @@ PYBIND11_MODULE(_rdb_ops, m) {
   m.def("gather_rows", &rdb::gather_rows, py::call_guard<py::gil_scoped_release>());
   m.def("image_to_nhwc", &rdb::image_to_nhwc, py::call_guard<py::gil_scoped_release>());
   m.def("image_to_s2d", &rdb::image_to_s2d, py::call_guard<py::gil_scoped_release>());
+  m.def("stem_s2d_pool", &rdb::stem_s2d_pool, py::call_guard<py::gil_scoped_release>());
   m.def("conv2d_nhwc", &rdb::conv2d_nhwc, py::call_guard<py::gil_scoped_release>());
   m.def("conv_splitk_bytes", &rdb::conv_splitk_bytes);
   m.def("maxpool_nhwc", &rdb::maxpool_nhwc, py::call_guard<py::gil_scoped_release>());

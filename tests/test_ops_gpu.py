@@ -370,6 +370,33 @@ def test_image_to_s2d_and_space_to_depth_stem():
     _close(y, ref, 2e-2, 2e-2)
 
 
+@pytest.mark.parametrize("N,H,W", [(3, 224, 224), (2, 64, 96), (1, 32, 32)])
+def test_stem_s2d_pool_fused(N, H, W):
+    """Image -> space-to-depth -> 4x4 stem conv -> ReLU -> 3x3/2 max-pool in one
+    kernel, against the three-kernel path and the fp32 7x7 / stride-2 reference;
+    the side job zeroes a split-K counter header."""
+    ops = _ops()
+    torch.manual_seed(H + W)
+    img = torch.randint(0, 256, (N, H, W, 3), device="cuda", dtype=torch.uint8)
+    g = torch.Generator().manual_seed(4)
+    w7 = torch.zeros(64, 7, 7, 8, dtype=torch.float16)
+    w7[..., :3] = (torch.randn(64, 7, 7, 3, generator=g) * (147 ** -0.5)).half()
+    w7 = w7.cuda()
+    b = (torch.randn(64, generator=g) * 0.1).half().cuda()
+    ws4 = ops.stem_weight_s2d(w7)
+    ws = ops.splitk_workspace("cuda", zeroed=False)
+    ws[:ops.SPLITK_HEADER].fill_(0x5A)
+    y = ops.stem_s2d_pool(img, ws4, b, zero=ws)
+    torch.cuda.synchronize()
+    assert y.shape == (N, H // 4, W // 4, 64)
+    assert int(ws[:ops.SPLITK_HEADER].sum()) == 0
+    three = ops.maxpool_nhwc(ops.conv2d_nhwc(ops.image_to_s2d(img), ws4, b, stride=1, pad=2, act="relu",
+                                             out_hw=(H // 2, W // 2)), 3, 2, 1)
+    _close(y, three, 1e-2, 1e-2)
+    ref = ops.maxpool_nhwc_ref(ops.conv2d_nhwc_ref(ops.image_to_nhwc(img, 8), w7, b, stride=2, pad=3, act="relu"))
+    _close(y, ref, 2e-2, 2e-2)
+
+
 def test_image_to_nhwc_and_gather():
     ops = _ops()
     img = torch.randint(0, 256, (3, 32, 32, 3), device="cuda", dtype=torch.uint8)
