@@ -23,6 +23,9 @@ shares).  ``--policy priority`` replaces the Nexus duty cycle by the engine's
 priority / earliest-deadline-first policy.
 
     python bench/colocation_replan_bench.py --slots 2 --json-out gpurun_out/replan.json
+
+Offered load: ``--load`` phases as fractions of the device's measured solo
+capacity per model (from the same profiles), or absolute ``--phases``.
 """
 from __future__ import annotations
 
@@ -35,14 +38,20 @@ import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
-DEFAULT_PHASES = "3000:6000,6000:10000,9000:14000,12000:16000,6000:20000,3000:8000"
+# the fork's ramp (test_scheduler.py:57-96) as fractions of the GPU's measured
+# capacity: utilisation 0.3 -> 0.8 -> 0.35, the mix shifting between the models
+DEFAULT_LOAD = "0.3:0.5,0.5:0.4,0.7:0.4,0.8:0.5,0.75:0.25,0.35:0.4"
 
 
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--models", default="resnet50,bert-base")
     ap.add_argument("--slos", default="30,30", help="SLO ms per model")
-    ap.add_argument("--phases", default=DEFAULT_PHASES, help="comma list of per-phase 'rate_m0:rate_m1' req/s")
+    ap.add_argument("--phases", default="", help="comma list of per-phase 'rate_m0:rate_m1' req/s (absolute)")
+    ap.add_argument("--load", default=DEFAULT_LOAD,
+                    help="comma list of per-phase 'utilisation:share_m0' of the GPU's measured capacity (used when "
+                         "--phases is empty): model 0 gets share_m0 of the utilisation, model 1 the rest")
+    ap.add_argument("--compute-streams", type=int, default=1)
     ap.add_argument("--phase-s", type=float, default=4.0)
     ap.add_argument("--slots", type=int, default=2, help="engine executors (GPU slots) on device 0")
     ap.add_argument("--policy", default="duty", choices=["duty", "priority"])
@@ -62,7 +71,6 @@ def main(argv=None):
 
     names = a.models.split(",")
     slos = dict(zip(names, map(float, a.slos.split(","))))
-    phases = [dict(zip(names, map(float, p.split(":")))) for p in a.phases.split(",")]
     batches = [int(b) for b in a.batches.split(",")]
     os.makedirs(a.profile_dir, exist_ok=True)
     torch.cuda.set_device(0)
@@ -82,12 +90,31 @@ def main(argv=None):
         del m, prof
         torch.cuda.empty_cache()
 
+    # solo capacity of each model on the device (req/s at its best profiled batch)
+    capacity = {n: max(b / (r["avg_latency_ms"] / 1e3) for b, r in p.items()) for n, p in profiles.items()}
+    if a.phases:
+        phases = [dict(zip(names, map(float, p.split(":")))) for p in a.phases.split(",")]
+    else:
+        phases = []
+        for p in a.load.split(","):
+            u, sh = map(float, p.split(":"))
+            phases.append({names[0]: round(u * sh * capacity[names[0]]),
+                           names[1]: round(u * (1 - sh) * capacity[names[1]])})
+    utilisation = [round(sum(ph[n] / capacity[n] for n in names), 3) for ph in phases]
+    # ``--slots`` executors share ONE device: the planner must see each slot as
+    # 1/slots of it, so its per-batch latencies are scaled by the slot count
+    plan_profiles = {n: {b: dict(r, avg_latency_ms=r["avg_latency_ms"] * a.slots) for b, r in p.items()}
+                     for n, p in profiles.items()}
     factories = {n: (lambda device, n=n: models.create(n, device=device)) for n in names}
-    sched = SLOScheduler(profiles, slos, factories, codecs, num_gpus=a.slots, executor="engine",
+    sched = SLOScheduler(plan_profiles, slos, factories, codecs, num_gpus=a.slots, executor="engine",
                          devices=[0] * a.slots, max_batch={n: max(batches) for n in names}, queue_capacity=8192,
-                         engine_policy=a.policy)
+                         engine_policy=a.policy, compute_streams=a.compute_streams)
     out = dict(models=names, slos_ms=slos, phases=phases, phase_s=a.phase_s, slots=a.slots, policy=a.policy,
+               capacity_rps={n: round(c) for n, c in capacity.items()}, offered_utilisation=utilisation,
+               slot_note=f"{a.slots} engine executor(s) on one MI355X; the planner sees each as 1/{a.slots} of it "
+                         "(profiled latencies x slots)",
                profiles={n: {b: r["avg_latency_ms"] for b, r in p.items()} for n, p in profiles.items()})
+    print(json.dumps(dict(capacity_rps=out["capacity_rps"], phases=phases, offered_utilisation=utilisation)), flush=True)
     replans, stop = [], threading.Event()
     t0 = time.time()
 
@@ -140,7 +167,8 @@ def main(argv=None):
                 t.start()
             for t in ts:
                 t.join()
-            row = dict(phase=pi, t_end=round(time.time() - t0, 2), offered=rates, models={})
+            row = dict(phase=pi, t_end=round(time.time() - t0, 2), offered=rates, utilisation=utilisation[pi],
+                       models={})
             for n in names:
                 r = res[n]
                 if r is None:

@@ -21,7 +21,7 @@ def test_replan_under_ramp_no_failed_requests(tmp_path, policy):
     import colocation_replan_bench as crb
 
     out = tmp_path / "replan.json"
-    crb.main(["--slots", "2", "--policy", policy, "--phases", "2000:4000,6000:12000,2000:16000,4000:3000",
+    crb.main(["--slots", "2", "--policy", policy, "--load", "0.3:0.5,0.7:0.4,0.6:0.2,0.3:0.6",
               "--phase-s", "2.0", "--batches", "1,4,16,32", "--profile-dir", str(tmp_path / "prof"),
               "--json-out", str(out)])
     d = json.loads(out.read_text())

@@ -1,0 +1,17 @@
+# round 4 BERT evidence: kernel trace of the headline bench (per-forward table, kernel sum),
+# per-kernel hardware counters of one bs32 forward, and a driver-shaped short bench run
+set -o pipefail
+bash tools/fresh.sh || exit 9
+mkdir -p gpurun_out/r4n
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r4n/prof -o b -- \
+  python3 bench.py --steps 2000 --warmup 50 > gpurun_out/r4n/bench_prof.log 2>&1 || exit $?
+f=$(ls gpurun_out/r4n/prof/*/b_kernel_trace.csv gpurun_out/r4n/prof/b_kernel_trace.csv 2>/dev/null | head -n 1)
+python3 bench/trace_table.py "$f" --tail 0.3 > gpurun_out/r4n/trace_table_bench.txt 2>&1
+python3 bench/trace_gaps.py "$f" --tail 0.3 > gpurun_out/r4n/trace_gaps_bench.txt 2>&1
+s=$(ls gpurun_out/r4n/prof/*/b_kernel_stats.csv gpurun_out/r4n/prof/b_kernel_stats.csv 2>/dev/null | head -n 1)
+cp "$s" gpurun_out/r4n/kernel_stats.csv
+rm -f "$f"
+bash tools/gpu_pmc_r4_bert.sh || exit $?
+timeout -k 10 300 python -u bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/r4n/bench_driver_shape.log 2>&1 || exit $?
+timeout -k 10 300 python -u bench.py --steps 2000 --warmup 50 > gpurun_out/r4n/bench_long.log 2>&1
