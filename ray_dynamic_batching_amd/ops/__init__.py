@@ -199,7 +199,7 @@ def _gemm_candidates(M: int, N: int, K: int):
     cands = list(range(NUM_TILE_CFGS))
     if _GEMM_DEEP and K >= 256:
         cands += [c | DEEP for c in _DEEP_TILES
-                  if -(-M // _TILE_BM[c]) * -(-N // _TILE_BN[c]) <= _DEEP_MAX_BLOCKS]
+                  if c in _DEEP_BIG or -(-M // _TILE_BM[c]) * -(-N // _TILE_BN[c]) <= _DEEP_MAX_BLOCKS]
     return cands
 
 
@@ -1074,7 +1074,8 @@ _GEMM_DEEP = os.environ.get("RDB_GEMM_DEEP", "1") != "0"
 #   ... | DEEP           tiles 0, 1, 2, 3, 9, 10 with one block per CU and up to 8 LDS stages
 CONV_LINEAR = 1 << 16
 DEEP = 1 << 12                        # gemm_core.h kDeepFlag: one block per CU, up to 8 LDS stages
-_DEEP_TILES = (0, 1, 2, 3, 9, 10)
+_DEEP_TILES = (0, 1, 2, 3, 9, 10, 6, 7)
+_DEEP_BIG = (6, 7)                    # 256x128 / 128x256: one block per CU at any grid size
 _DEEP_MAX_BLOCKS = 320                # DEEP candidates only where the grid is ~one block per CU
 SPLITK_HEADER = 65536                 # gemm_core.h kSplitKHeader (tile arrival counters)
 SPLITK_WS_BYTES = 40 << 20            # one forward's split-K workspace (ops.splitk_workspace)
@@ -1107,7 +1108,7 @@ def _conv_candidates(M: int, K_out: int, Kg: int, one_by_one: bool):
         return -(-M // _TILE_BM[c]) * -(-K_out // _TILE_BN[c])
 
     if _GEMM_DEEP:
-        cands += [c | DEEP for c in _DEEP_TILES if tiles_of(c) <= _DEEP_MAX_BLOCKS and nk >= 4]
+        cands += [c | DEEP for c in _DEEP_TILES if (c in _DEEP_BIG or tiles_of(c) <= _DEEP_MAX_BLOCKS) and nk >= 4]
     if _CONV_SPLITK:
         for c in range(NUM_CONV_TILE_CFGS):
             tiles = tiles_of(c)

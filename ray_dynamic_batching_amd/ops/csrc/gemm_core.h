@@ -1224,7 +1224,7 @@ constexpr int kNumTiles = 26;
 constexpr int kTileBM[kNumTiles] = {128, 64, 128, 64, 128, 192, 256, 128, 128, 64, 128, 256, 128, 256, 128, 256, 256, 128, 256, 256, 256, 128, 256, 256, 256, 256};
 constexpr int kTileBN[kNumTiles] = {128, 128, 64, 64, 192, 128, 128, 256, 144, 96, 96, 144, 48, 128, 256, 192, 144, 96, 96, 128, 144, 256, 256, 128, 192, 192};
 // tile cfg flag: the DEEP (one block per CU, up to 8 LDS stages) variant of
-// 4-wave tiles 0, 1, 2, 3, 9, 10 (plain epilogues); other tiles ignore it
+// 4-wave tiles 0, 1, 2, 3, 6, 7, 9, 10 (plain epilogues); other tiles ignore it
 constexpr int kDeepFlag = 1 << 12;
 constexpr int kTileWGM[kNumTiles] = {2, 2, 2, 2, 2, 2, 2, 2, 4, 2, 2, 4, 4, 4, 2, 4, 8, 4, 8, 4, 8, 2, 4, 4, 4, 4};
 constexpr int kTileNW[kNumTiles] = {4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 8, 8, 8, 8, 8, 8, 8, 8, 8, 8, 8, 8, 8};
@@ -1350,6 +1350,10 @@ void launch_mfma_gemm_t(const P& ap, const T* W, int ldw, OutT* C, int ldc, cons
           RDB_TILE_DEEP(3, 64, 64)
           RDB_TILE_DEEP(9, 64, 96)
           RDB_TILE_DEEP(10, 128, 96)
+          // 4-wave 256x128 / 128x256: 128x64 / 64x128 accumulators per wave (in
+          // AGPRs), only spill-free with the whole register file of a 1-block CU
+          RDB_TILE_DEEP(6, 256, 128)
+          RDB_TILE_DEEP(7, 128, 256)
           default: break;
         }
 #undef RDB_TILE_DEEP

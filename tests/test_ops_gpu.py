@@ -291,7 +291,7 @@ def test_linear_deep_tiles(M, N, K):
     r = torch.randn(M, N, device="cuda", dtype=torch.bfloat16)
     ref = torch.nn.functional.gelu(x.float() @ w.float().t() + b.float())
     ref_r = x.float() @ w.float().t() + b.float() + r.float()
-    for c in (0, 1, 2, 3, 9, 10):
+    for c in (0, 1, 2, 3, 9, 10, 6, 7):
         _close(ops.linear(x, w, b, act="gelu", tile_cfg=c | ops.DEEP), ref, 2e-2, 2e-2)
         _close(ops.linear(x, w, b, residual=r, tile_cfg=c | ops.DEEP), ref_r, 2e-2, 2e-2)
 

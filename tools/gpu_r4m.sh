@@ -4,7 +4,7 @@ set -o pipefail
 bash tools/fresh.sh || exit 9
 mkdir -p gpurun_out/r4m
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-timeout -k 10 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_ops_gpu.py -k "stem or s2d" \
+timeout -k 10 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_ops_gpu.py -k "stem or s2d or deep" \
   tests/test_models2_gpu.py::test_resnet50_hip_matches_torch tests/test_models_fp32_gpu.py::test_resnet50_hip_vs_fp32 \
   > gpurun_out/r4m/pytest.log 2>&1 || exit $?
 for r in 1 2; do
@@ -23,3 +23,8 @@ timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun
 f=$(ls gpurun_out/r4m/profcnn/*/c_kernel_trace.csv gpurun_out/r4m/profcnn/c_kernel_trace.csv 2>/dev/null | head -n 1)
 python3 bench/trace_table.py "$f" --tail 0.5 --marker softmax_topk > gpurun_out/r4m/trace_table_resnet_forward.txt 2>&1
 rm -f "$f"
+# the 4-wave 256x128 / 128x256 DEEP tiles (128x64 / 64x128 accumulators per wave, spill-free at 1 block / CU)
+for shp in "4096 3072 768 --act gelu --bias" "4096 2304 768" "4096 768 3072 --bias --res" "4096 768 768 --bias --res"; do
+  set -- $shp
+  timeout -k 10 120 python -u bench/gemm_probe.py --m $1 --n $2 --k $3 ${@:4} --iters 100 >> gpurun_out/r4m/gemm_probe.jsonl 2> gpurun_out/r4m/gemm_probe.err || exit $?
+done

@@ -14,4 +14,7 @@ cp "$s" gpurun_out/r4n/kernel_stats.csv
 rm -f "$f"
 bash tools/gpu_pmc_r4_bert.sh || exit $?
 timeout -k 10 300 python -u bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/r4n/bench_driver_shape.log 2>&1 || exit $?
-timeout -k 10 300 python -u bench.py --steps 2000 --warmup 50 > gpurun_out/r4n/bench_long.log 2>&1
+timeout -k 10 300 python -u bench.py --steps 2000 --warmup 50 > gpurun_out/r4n/bench_long.log 2>&1 || exit $?
+# the 8-rank protocol with the uniform pow-2 second sample (round 3 saw alternating per-replica counts)
+timeout -k 10 300 python -u bench.py --gpus 8 --rehearse-one-gpu --steps 40 --warmup 5 > gpurun_out/r4n/rehearsal_8.log 2>&1 || exit $?
+timeout -k 10 300 python -u bench.py --gpus 4 --rehearse-one-gpu --steps 40 --warmup 5 > gpurun_out/r4n/rehearsal_4.log 2>&1
