@@ -1,0 +1,61 @@
+"""Tile-choice encodings the conv / GEMM tuners rank (ops/__init__.py; decoded
+by gemm_core.h launch_mfma_gemm / conv.hip): tile | splits << 8 | DEEP, and
+CONV_LINEAR | cfg for 1x1 convolutions on the dense GEMM tiles.  CPU-only:
+the candidate lists, not the kernels."""
+from ray_dynamic_batching_amd import ops
+
+
+def _decode(c):
+    return c & 255, (c >> 8) & 15, bool(c & ops.DEEP), c >= ops.CONV_LINEAR
+
+
+def test_conv_candidates_encode_valid_choices():
+    # ResNet-50 layer-3 3x3 conv at bs32 and a layer-1 1x1 conv
+    for M, N, Kg, one in ((6272, 256, 2304, False), (100352, 256, 64, True), (1568, 512, 4608, False)):
+        cands = ops._conv_candidates(M, N, Kg, one)
+        assert len(cands) == len(set(cands))
+        nk = -(-Kg // 64)
+        for c in cands:
+            tile, splits, deep, linear = _decode(c)
+            if linear:
+                assert one and (c - ops.CONV_LINEAR) & 0xFF < ops.NUM_TILE_CFGS
+                continue
+            assert 0 <= tile < ops.NUM_CONV_TILE_CFGS
+            if deep:
+                assert tile in ops._DEEP_TILES
+            if splits:
+                kper = -(-nk // splits)
+                assert kper >= 4 and -(-nk // kper) >= 2          # every split non-empty, >= 4 K steps
+                tiles = -(-M // ops._TILE_BM[tile]) * -(-N // ops._TILE_BN[tile])
+                assert ops.SPLITK_HEADER + tiles * -(-nk // kper) * ops._TILE_BM[tile] * ops._TILE_BN[tile] * 4 \
+                    <= ops.SPLITK_WS_BYTES
+        if one:
+            assert any(c >= ops.CONV_LINEAR for c in cands)
+        if M == 1568:
+            assert any((c >> 8) & 15 for c in cands)                # the small-grid conv gets split-K choices
+
+
+def test_gemm_candidates_deep_only_where_a_block_per_cu():
+    cands = ops._gemm_candidates(4096, 768, 3072)
+    assert set(range(ops.NUM_TILE_CFGS)) <= set(cands)
+    for c in cands:
+        if c & ops.DEEP:
+            t = c & 255
+            assert t in ops._DEEP_TILES
+            if t not in ops._DEEP_BIG:
+                assert -(-4096 // ops._TILE_BM[t]) * -(-768 // ops._TILE_BN[t]) <= ops._DEEP_MAX_BLOCKS
+    assert all(not (c & ops.DEEP) for c in ops._gemm_candidates(4096, 768, 128))   # short K: none
+
+
+def test_tile_tables_match_the_tuned_directory():
+    """Every shipped table entry decodes to a valid choice."""
+    import glob
+    import json
+    import os
+
+    d = os.path.join(os.path.dirname(ops.__file__), "tuned")
+    for f in glob.glob(os.path.join(d, "*.json")):
+        for key, c in json.load(open(f)):
+            assert isinstance(c, int) and c >= -1, (f, key, c)
+            if key[0] == "conv" and c >= 0 and c < ops.CONV_LINEAR:
+                assert (c & 255) < ops.NUM_CONV_TILE_CFGS, (f, key, c)
