@@ -7,10 +7,12 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-def test_resnet50_hip_matches_torch():
+@pytest.mark.parametrize("stem", ["fused", "three_kernels"])
+def test_resnet50_hip_matches_torch(stem):
     from ray_dynamic_batching_amd.models.resnet import ResNet50
 
     m = ResNet50(device="cuda", backend="hip")
+    m.stem_fused = stem == "fused"
     x = m.example_input(4, seed=1)
     lg = m.logits(x)
     m.backend = "torch"

@@ -5,8 +5,9 @@ bash tools/fresh.sh || exit 9
 mkdir -p gpurun_out/r4m
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 timeout -k 10 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_ops_gpu.py -k "stem or s2d or deep" \
-  tests/test_models2_gpu.py::test_resnet50_hip_matches_torch tests/test_models_fp32_gpu.py::test_resnet50_hip_vs_fp32 \
   > gpurun_out/r4m/pytest.log 2>&1 || exit $?
+timeout -k 10 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_models2_gpu.py::test_resnet50_hip_matches_torch \
+  tests/test_models_fp32_gpu.py::test_resnet50_hip_vs_fp32 >> gpurun_out/r4m/pytest.log 2>&1 || exit $?
 for r in 1 2; do
   i=0
   for arm in "RDB_RESNET_STEM_FUSED=0" "RDB_RESNET_STEM_FUSED=1"; do
