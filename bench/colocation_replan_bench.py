@@ -101,18 +101,16 @@ def main(argv=None):
             phases.append({names[0]: round(u * sh * capacity[names[0]]),
                            names[1]: round(u * (1 - sh) * capacity[names[1]])})
     utilisation = [round(sum(ph[n] / capacity[n] for n in names), 3) for ph in phases]
-    # ``--slots`` executors share ONE device: the planner must see each slot as
-    # 1/slots of it, so its per-batch latencies are scaled by the slot count
-    plan_profiles = {n: {b: dict(r, avg_latency_ms=r["avg_latency_ms"] * a.slots) for b, r in p.items()}
-                     for n, p in profiles.items()}
+    # ``--slots`` executors share ONE device: SLOScheduler plans each as 1/slots
+    # of it (its ``slot_share``: per-batch latencies planned slots x longer)
     factories = {n: (lambda device, n=n: models.create(n, device=device)) for n in names}
-    sched = SLOScheduler(plan_profiles, slos, factories, codecs, num_gpus=a.slots, executor="engine",
+    sched = SLOScheduler(profiles, slos, factories, codecs, num_gpus=a.slots, executor="engine",
                          devices=[0] * a.slots, max_batch={n: max(batches) for n in names}, queue_capacity=8192,
                          engine_policy=a.policy, compute_streams=a.compute_streams)
     out = dict(models=names, slos_ms=slos, phases=phases, phase_s=a.phase_s, slots=a.slots, policy=a.policy,
                capacity_rps={n: round(c) for n, c in capacity.items()}, offered_utilisation=utilisation,
-               slot_note=f"{a.slots} engine executor(s) on one MI355X; the planner sees each as 1/{a.slots} of it "
-                         "(profiled latencies x slots)",
+               slot_note=f"{a.slots} engine executor(s) on one MI355X; the planner sees each as "
+                         f"{sched.slot_share:.3g} of it (profiled latencies x {a.slots})",
                profiles={n: {b: r["avg_latency_ms"] for b, r in p.items()} for n, p in profiles.items()})
     print(json.dumps(dict(capacity_rps=out["capacity_rps"], phases=phases, offered_utilisation=utilisation)), flush=True)
     replans, stop = [], threading.Event()

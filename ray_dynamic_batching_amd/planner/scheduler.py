@@ -20,11 +20,13 @@
 """
 from __future__ import annotations
 
+import collections
 import copy
 import logging
 import math
 import threading
 import time
+import warnings
 from dataclasses import dataclass, field
 from typing import Any, Callable, Dict, List, Optional
 
@@ -370,6 +372,22 @@ class SLOScheduler:
         way at packing time (293-project/src/nexus.py:223-227)."""
         self.plan_path = plan_path
         from ..runtime.resources import MI355X_HBM_BYTES as DEFAULT_HBM_BYTES
+
+        # Several engine executors ("GPU slots") on one device: the planner packs
+        # whole GPUs, so it must see each slot as 1/k of its device -- its
+        # per-batch latencies are planned k times longer (the duty cycles then
+        # leave the other slots' share of every cycle idle on this one)
+        self.slot_share = 1.0
+        if executor == "engine":
+            devices = list(devices if devices is not None else range(num_gpus))
+            counts = collections.Counter(devices)
+            k = max(counts.values())
+            if k > 1:
+                if len(set(counts.values())) > 1:
+                    warnings.warn(f"uneven GPU slots per device {dict(counts)}: planning every slot as 1/{k}")
+                self.slot_share = 1.0 / k
+                profiles = {m: {b: dict(r, avg_latency_ms=r["avg_latency_ms"] * k) for b, r in p.items()}
+                            for m, p in profiles.items()}
 
         self.hbm_budget_bytes = int((hbm_budget_gb * 1e9) if hbm_budget_gb is not None else DEFAULT_HBM_BYTES)
         self._footprint_hint = {m: int(v * 1e9) for m, v in (model_footprint_gb or {}).items()}

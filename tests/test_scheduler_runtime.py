@@ -311,3 +311,38 @@ def test_unload_with_no_other_server_fails_leftovers_fast():
         assert sorted(got) == sorted(rids) and set(got.values()) == {2}
     finally:
         s.shutdown()
+
+
+def test_engine_slots_sharing_one_device_are_planned_as_fractions(monkeypatch):
+    """Two engine executors on ONE device: the planner sees each as half of it
+    (per-batch latencies planned twice as long), so a load that one whole GPU
+    carries is not planned twice over on the shared device (config-5 rehearsal,
+    bench/colocation_replan_bench.py --slots 2)."""
+    from ray_dynamic_batching_amd.planner import scheduler as sch
+
+    class _Stub:
+        def __init__(self, sched, g, device, mb, compute_streams=1, policy="duty"):
+            self.device = device
+
+        def stop(self):
+            pass
+
+    monkeypatch.setattr(sch, "EngineExecutor", _Stub)
+    prof = {"a": synthetic_profile(2, 0.1, 50, 1, batches=range(1, 33))}
+    codecs = {"a": TensorCodec((32,), torch.float32, (8,), torch.float32)}
+    shared = SLOScheduler(prof, {"a": 200.0}, {"a": MLP}, codecs, num_gpus=2, executor="engine", devices=[0, 0])
+    whole = SLOScheduler(prof, {"a": 200.0}, {"a": MLP}, codecs, num_gpus=2, executor="engine", devices=[0, 1])
+    try:
+        assert shared.slot_share == 0.5 and whole.slot_share == 1.0
+        for b, r in prof["a"].items():
+            assert shared.planner.profile["a"][b]["avg_latency_ms"] == 2 * r["avg_latency_ms"]
+            assert whole.planner.profile["a"][b]["avg_latency_ms"] == r["avg_latency_ms"]
+        # the same rate needs at least as many (half-)slots on the shared device
+        rate = 0.8 * max(b / (r["avg_latency_ms"] / 1e3) for b, r in prof["a"].items())
+        from ray_dynamic_batching_amd.planner.nexus import Session
+
+        occ = lambda s: sum(o for n in s.planner.plan([Session("a", 200.0, rate)]).nodes for _, o in n.sessions)
+        assert occ(shared) >= 1.9 * occ(whole)          # twice the slot time for the same rate
+    finally:
+        shared.shutdown()
+        whole.shutdown()
