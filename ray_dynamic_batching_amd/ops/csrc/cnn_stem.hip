@@ -55,8 +55,9 @@ stem_s2d_pool_kernel(const uint8_t* __restrict__ img, int H, int W, const f16* _
   const int i0 = blockIdx.y * kPT, j0 = blockIdx.x * kPT, n = blockIdx.z;
   {
     // side job: zero a split-K counter header for the rest of the forward
-    const int z = (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x * 256 + blockIdx.x * 256 + tid;
-    if (z < zero_n) zero[z] = u32x4{0u, 0u, 0u, 0u};
+    const int nthr = gridDim.x * gridDim.y * gridDim.z * 256;
+    for (int z = ((blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x) * 256 + tid; z < zero_n; z += nthr)
+      zero[z] = u32x4{0u, 0u, 0u, 0u};
   }
 
   // ---- weights -> LDS (2048 16-B chunks) ----
@@ -179,7 +180,6 @@ void stem_s2d_pool(uintptr_t img, int N, int H, int W, uintptr_t w, uintptr_t bi
     throw std::invalid_argument("stem_s2d_pool: alignment (image 2 B, weights / out / zero 16 B)");
   const dim3 grid(W / 32, H / 32, N);
   const long zn = zero ? zero_bytes / 16 : 0;
-  if (zn > (long)grid.x * grid.y * grid.z * 256) throw std::invalid_argument("stem_s2d_pool: zero range too large");
   hipLaunchKernelGGL(stem_s2d_pool_kernel, grid, dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
                      (const uint8_t*)img, H, W, (const f16*)w, (const f16*)bias, (f16*)out, 0.485f, 0.456f, 0.406f,
                      0.229f, 0.224f, 0.225f, (u32x4*)zero, (int)zn);
