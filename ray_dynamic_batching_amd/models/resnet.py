@@ -60,9 +60,9 @@ class ResNet50:
         # the stem on the space-to-depth image: 4x4 / stride-1 conv, 256 reduction
         # elements per output instead of 392 (RDB_RESNET_S2D=0: the 7x7 conv)
         self.stem_s2d = os.environ.get("RDB_RESNET_S2D", "1") != "0"
-        # ... and fused with the max-pool and the image conversion (RDB_RESNET_STEM_FUSED=1; default: the
-        # three-kernel stem until the fused kernel's same-box A/B is in)
-        self.stem_fused = os.environ.get("RDB_RESNET_STEM_FUSED", "0") == "1"
+        # ... and fused with the max-pool and the image conversion: +6.3 % img/s in a same-box serving A/B
+        # (profiles/resnet50_stem_fused_ab_r4.json); RDB_RESNET_STEM_FUSED=0: the three-kernel stem
+        self.stem_fused = os.environ.get("RDB_RESNET_STEM_FUSED", "1") != "0"
         self.stem_w_s2d = ops.stem_weight_s2d(self.stem_w)
         self.blocks: List[dict] = []
         cin = 64
