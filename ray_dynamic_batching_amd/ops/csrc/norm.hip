@@ -138,8 +138,9 @@ norm16_kernel(const T* __restrict__ x, const T* __restrict__ res, T* __restrict_
               float eps) {
   constexpr int D = 256 * NV16;
   const int hl = threadIdx.x & 31;
-  const int row = blockIdx.x * 8 + (threadIdx.x >> 5);
-  if (row >= rows) return;
+  // grid-stride over 8-row groups: a capped grid (RDB_LN_BLOCKS) leaves CUs to a
+  // concurrently running kernel of another stream instead of flooding the dispatcher
+  for (int row = blockIdx.x * 8 + (threadIdx.x >> 5); row < rows; row += gridDim.x * 8) {
   const T* xr = x + (size_t)row * ldx;
   float v[NV16][8];
 #pragma unroll
@@ -186,6 +187,7 @@ norm16_kernel(const T* __restrict__ x, const T* __restrict__ res, T* __restrict_
 #pragma unroll
     for (int q = 0; q < 8; ++q) o[q] = MODE == 0 ? (v[i][q] - mean) * rstd * g[q] + b[q] : v[i][q] * rstd * g[q];
     st8(yr + c, o);
+  }
   }
 }
 
@@ -366,7 +368,12 @@ static void launch_embed(dim3 grid, hipStream_t s, uintptr_t ids, uintptr_t type
 template <typename T, int MODE>
 static bool launch_norm16(hipStream_t s, uintptr_t x, uintptr_t res, uintptr_t res_out, uintptr_t gamma,
                           uintptr_t beta, uintptr_t y, int rows, int D, int ldx, float eps) {
-  const dim3 grid((rows + 7) / 8), blk(256);
+  static const int max_blocks = [] {
+    const char* e = std::getenv("RDB_LN_BLOCKS");
+    return e ? std::atoi(e) : 0;
+  }();
+  const int groups = (rows + 7) / 8;
+  const dim3 grid(max_blocks > 0 && groups > max_blocks ? max_blocks : groups), blk(256);
 #define RDB_N16(NV)                                                                                         \
   if (D == 256 * NV) {                                                                                      \
     hipLaunchKernelGGL((norm16_kernel<T, MODE, NV>), grid, blk, 0, s, (const T*)x, (const T*)res, (T*)res_out, \

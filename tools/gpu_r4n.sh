@@ -17,4 +17,12 @@ timeout -k 10 300 python -u bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out
 timeout -k 10 300 python -u bench.py --steps 2000 --warmup 50 > gpurun_out/r4n/bench_long.log 2>&1 || exit $?
 # the 8-rank protocol with the uniform pow-2 second sample (round 3 saw alternating per-replica counts)
 timeout -k 10 300 python -u bench.py --gpus 8 --rehearse-one-gpu --steps 40 --warmup 5 > gpurun_out/r4n/rehearsal_8.log 2>&1 || exit $?
-timeout -k 10 300 python -u bench.py --gpus 4 --rehearse-one-gpu --steps 40 --warmup 5 > gpurun_out/r4n/rehearsal_4.log 2>&1
+timeout -k 10 300 python -u bench.py --gpus 4 --rehearse-one-gpu --steps 40 --warmup 5 > gpurun_out/r4n/rehearsal_4.log 2>&1 || exit $?
+# ResNet-50 forward with the fused stem: per-forward kernel table (kernel sum) and single-stream time
+T=ray_dynamic_batching_amd/ops/tuned/mi355x_resnet50_B32_cs2_d4.json
+timeout -k 10 200 python -u bench/cnn_breakdown.py --model resnet50 --batch 32 --iters 30 --tune-file $T > gpurun_out/r4n/cnn_breakdown.log 2>&1 || exit $?
+timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r4n/profcnn -o c -- \
+  python3 bench/cnn_breakdown.py --model resnet50 --batch 32 --iters 20 --tune-file $T > gpurun_out/r4n/prof_cnn.log 2>&1 || exit $?
+f=$(ls gpurun_out/r4n/profcnn/*/c_kernel_trace.csv gpurun_out/r4n/profcnn/c_kernel_trace.csv 2>/dev/null | head -n 1)
+python3 bench/trace_table.py "$f" --tail 0.5 --marker softmax_topk > gpurun_out/r4n/trace_table_resnet_forward.txt 2>&1
+rm -f "$f"
