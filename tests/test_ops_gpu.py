@@ -296,6 +296,42 @@ def test_linear_deep_tiles(M, N, K):
         _close(ops.linear(x, w, b, residual=r, tile_cfg=c | ops.DEEP), ref_r, 2e-2, 2e-2)
 
 
+@pytest.mark.parametrize("M,N,K", [(128, 4096, 14336), (256, 1000, 2056), (300, 768, 3072)])
+def test_linear_splitk(M, N, K):
+    """Split-K on the dense GEMM (tile | splits << 8): with a caller workspace,
+    with a private one, and captured in a graph (the private workspace lives in
+    the graph's pool) -- against the fp32 reference, ragged M / N / K tails."""
+    ops = _ops()
+    torch.manual_seed(M + N)
+    x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    w = torch.randn(N, K, device="cuda", dtype=torch.bfloat16) * K ** -0.5
+    b = torch.randn(N, device="cuda", dtype=torch.bfloat16) * 0.1
+    r = torch.randn(M, N, device="cuda", dtype=torch.bfloat16)
+    ref = x.float() @ w.float().t() + b.float() + r.float()
+    ref_g = torch.nn.functional.gelu(x.float() @ w.float().t() + b.float())
+    ws = ops.splitk_workspace("cuda")
+    for c in (0, 1, 3, 9, 12):
+        for sp in (2, 4, 8):
+            cfg = c | (sp << 8)
+            _close(ops.linear(x, w, b, residual=r, tile_cfg=cfg, workspace=ws), ref, 2e-2, 2e-2)
+            _close(ops.linear(x, w, b, act="gelu", tile_cfg=cfg), ref_g, 2e-2, 2e-2)
+    torch.cuda.synchronize()
+    assert int(ws[:ops.SPLITK_HEADER].view(torch.int32).abs().sum()) == 0
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        ops.linear(x, w, b, residual=r, tile_cfg=0 | (4 << 8))
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            y = ops.linear(x, w, b, residual=r, tile_cfg=0 | (4 << 8))
+    torch.cuda.synchronize()
+    for _ in range(2):
+        x.copy_(torch.randn_like(x))
+        g.replay()
+        torch.cuda.synchronize()
+        _close(y, x.float() @ w.float().t() + b.float() + r.float(), 2e-2, 2e-2)
+
+
 def test_conv2d_splitk_graph_replay():
     """Split-K inside a captured graph with the per-forward workspace idiom of
     ResNet50._logits_hip, replayed with new inputs."""
