@@ -193,22 +193,41 @@ def _tuned_cfg(key: tuple, launch: Callable[[int], None], candidates=range(NUM_T
 # ---------------------------------------------------------------------------
 # GEMM (+ fused bias / activation / residual epilogue)
 # ---------------------------------------------------------------------------
-def _gemm_candidates(M: int, N: int, K: int):
+def _gemm_candidates(M: int, N: int, K: int, splitk: bool = False):
     """Dense GEMM tile choices: every tile cfg, plus the DEEP variants of the
-    4-wave tiles whose grid is about one block per CU (``DEEP`` flag)."""
+    4-wave tiles whose grid is about one block per CU (``DEEP`` flag), plus
+    (``splitk``) split-K variants of the 4-wave tiles where the tile grid leaves
+    CUs idle and each split keeps >= 8 K steps (long-K GEMMs of small M: the
+    Llama prefill's down projection at 128 tokens is 128 blocks x 224 K steps)."""
     cands = list(range(NUM_TILE_CFGS))
     if _GEMM_DEEP and K >= 256:
         cands += [c | DEEP for c in _DEEP_TILES
                   if c in _DEEP_BIG or -(-M // _TILE_BM[c]) * -(-N // _TILE_BN[c]) <= _DEEP_MAX_BLOCKS]
+    if splitk and _GEMM_SPLITK:
+        nk = -(-K // 64)
+        for c in range(NUM_CONV_TILE_CFGS):
+            tiles = -(-M // _TILE_BM[c]) * -(-N // _TILE_BN[c])
+            if tiles >= 256:
+                continue
+            for sp in _SPLITS:
+                kper = -(-nk // sp)
+                eff = -(-nk // kper)
+                if eff < 2 or kper < 8 or tiles * eff > 1024:
+                    continue
+                if SPLITK_HEADER + tiles * eff * _TILE_BM[c] * _TILE_BN[c] * 4 > SPLITK_WS_BYTES:
+                    continue
+                cands.append(c | (sp << 8))
     return cands
 
 
 def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, act: str = "none",
            residual: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None,
-           out_dtype: Optional[torch.dtype] = None, alpha: float = 1.0, tile_cfg: int = -1) -> torch.Tensor:
+           out_dtype: Optional[torch.dtype] = None, alpha: float = 1.0, tile_cfg: int = -1,
+           workspace: Optional[torch.Tensor] = None) -> torch.Tensor:
     """y = act(alpha * x @ w.T + bias + residual).  x: [..., K] or a 2-D row-strided
     view; w: [N, K] contiguous.  act="swiglu" expects w rows interleaved (gate, up)
-    and returns N/2 columns."""
+    and returns N/2 columns.  ``workspace`` (``splitk_workspace``): used when the
+    chosen tile is split-K (else a private one is allocated)."""
     _check(x.is_cuda and w.is_cuda, "linear: tensors must be on the GPU")
     _check(x.dtype in (torch.bfloat16, torch.float16) and w.dtype == x.dtype, "linear: bf16/f16 inputs of equal dtype")
     _check(w.dim() == 2 and w.is_contiguous(), "linear: w must be a contiguous [N, K] matrix")
@@ -243,13 +262,29 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
         _check(residual.dtype == x.dtype and residual.shape[-1] == n_out, "linear: bad residual")
     args = (DTYPE_CODE[x.dtype], DTYPE_CODE[od], x2.data_ptr(), lda, w.data_ptr(), K, out.data_ptr(),
             n_out, _ptr(bias), _ptr(residual), ldr, M, N, K, float(alpha), ACT_CODE[act])
-    fn = _ops().gemm_tn
+    fn = _ops().gemm_tn_sk
     skinny = M <= SKINNY_MAX_M and K % 32 == 0 and act != "swiglu"   # C++ routes these to the skinny-M kernel
+
+    def launch(c: int, ws: Optional[torch.Tensor]) -> None:
+        if c >= 0 and (c >> 8) & 15 and ws is None:
+            # a split-K choice without a caller workspace: a private one (one memset)
+            ws = splitk_workspace(x.device, max(SPLITK_HEADER, int(_ops().conv_splitk_bytes(M, N, c & 255, (c >> 8) & 15))))
+        fn(*args, _stream(), int(c), _ptr(ws), 0 if ws is None else ws.numel())
+
     if tile_cfg < 0 and od != torch.float32 and not skinny:
         key = ("gemm", x.dtype, M, N, K, lda, act, bias is not None, residual is not None)
-        tile_cfg = _tuned_cfg(key, lambda c: fn(*args, _stream(), c),
-                              _gemm_candidates(M, N, K) if act != "swiglu" else range(NUM_TILE_CFGS))
-    fn(*args, _stream(), int(tile_cfg))
+
+        def tune_launch(c: int) -> None:
+            ws = None
+            if (c >> 8) & 15:
+                sid = _stream()
+                ws = _tune_ws.get(sid)
+                if ws is None:
+                    ws = _tune_ws[sid] = splitk_workspace(x.device)
+            launch(c, ws)
+        tile_cfg = _tuned_cfg(key, tune_launch,
+                              _gemm_candidates(M, N, K, splitk=True) if act != "swiglu" else range(NUM_TILE_CFGS))
+    launch(int(tile_cfg), workspace)
     return out
 
 
@@ -1065,6 +1100,8 @@ def image_to_nhwc_ref(img_u8, Cp=8):
 _CONV1X1_GEMM = os.environ.get("RDB_CONV1X1_GEMM", "1") != "0"
 # RDB_CONV_SPLITK=0: no split-K candidates
 _CONV_SPLITK = os.environ.get("RDB_CONV_SPLITK", "1") != "0"
+# RDB_GEMM_SPLITK=0: no split-K candidates for the dense GEMM (linear)
+_GEMM_SPLITK = os.environ.get("RDB_GEMM_SPLITK", "1") != "0"
 # RDB_GEMM_DEEP=0: no DEEP (one block per CU, many LDS stages) tile candidates
 _GEMM_DEEP = os.environ.get("RDB_GEMM_DEEP", "1") != "0"
 # Encoded conv tile choices (what the tuner / tile tables store):

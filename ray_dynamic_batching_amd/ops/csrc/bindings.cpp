@@ -14,6 +14,10 @@ namespace rdb {
 void gemm_tn(int in_dtype, int out_dtype, uintptr_t A, int lda, uintptr_t W, int ldw, uintptr_t C,
              int ldc, uintptr_t bias, uintptr_t R, int ldr, int M, int N, int K, float alpha,
              int act, uintptr_t stream, int force_cfg);
+void gemm_tn_sk(int in_dtype, int out_dtype, uintptr_t A, int lda, uintptr_t W, int ldw, uintptr_t C,
+                int ldc, uintptr_t bias, uintptr_t R, int ldr, int M, int N, int K, float alpha,
+                int act, uintptr_t stream, int force_cfg, uintptr_t ws, size_t ws_bytes);
+size_t conv_splitk_bytes(int M, int N, int cfg, int splits);
 void gemm_tn_ln(uintptr_t A, int lda, uintptr_t W, int ldw, uintptr_t C, int ldc, uintptr_t bias, uintptr_t R,
                 int ldr, int M, int N, int K, float alpha, int act, int mode, uintptr_t a_stats, int a_ld,
                 uintptr_t a_colsum, uintptr_t a_bias, uintptr_t r_stats, int r_ld, uintptr_t r_g, uintptr_t r_b,
@@ -50,7 +54,6 @@ void stem_s2d_pool(uintptr_t img, int N, int H, int W, uintptr_t w, uintptr_t bi
 void conv2d_nhwc(uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t res, uintptr_t y, int N, int H,
                  int W, int C, int K, int R, int S, int stride, int pad, int P, int Q, int act,
                  uintptr_t stream, int force_cfg, uintptr_t ws, size_t ws_bytes);
-size_t conv_splitk_bytes(int M, int N, int cfg, int splits);
 void maxpool_nhwc(uintptr_t x, uintptr_t y, int N, int H, int W, int C, int k, int stride, int pad,
                   int P, int Q, uintptr_t stream);
 void avgpool_nhwc(uintptr_t x, uintptr_t y, int N, int HW, int C, uintptr_t stream);
@@ -83,6 +86,7 @@ static void hip_check(hipError_t e, const char* what) {
 PYBIND11_MODULE(_rdb_ops, m) {
   m.doc() = "ray_dynamic_batching_amd gfx950 kernels (MFMA GEMM/conv, norm, attention, ...)";
   m.def("gemm_tn", &rdb::gemm_tn, py::call_guard<py::gil_scoped_release>());
+  m.def("gemm_tn_sk", &rdb::gemm_tn_sk, py::call_guard<py::gil_scoped_release>());
   m.def("gemm_tn_ln", &rdb::gemm_tn_ln, py::arg("A"), py::arg("lda"), py::arg("W"), py::arg("ldw"), py::arg("C"),
         py::arg("ldc"), py::arg("bias"), py::arg("R"), py::arg("ldr"), py::arg("M"), py::arg("N"), py::arg("K"),
         py::arg("alpha"), py::arg("act"), py::arg("mode"), py::arg("a_stats"), py::arg("a_ld"), py::arg("a_colsum"),
