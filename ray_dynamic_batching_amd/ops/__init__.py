@@ -129,6 +129,35 @@ def tune_in_context(time_forward: Callable[[], float], keys: Optional[list] = No
     return changed
 
 
+# gemm_core.h kTileBM / kTileBN / kTileNW and tile_blocks_per_cu (CU-time estimates of the tuner)
+_ALL_BM = (128, 64, 128, 64, 128, 192, 256, 128, 128, 64, 128, 256, 128, 256, 128, 256, 256, 128, 256, 256, 256, 128,
+           256, 256, 256, 256)
+_ALL_BN = (128, 128, 64, 64, 192, 128, 128, 256, 144, 96, 96, 144, 48, 128, 256, 192, 144, 96, 96, 128, 144, 256, 256,
+           128, 192, 192)
+_ALL_NW = (4,) * 13 + (8,) * 13
+
+
+def _blocks_per_cu(t: int) -> int:
+    if t == 23:
+        return 2
+    if t >= 19:
+        return 1
+    q = 8 * _ALL_NW[t]
+    bnp = -(-_ALL_BN[t] // q) * q
+    return max(1, min(8 // _ALL_NW[t], 163840 // (2 * (_ALL_BM[t] + bnp) * 64 * 2)))
+
+
+def _cu_share(c: int, M: int, N: int, cus: int = 256) -> float:
+    """Share of the GPU's CUs a GEMM launch with tile choice ``c`` holds (split-K
+    multiplies the blocks, DEEP holds a whole CU per block)."""
+    t = c & 255
+    if not 0 <= t < len(_ALL_BM):
+        return 1.0
+    blocks = -(-M // _ALL_BM[t]) * -(-N // _ALL_BN[t]) * max(1, (c >> 8) & 15)
+    per_cu = 1 if c & DEEP else _blocks_per_cu(t)
+    return min(1.0, blocks / (cus * per_cu))
+
+
 _KEY_LOG: Optional[list] = None
 
 
@@ -184,8 +213,16 @@ def _tuned_cfg(key: tuple, launch: Callable[[int], None], candidates=range(NUM_T
         times[c] = t
         if t < best_t:
             best_t, best_c = t, c
-    # the runners-up within 15 %: candidates for in-context selection (tune_in_context)
-    _TUNE_TOP[key] = [c for c in sorted(times, key=times.get) if times[c] <= best_t * 1.15][:3]
+    # the runners-up within 15 %: candidates for in-context selection (tune_in_context) ...
+    top = [c for c in sorted(times, key=times.get) if times[c] <= best_t * 1.15][:3]
+    if key[0] == "gemm":
+        # ... plus the two with the least CU-TIME (time x share of the CUs the grid holds): beside
+        # another stream's batch a slower tile on fewer blocks can win (profiles/ab_r4_tables_cu_time.json:
+        # BERT's o-projection on 96 ping-pong blocks, +2.7..6.5 % over the fastest-alone 256-block tile)
+        M, N = key[2], key[3]
+        cu = {c: t * _cu_share(c, M, N) for c, t in times.items() if t < float("inf")}
+        top += [c for c in sorted(cu, key=cu.get)[:2] if c not in top]
+    _TUNE_TOP[key] = top
     _TUNE[key] = best_c
     return best_c
 

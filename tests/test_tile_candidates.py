@@ -59,3 +59,14 @@ def test_tile_tables_match_the_tuned_directory():
             assert isinstance(c, int) and c >= -1, (f, key, c)
             if key[0] == "conv" and c >= 0 and c < ops.CONV_LINEAR:
                 assert (c & 255) < ops.NUM_CONV_TILE_CFGS, (f, key, c)
+
+
+def test_cu_share_of_tile_grids():
+    """CU share the tuner multiplies a tile's time by to rank CU-time: BERT's
+    o-projection (4096 x 768) holds half the CUs on 256 4-wave 128x96 blocks (two
+    per CU) and 3/8 of them on 96 ping-pong 256x128 blocks; a full grid holds all."""
+    assert ops._cu_share(10, 4096, 768) == 0.5
+    assert ops._cu_share(19, 4096, 768) == 96 / 256
+    assert ops._cu_share(3, 4096, 768) == 1.0
+    assert ops._cu_share(0 | (2 << 8), 4096, 768) == 1.0 or ops._cu_share(0 | (2 << 8), 4096, 768) > ops._cu_share(0, 4096, 768)
+    assert ops._cu_share(0 | ops.DEEP, 1024, 768) == min(1.0, 8 * 6 / 256)
