@@ -147,6 +147,19 @@ def _blocks_per_cu(t: int) -> int:
     return max(1, min(8 // _ALL_NW[t], 163840 // (2 * (_ALL_BM[t] + bnp) * 64 * 2)))
 
 
+def _key_mn(key: tuple):
+    """(M, N) of the output a tuning key's launches write: dense GEMM keys carry
+    them, conv keys give N*P*Q output pixels x K channels; None otherwise."""
+    if key[0] == "gemm":
+        return key[2], key[3]
+    if key[0] == "conv":
+        N, H, W, C, K, R, S, stride, pad = key[1:10]
+        P, Q = (key[13], key[14]) if len(key) >= 15 else ((H + 2 * pad - R) // stride + 1,
+                                                           (W + 2 * pad - S) // stride + 1)
+        return N * P * Q, K
+    return None
+
+
 def _cu_share(c: int, M: int, N: int, cus: int = 256) -> float:
     """Share of the GPU's CUs a GEMM launch with tile choice ``c`` holds (split-K
     multiplies the blocks, DEEP holds a whole CU per block)."""
@@ -215,12 +228,12 @@ def _tuned_cfg(key: tuple, launch: Callable[[int], None], candidates=range(NUM_T
             best_t, best_c = t, c
     # the runners-up within 15 %: candidates for in-context selection (tune_in_context) ...
     top = [c for c in sorted(times, key=times.get) if times[c] <= best_t * 1.15][:3]
-    if key[0] == "gemm":
+    mn = _key_mn(key)
+    if mn is not None:
         # ... plus the two with the least CU-TIME (time x share of the CUs the grid holds): beside
         # another stream's batch a slower tile on fewer blocks can win (profiles/ab_r4_tables_cu_time.json:
         # BERT's o-projection on 96 ping-pong blocks, +2.7..6.5 % over the fastest-alone 256-block tile)
-        M, N = key[2], key[3]
-        cu = {c: t * _cu_share(c, M, N) for c, t in times.items() if t < float("inf")}
+        cu = {c: t * _cu_share(c, *mn) for c, t in times.items() if t < float("inf")}
         top += [c for c in sorted(cu, key=cu.get)[:2] if c not in top]
     _TUNE_TOP[key] = top
     _TUNE[key] = best_c
