@@ -70,3 +70,12 @@ def test_cu_share_of_tile_grids():
     assert ops._cu_share(3, 4096, 768) == 1.0
     assert ops._cu_share(0 | (2 << 8), 4096, 768) == 1.0 or ops._cu_share(0 | (2 << 8), 4096, 768) > ops._cu_share(0, 4096, 768)
     assert ops._cu_share(0 | ops.DEEP, 1024, 768) == min(1.0, 8 * 6 / 256)
+
+
+def test_key_output_shape_for_cu_time():
+    assert ops._key_mn(("gemm", "torch.bfloat16", 4096, 768, 3072, 3072, "none", True, True)) == (4096, 768)
+    assert ops._key_mn(("conv", 32, 14, 14, 256, 256, 3, 3, 1, 1, "relu", True, False)) == (32 * 14 * 14, 256)
+    assert ops._key_mn(("conv", 32, 112, 112, 16, 64, 4, 4, 1, 2, "relu", True, False, 112, 112)) == (32 * 112 * 112, 64)
+    assert ops._key_mn(("qkv_attn", "torch.bfloat16", 32, 128, 12, 768, 768, False)) is None
+    # a 1x1 conv on the dense ping-pong tile: its share follows the GEMM grid
+    assert ops._cu_share(ops.CONV_LINEAR | 19, 1568, 2048) == ops._cu_share(19, 1568, 2048)
