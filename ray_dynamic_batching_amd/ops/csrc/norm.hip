@@ -140,7 +140,8 @@ norm16_kernel(const T* __restrict__ x, const T* __restrict__ res, T* __restrict_
   const int hl = threadIdx.x & 31;
   // grid-stride over 8-row groups: a capped grid (RDB_LN_BLOCKS) leaves CUs to a
   // concurrently running kernel of another stream instead of flooding the dispatcher
-  for (int row = blockIdx.x * 8 + (threadIdx.x >> 5); row < rows; row += gridDim.x * 8) {
+  const int rpb = blockDim.x >> 5;             // rows per block (half-wave per row)
+  for (int row = blockIdx.x * rpb + (threadIdx.x >> 5); row < rows; row += gridDim.x * rpb) {
   const T* xr = x + (size_t)row * ldx;
   float v[NV16][8];
 #pragma unroll
@@ -372,8 +373,15 @@ static bool launch_norm16(hipStream_t s, uintptr_t x, uintptr_t res, uintptr_t r
     const char* e = std::getenv("RDB_LN_BLOCKS");
     return e ? std::atoi(e) : 0;
   }();
-  const int groups = (rows + 7) / 8;
-  const dim3 grid(max_blocks > 0 && groups > max_blocks ? max_blocks : groups), blk(256);
+  // RDB_LN_THREADS: 64 / 128 / 256 threads = 2 / 4 / 8 rows per block (A/B knob; default 256)
+  static const int threads = [] {
+    const char* e = std::getenv("RDB_LN_THREADS");
+    const int t = e ? std::atoi(e) : 256;
+    return (t == 64 || t == 128) ? t : 256;
+  }();
+  const int rpb = threads / 32;
+  const int groups = (rows + rpb - 1) / rpb;
+  const dim3 grid(max_blocks > 0 && groups > max_blocks ? max_blocks : groups), blk(threads);
 #define RDB_N16(NV)                                                                                         \
   if (D == 256 * NV) {                                                                                      \
     hipLaunchKernelGGL((norm16_kernel<T, MODE, NV>), grid, blk, 0, s, (const T*)x, (const T*)res, (T*)res_out, \
