@@ -226,6 +226,10 @@ constexpr int EPI_LNA = 1, EPI_LNR = 2, EPI_STATS = 4, EPI_SELF = 8, EPI_LNOUT =
 // vectors are staged in LDS by the kernel's prologue (ln_stage), so the
 // epilogue reads them like the bias.
 constexpr int EPI_STG = 32;
+// EPI_SWG: the ping-pong kernels' SwiGLU instantiation (plain staged epilogue, N/2
+// output columns; a separate kernel so the other epilogues' register allocation is
+// untouched by the SiLU-pairing path)
+constexpr int EPI_SWG = 64;
 struct LnEpi {
   const float* a_stats;   // LNA: (sum, sumsq) of A's rows, row stride a_ld floats
   const float* a_colsum;  // LNA: colsum(W') [N]
@@ -361,6 +365,14 @@ struct StagedEpi {
   static_assert(BN % 8 == 0 && RC >= 16 && BM % RC == 0, "staged epilogue geometry");
 };
 
+// Activation tag of the staged 16-bit epilogue for SwiGLU: W rows interleaved
+// (gate_j, up_j), so a lane's 4 consecutive columns n..n+3 hold (g, u, g', u')
+// and it parks silu(g) * u, silu(g') * u' at output columns n/2, n/2 + 1; the
+// stored tile is BN/2 wide (output row stride ldc, N/2 columns).
+struct SwigluAct {
+  __device__ __forceinline__ float operator()(float x) const { return x; }
+};
+
 // 16-bit staging rows (residual-free epilogue): BN x 2 B + 32 B, so the 16 rows
 // of one ds_write_b64 wave instruction start 8 banks apart.
 template <int BM, int BN, int SMEM_BYTES>
@@ -448,8 +460,13 @@ __device__ __forceinline__ void staged_epilogue(char* smem, const f32x4 (&acc)[T
       } else if constexpr (HAS_BIAS) {
         v += *reinterpret_cast<const f32x4*>(smem + BIAS_LDS + nt * 4);
       }
-      OutT o4[4] = {(OutT)actf(v[0]), (OutT)actf(v[1]), (OutT)actf(v[2]), (OutT)actf(v[3])};
-      *reinterpret_cast<u32x2*>(smem + rt * E16::ROWB + nt * 2) = *reinterpret_cast<const u32x2*>(o4);
+      if constexpr (std::is_same<ActF, SwigluAct>::value) {
+        OutT o2[2] = {(OutT)(apply_act<ACT_SILU>(v[0]) * v[1]), (OutT)(apply_act<ACT_SILU>(v[2]) * v[3])};
+        *reinterpret_cast<uint32_t*>(smem + rt * E16::ROWB + nt) = *reinterpret_cast<const uint32_t*>(o2);
+      } else {
+        OutT o4[4] = {(OutT)actf(v[0]), (OutT)actf(v[1]), (OutT)actf(v[2]), (OutT)actf(v[3])};
+        *reinterpret_cast<u32x2*>(smem + rt * E16::ROWB + nt * 2) = *reinterpret_cast<const u32x2*>(o4);
+      }
     };
 #pragma unroll 1
     for (int c = 0; c < BM / E16::RC; ++c) {
@@ -467,11 +484,16 @@ __device__ __forceinline__ void staged_epilogue(char* smem, const f32x4 (&acc)[T
         }
       }
       __syncthreads();
+      // SwiGLU: BN/2 output columns per row, starting at n0/2 (N/2 in all)
+      constexpr bool SWG = std::is_same<ActF, SwigluAct>::value;
+      static_assert(!SWG || (BN % 16 == 0), "staged SwiGLU: BN % 16 == 0");
+      constexpr int NVO = SWG ? E16::NV / 2 : E16::NV;
+      const int n_base = SWG ? (n0 >> 1) : n0, n_lim = SWG ? (N >> 1) : N;
 #pragma unroll 4
-      for (int idx = tid; idx < E16::RC * E16::NV; idx += NT) {
-        const int r = idx / E16::NV, vcol = idx - r * E16::NV;
-        const int m = m0 + c * E16::RC + r, n = n0 + vcol * 8;
-        if (m < M && n < N)
+      for (int idx = tid; idx < E16::RC * NVO; idx += NT) {
+        const int r = idx / NVO, vcol = idx - r * NVO;
+        const int m = m0 + c * E16::RC + r, n = n_base + vcol * 8;
+        if (m < M && n < n_lim)
           *reinterpret_cast<u32x4*>(C + (size_t)m * ldc + n) =
               *reinterpret_cast<const u32x4*>(smem + r * E16::ROWB + vcol * 16);
       }
@@ -1021,13 +1043,18 @@ mfma_gemm_kernel(typename LoaderT<T, 1>::Params ap, const T* __restrict__ W, int
   // ---- LDS-staged coalesced epilogue (plain modes; LN / SwiGLU keep the direct one) ----
   if constexpr ((EPI == 0 || STG) && sizeof(OutT) == 2) {
     // (STG launches are host-checked for the staged epilogue's requirements)
-    if (STG || (act != ACT_SWIGLU && staged_epilogue_ok<T, OutT, HAS_RES>(N, C, ldc, bias, R, ldr))) {
+    // SwiGLU stages too when there is no residual (N/2 output columns, N % 16, BN % 16)
+    const bool swg_ok = !HAS_RES && (N & 15) == 0 && BN % 16 == 0;
+    if (STG || ((act != ACT_SWIGLU || swg_ok) && staged_epilogue_ok<T, OutT, HAS_RES>(N, C, ldc, bias, R, ldr))) {
       constexpr int SB = kStages * kStage;
       auto go = [&](auto actf) {
         staged_epilogue<T, OutT, BM, BN, SB, NT, TM, TN, HAS_BIAS, HAS_RES, decltype(actf), -1, EPI,
                         STG ? LN_OFF : -1>(smem, acc, wm * WM, wn * WN, m0, n0, M, N, C, ldc, bias, R, ldr, alpha,
                                            actf, &ln, tile_n);
       };
+      if constexpr (!HAS_RES && !STG && BN % 16 == 0) {
+        if (act == ACT_SWIGLU) { go(SwigluAct{}); return; }
+      }
       switch (act) {
         case ACT_GELU: go([](float x) { return apply_act<ACT_GELU>(x); }); break;
         case ACT_RELU: go([](float x) { return apply_act<ACT_RELU>(x); }); break;

@@ -82,8 +82,8 @@ struct PPGeom {
 // OCC = waves per SIMD the register budget must allow: 2 = one 8-wave block
 // per CU (<= 256 VGPRs), 4 = two co-resident blocks (<= 128 VGPRs; the tile's
 // LDS must then fit twice in 160 KiB)
-// EPI: 0 or an EPI_STG LayerNorm mode (gemm_core.h): its operands are staged in
-// LDS after the bias by the prologue and applied by the staged epilogue.
+// EPI: 0, EPI_SWG (SwiGLU) or an EPI_STG LayerNorm mode (gemm_core.h): LN operands
+// are staged in LDS after the bias by the prologue and applied by the staged epilogue.
 template <typename T, typename OutT, int NW, int BM, int BN, int GM, int GN, int STAGES, bool HAS_BIAS, bool HAS_RES,
           int BK_ = 64, int OCC = 2, int EPI = 0>
 __global__ void __launch_bounds__(64 * NW, OCC)
@@ -106,8 +106,11 @@ gemm_pp_kernel(const T* __restrict__ A, int lda, const T* __restrict__ W, int ld
   // staging buffers, then the tile's bias as f32 (read by the epilogue)
   constexpr int BIAS_OFF = STAGES * G::STAGE_BYTES;
   constexpr int LN_OFF = BIAS_OFF + (HAS_BIAS ? BN * 4 : 0);
-  constexpr int LN_BYTES = EPI ? LnLds<BM, BN>::BYTES : 0;
-  static_assert(EPI == 0 || (EPI & EPI_STG), "ping-pong tiles: plain or staged-LN epilogues");
+  constexpr bool SWG = EPI == EPI_SWG;       // SwiGLU instantiation: plain epilogue otherwise
+  constexpr int LEPI = SWG ? 0 : EPI;
+  constexpr int LN_BYTES = LEPI ? LnLds<BM, BN>::BYTES : 0;
+  static_assert(LEPI == 0 || (LEPI & EPI_STG), "ping-pong tiles: plain, SwiGLU or staged-LN epilogues");
+  static_assert(!SWG || (!HAS_RES && BN % 16 == 0), "ping-pong SwiGLU: no residual, BN % 16 == 0");
   __shared__ __attribute__((aligned(16))) char smem[LN_OFF + LN_BYTES];
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -218,7 +221,7 @@ gemm_pp_kernel(const T* __restrict__ A, int lda, const T* __restrict__ W, int ld
       *reinterpret_cast<f32x4*>(smem + BIAS_OFF + q * 16) = f32x4{(float)e[0], (float)e[1], (float)e[2], (float)e[3]};
     }
   }
-  if constexpr (EPI != 0) ln_stage<T, EPI, BM, BN, G::NT>(smem + LN_OFF, ln, m0, n0, M, N);
+  if constexpr (LEPI != 0) ln_stage<T, LEPI, BM, BN, G::NT>(smem + LN_OFF, ln, m0, n0, M, N);
   // prologue: tiles 0 .. STAGES-2 in flight, tile 0 retired and visible
 #pragma unroll
   for (int s = 0; s < STAGES - 1; ++s)
@@ -254,22 +257,26 @@ gemm_pp_kernel(const T* __restrict__ A, int lda, const T* __restrict__ W, int ld
 #endif
 
   // ---- epilogue: LDS-staged, row-coalesced (launch_gemm_pp's caller guarantees
-  // its requirements: 16-bit output, N % 8 == 0, no SwiGLU, 16-B alignment) ----
+  // its requirements: 16-bit output, N % 8 == 0 (SwiGLU: N % 16, no residual), 16-B alignment) ----
   static_assert(sizeof(OutT) == 2, "ping-pong GEMM stores 16-bit outputs");
   constexpr int SB = STAGES * G::STAGE_BYTES;
   auto go = [&](auto actf) {
-    staged_epilogue<T, OutT, BM, BN, SB, G::NT, TM, TN, HAS_BIAS, HAS_RES, decltype(actf), BIAS_OFF, EPI,
-                    EPI ? LN_OFF : -1>(smem, acc, grp * GBM + wm * WM, wn * WN, m0, n0, M, N, C, ldc, bias, R, ldr,
+    staged_epilogue<T, OutT, BM, BN, SB, G::NT, TM, TN, HAS_BIAS, HAS_RES, decltype(actf), BIAS_OFF, LEPI,
+                    LEPI ? LN_OFF : -1>(smem, acc, grp * GBM + wm * WM, wn * WN, m0, n0, M, N, C, ldc, bias, R, ldr,
                                        alpha, actf, &ln, tile_n);
   };
-  switch (act) {
-    case ACT_GELU: go([](float x) { return apply_act<ACT_GELU>(x); }); break;
-    case ACT_RELU: go([](float x) { return apply_act<ACT_RELU>(x); }); break;
-    case ACT_TANH: go([](float x) { return apply_act<ACT_TANH>(x); }); break;
-    case ACT_SILU: go([](float x) { return apply_act<ACT_SILU>(x); }); break;
-    case ACT_GELU_TANH: go([](float x) { return apply_act<ACT_GELU_TANH>(x); }); break;
-    case ACT_SIGMOID: go([](float x) { return apply_act<ACT_SIGMOID>(x); }); break;
-    default: go([](float x) { return x; }); break;
+  if constexpr (SWG) {
+    go(SwigluAct{});   // host-checked: no residual, N % 16 == 0 (gemm_pp_ok)
+  } else {
+    switch (act) {
+      case ACT_GELU: go([](float x) { return apply_act<ACT_GELU>(x); }); break;
+      case ACT_RELU: go([](float x) { return apply_act<ACT_RELU>(x); }); break;
+      case ACT_TANH: go([](float x) { return apply_act<ACT_TANH>(x); }); break;
+      case ACT_SILU: go([](float x) { return apply_act<ACT_SILU>(x); }); break;
+      case ACT_GELU_TANH: go([](float x) { return apply_act<ACT_GELU_TANH>(x); }); break;
+      case ACT_SIGMOID: go([](float x) { return apply_act<ACT_SIGMOID>(x); }); break;
+      default: go([](float x) { return x; }); break;
+    }
   }
 #ifdef RDB_PP_STAMPS
   if (tid == 0) {
@@ -284,7 +291,9 @@ gemm_pp_kernel(const T* __restrict__ A, int lda, const T* __restrict__ W, int ld
 // Host-side precondition of the ping-pong kernels' staged epilogue.
 inline bool gemm_pp_ok(int N, int ldc, int ldr, const void* C, const void* bias, const void* R, int act) {
   auto al = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
-  return act != ACT_SWIGLU && N % 8 == 0 && ldc % 8 == 0 && al(C) && (R == nullptr || (ldr % 8 == 0 && al(R)));
+  // SwiGLU: staged epilogue with N/2 output columns -- no residual, N % 16 == 0 (every pp tile's BN % 16 == 0)
+  if (act == ACT_SWIGLU) return R == nullptr && N % 16 == 0 && ldc % 8 == 0 && al(C);
+  return N % 8 == 0 && ldc % 8 == 0 && al(C) && (R == nullptr || (ldr % 8 == 0 && al(R)));
 }
 
 template <typename T, typename OutT, int NW, int BM, int BN, int GM, int GN, int STAGES, int BK = 64, int OCC = 2>
@@ -293,6 +302,15 @@ void launch_gemm_pp(const T* A, int lda, const T* W, int ldw, OutT* C, int ldc, 
   const int nwg = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
   const dim3 grid(nwg), block(64 * NW);
   const LnEpi ln{};
+  if (act == ACT_SWIGLU) {   // gemm_pp_ok: R == nullptr
+    if (bias)
+      hipLaunchKernelGGL((gemm_pp_kernel<T, OutT, NW, BM, BN, GM, GN, STAGES, true, false, BK, OCC, EPI_SWG>), grid, block,
+                         0, s, A, lda, W, ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act, ln);
+    else
+      hipLaunchKernelGGL((gemm_pp_kernel<T, OutT, NW, BM, BN, GM, GN, STAGES, false, false, BK, OCC, EPI_SWG>), grid, block,
+                         0, s, A, lda, W, ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act, ln);
+    return;
+  }
   if (bias && R)
     hipLaunchKernelGGL((gemm_pp_kernel<T, OutT, NW, BM, BN, GM, GN, STAGES, true, true, BK, OCC>), grid, block, 0, s, A, lda, W,
                        ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act, ln);

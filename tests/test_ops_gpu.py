@@ -470,6 +470,11 @@ def test_linear_swiglu_and_f16_tiles(cfg):
     w = torch.randn(512, 256, device="cuda", dtype=torch.float16) * 0.05
     _close(ops.linear(x, w, act="swiglu", tile_cfg=cfg), ops.linear_ref(x, w, act="swiglu"), 3e-2, 2e-2)
     _close(ops.linear(x, w, tile_cfg=cfg), ops.linear_ref(x, w), 3e-2, 2e-2)
+    # staged SwiGLU epilogue with bias (N % 16 == 0), and the direct one (N % 16 == 8)
+    for n in (1040, 520):
+        w2 = torch.randn(n, 256, device="cuda", dtype=torch.float16) * 0.05
+        b2 = torch.randn(n, device="cuda", dtype=torch.float16) * 0.1
+        _close(ops.linear(x, w2, b2, act="swiglu", tile_cfg=cfg), ops.linear_ref(x, w2, b2, act="swiglu"), 3e-2, 2e-2)
 
 
 @pytest.mark.parametrize("cfg", list(range(13)))
