@@ -1,6 +1,9 @@
-# round 4: same-box A/B of the LayerNorm grid cap (RDB_LN_BLOCKS: grid-stride LN on fewer blocks so the
-# other compute stream's GEMM keeps CUs) on the headline bench
+# round 4 final tree: the round-end checks (whole GPU suite, smoke) plus the 1-GPU headline bench
 set -o pipefail
-rm -f gpurun_out/abe/summary.txt
-bash tools/gpu_ab_env.sh 3 "RDB_AB=0" "RDB_LN_BLOCKS=128" "RDB_LN_BLOCKS=64" || exit $?
-mkdir -p gpurun_out/r4q && cp gpurun_out/abe/summary.txt gpurun_out/r4q/ln_blocks_ab.txt
+bash tools/fresh.sh || exit 9
+mkdir -p gpurun_out/r4q
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 600 --timeout-method thread \
+  > gpurun_out/r4q/pytest_gpu_full.log 2>&1 || exit $?
+timeout -k 10 150 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > gpurun_out/r4q/smoke.log 2>&1 || exit $?
+timeout -k 10 300 python -u bench.py > gpurun_out/r4q/bench.log 2>&1
