@@ -1,6 +1,9 @@
-# round 4: same-box tile-table A/B on the headline bench: o-proj on 64x96 (cfg 9, fastest alone),
-# FFN-down on 64x64 (cfg 3, fastest alone), FFN-up on the 256x192 ping-pong tile (cfg 25, fastest alone)
+# round 4: config 4 refresh with SwiGLU on the ping-pong tiles -- TP1 serving through the shm rings, TP8 rehearsal
 set -o pipefail
-rm -f gpurun_out/abt/summary.txt
-AB_TABLES=tools/ab_tables_r4s bash tools/gpu_ab_tables.sh 3 || exit $?
-mkdir -p gpurun_out/r4s && cp gpurun_out/abt/summary.txt gpurun_out/r4s/tables_ab.txt
+bash tools/fresh.sh || exit 9
+mkdir -p gpurun_out/r4s
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+timeout -k 10 500 python -u bench/llama_tp_bench.py --serve --json-out gpurun_out/r4s/llama3_8b_tp1_serve_r4.json \
+  > gpurun_out/r4s/serve.log 2>&1 || exit $?
+timeout -k 10 600 python -u bench/llama_tp8_rehearsal.py --world 8 --json-out gpurun_out/r4s/llama3_8b_tp8_rehearsal_r4.json \
+  > gpurun_out/r4s/rehearsal.log 2>&1
