@@ -316,9 +316,9 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
     skinny = M <= SKINNY_MAX_M and K % 32 == 0 and act != "swiglu"   # C++ routes these to the skinny-M kernel
 
     def launch(c: int, ws: Optional[torch.Tensor]) -> None:
-        if c >= 0 and (c >> 8) & 15 and ws is None:
-            # a split-K choice without a caller workspace: a private one (one memset)
-            ws = splitk_workspace(x.device, max(SPLITK_HEADER, int(_ops().conv_splitk_bytes(M, N, c & 255, (c >> 8) & 15))))
+        if c >= 0 and splits_of(c) > 1 and ws is None:
+            # a split-K choice without a caller workspace: the cached one of this stream
+            ws = _private_splitk_ws(x.device, int(_ops().conv_splitk_bytes(M, N, c & 255, splits_of(c))))
         fn(*args, _stream(), int(c), _ptr(ws), 0 if ws is None else ws.numel())
 
     if tile_cfg < 0 and od != torch.float32 and not skinny:
@@ -326,7 +326,7 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
 
         def tune_launch(c: int) -> None:
             ws = None
-            if (c >> 8) & 15:
+            if splits_of(c) > 1:
                 sid = _stream()
                 ws = _tune_ws.get(sid)
                 if ws is None:
@@ -1170,6 +1170,27 @@ _SPLITS = (2, 3, 4, 6, 8)
 _TILE_BM = (128, 64, 128, 64, 128, 192, 256, 128, 128, 64, 128, 256, 128)   # gemm_core.h kTileBM/BN, 4-wave tiles
 _TILE_BN = (128, 128, 64, 64, 192, 128, 128, 256, 144, 96, 96, 144, 48)
 _tune_ws: Dict[int, torch.Tensor] = {}
+_priv_ws: Dict[tuple, torch.Tensor] = {}
+
+
+def splits_of(c: int) -> int:
+    """Split-K factor of an encoded tile choice (0 / 1: not split).  The factor is
+    the 4-bit field at bit 8 (gemm_core.h decodes ``(cfg >> 8) & 15``): the DEEP
+    flag (bit 12) and CONV_LINEAR (bit 16) are not part of it."""
+    return 0 if c < 0 or c >= CONV_LINEAR else (c >> 8) & 15
+
+
+def _private_splitk_ws(device, need: int) -> torch.Tensor:
+    """The split-K workspace a launch without a caller workspace uses: one per
+    (device, stream), grown on demand, so a forward that passes none pays no
+    allocation or counter memset per call.  Split-K launches leave the counters
+    zero, so consecutive launches on one stream may share it (two streams never do)."""
+    key = (str(device), _stream())
+    need = max(SPLITK_HEADER, int(need))
+    ws = _priv_ws.get(key)
+    if ws is None or ws.numel() < need:
+        ws = _priv_ws[key] = splitk_workspace(device, max(need, SPLITK_WS_BYTES))
+    return ws
 
 
 def splitk_workspace(device, nbytes: int = SPLITK_WS_BYTES, zeroed: bool = True) -> torch.Tensor:
@@ -1255,9 +1276,9 @@ def conv2d_nhwc(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] =
                            out.data_ptr(), K, _ptr(bias), _ptr(residual), K if residual is not None else 0, M, K, C,
                            1.0, ACT_CODE[act], _stream(), c - CONV_LINEAR)
             return
-        if (c >> 8) > 1 and ws is None:
-            ws = splitk_workspace(x.device, max(SPLITK_HEADER,
-                                                int(_ops().conv_splitk_bytes(M, K, c & 255, c >> 8))))
+        sp = splits_of(c)
+        if sp > 1 and ws is None:
+            ws = _private_splitk_ws(x.device, int(_ops().conv_splitk_bytes(M, K, c & 255, sp)))
         fn(*args, _stream(), int(c), _ptr(ws), 0 if ws is None else ws.numel())
 
     if tile_cfg < 0:
@@ -1267,7 +1288,7 @@ def conv2d_nhwc(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] =
         def tune_launch(c: int) -> None:
             # tuning launches may overlap on side streams: one workspace per stream
             ws = None
-            if (c >> 8) > 1 and c < CONV_LINEAR:
+            if splits_of(c) > 1:
                 sid = _stream()
                 ws = _tune_ws.get(sid)
                 if ws is None:

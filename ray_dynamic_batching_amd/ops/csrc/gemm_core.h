@@ -434,6 +434,10 @@ __device__ __forceinline__ void staged_epilogue(char* smem, const f32x4 (&acc)[T
 #else
   constexpr bool kStage16 = !HAS_RES && sizeof(OutT) == 2 && !SOST;
 #endif
+  // SwigluAct is an identity functor: only the 16-bit staged branch pairs the
+  // gate / up columns into silu(g) * u at half width.
+  static_assert(kStage16 || !std::is_same<ActF, SwigluAct>::value,
+                "SwiGLU needs the 16-bit staged epilogue (not in RDB_EPI_F32_STAGING builds)");
   if constexpr (kStage16) {
     // No residual: bias + activation run once on the accumulator registers,
     // the tile is parked as 16-bit output (half the LDS traffic of f32, twice

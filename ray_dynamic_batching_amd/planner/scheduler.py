@@ -65,6 +65,7 @@ class DutyCycleExecutor(threading.Thread):
         self.loads = 0
         self.unloads = 0
         self.rerouted = 0
+        self.failed_on_unload = 0      # leftovers failed because no GPU serves the model any more
 
     def resident_bytes(self) -> int:
         return sum(self.footprint.get(m, 0) for m in self.models)
@@ -90,7 +91,10 @@ class DutyCycleExecutor(threading.Thread):
                 if cons is not None:
                     # queued requests follow the model to a GPU that serves it
                     moved = self.sched._reroute_queue(self.sched.queue_id(self.gpu, m), m, cons)
-                    self.rerouted += max(0, moved)
+                    if moved >= 0:
+                        self.rerouted += moved
+                    else:
+                        self.failed_on_unload += -moved
         for m in new_models:
             if m not in self.models:          # load
                 self.models[m] = self.sched.model_factories[m]()
@@ -601,7 +605,9 @@ class SLOScheduler:
         """Move the requests left in queue ``q`` (model ``m`` just left that GPU)
         to the least-loaded GPU queue that serves ``m`` (native
         ``Consumer.forward``: headers kept, completions reach the original
-        client); held in the ring if no GPU serves ``m`` right now."""
+        client).  If no GPU serves ``m`` in the new plan the leftovers are
+        failed at once with ST_ERROR ("model unloaded") and the count is
+        returned negated (-failed), so callers can tell moved from failed."""
         targets = [self.queue_id(g, m) for g in range(self.num_gpus)
                    if self.queue_id(g, m) != q and self.slots[g] is not None and m in self.slots[g].models()]
         cons = consumer if consumer is not None else rjob.Consumer(self.job, [q])

@@ -113,6 +113,15 @@ class JobHandle {
   }
   // Test hook (router unit tests): make queue q look `depth` deep to the
   // router without enqueuing anything (submitted = completed + depth).
+  // RDB_RING_DEBUG tests: add `delta` to the sequence number of the request
+  // slot `ahead` positions past queue q's consumer tail (simulates a producer
+  // that published the wrong lap / a stray write into the ring).
+  void test_corrupt_seq(uint32_t q, uint64_t ahead, int64_t delta) {
+    check_q(q);
+    Ring r = job_.req_ring(q);
+    SlotHeader* s = r.slot(r.h->tail.load() + ahead);
+    s->seq.fetch_add((uint64_t)delta, std::memory_order_acq_rel);
+  }
   void test_set_queue_depth(uint32_t q, uint64_t depth) {
     check_q(q);
     QueueState* s = job_.queue(q);
@@ -850,6 +859,11 @@ PYBIND11_MODULE(_rdb_runtime, m) {
   m.attr("RS_DRAINING") = (int)RS_DRAINING;
   m.attr("RS_DEAD") = (int)RS_DEAD;
   m.def("now_ns", &now_ns);
+  m.def("ring_debug_level", &ring_debug_level, "RDB_RING_DEBUG as read by this process (0 = off)");
+  m.def("ring_violations", [] {
+    RingDebugState& st = ring_debug_state();
+    return py::make_tuple(st.violations.load(), std::string(st.last));
+  }, "(count, last message) of ring sequence violations seen by this process (RDB_RING_DEBUG >= 1)");
 
   py::class_<JobHandle>(m, "Job")
       .def(py::init<const std::string&, bool, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t,
@@ -869,6 +883,7 @@ PYBIND11_MODULE(_rdb_runtime, m) {
       .def("queue_replica", &JobHandle::queue_replica)
       .def("set_queue_models", &JobHandle::set_queue_models)
       .def("_test_set_queue_depth", &JobHandle::test_set_queue_depth)
+      .def("_test_corrupt_seq", &JobHandle::test_corrupt_seq, py::arg("queue"), py::arg("ahead"), py::arg("delta"))
       .def("queue_models", &JobHandle::queue_models)
       .def("heartbeat", &JobHandle::heartbeat)
       .def("heartbeat_age_s", &JobHandle::heartbeat_age_s)

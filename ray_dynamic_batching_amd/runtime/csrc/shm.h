@@ -26,6 +26,7 @@
 #include <climits>
 #include <cstdint>
 #include <cstdlib>
+#include <cstdio>
 #include <cstring>
 #include <ctime>
 #include <fcntl.h>
@@ -129,6 +130,45 @@ struct Histogram {
 };
 
 // ---------------------------------------------------------------------------
+// Ring sequence-check debug mode ("a debug mode for the rings that
+// checks sequence numbers"; the reference's analogue is the _RAY_TSAN_BUILD /
+// sanitizer CI configs, .bazelrc:103-136).  RDB_RING_DEBUG=1 checks every
+// publish / peek / commit against the Vyukov protocol's invariants:
+//   publish(pos): the slot still holds the producer's reservation (seq == pos);
+//   peek(pos)   : pos is not behind the consumer's tail, and the slot holds
+//                 either pos (not yet published) or pos + 1 (published);
+//   commit(upto): tail <= upto <= head, and every released slot is published.
+// A violation is counted (process-wide), reported on stderr with the ring,
+// position and sequence number, and the slot is treated as unpublished so the
+// consumer never reads it; RDB_RING_DEBUG=2 aborts instead (core dump at the
+// first bad access).  Off (the default) the checks cost one predictable branch.
+// ---------------------------------------------------------------------------
+inline int ring_debug_level() {
+  static const int lvl = [] {
+    const char* e = getenv("RDB_RING_DEBUG");
+    return e ? atoi(e) : 0;
+  }();
+  return lvl;
+}
+struct RingDebugState {
+  std::atomic<uint64_t> violations{0};
+  char last[256] = {0};
+};
+inline RingDebugState& ring_debug_state() {
+  static RingDebugState st;
+  return st;
+}
+__attribute__((noinline, cold)) inline void ring_violation(const void* ring, const char* what, uint64_t pos,
+                                                           uint64_t seq, uint64_t extra) {
+  RingDebugState& st = ring_debug_state();
+  st.violations.fetch_add(1, std::memory_order_relaxed);
+  snprintf(st.last, sizeof(st.last), "ring %p: %s (pos=%llu seq=%llu other=%llu)", ring, what,
+           (unsigned long long)pos, (unsigned long long)seq, (unsigned long long)extra);
+  fprintf(stderr, "[rdb ring debug] %s\n", st.last);
+  if (ring_debug_level() >= 2) abort();
+}
+
+// ---------------------------------------------------------------------------
 // Bounded MPSC ring.
 // ---------------------------------------------------------------------------
 struct alignas(64) SlotHeader {
@@ -202,11 +242,22 @@ struct Ring {
       } else if (dif < 0) {
         return nullptr;  // full
       } else {
+        const uint64_t prev = pos;
         pos = h->head.load(std::memory_order_relaxed);
+        if (__builtin_expect(ring_debug_level() > 0, 0) && pos == prev) {
+          // head did not move, yet the slot claims a later lap: a stray
+          // publish; without the check this producer spins here forever
+          ring_violation(h, "reserve: free slot carries a sequence number ahead of head", pos, seq, 0);
+          return nullptr;
+        }
       }
     }
   }
   void publish(SlotHeader* s, uint64_t pos) {
+    if (__builtin_expect(ring_debug_level() > 0, 0)) {
+      const uint64_t q = s->seq.load(std::memory_order_acquire);
+      if (q != pos) ring_violation(h, "publish: slot no longer holds this producer's reservation", pos, q, 0);
+    }
     s->seq.store(pos + 1, std::memory_order_seq_cst);
     if (h->waiters.load(std::memory_order_seq_cst) > 0) {
       h->doorbell.fetch_add(1, std::memory_order_seq_cst);
@@ -217,11 +268,37 @@ struct Ring {
   // position pos if it has been published.
   SlotHeader* peek(uint64_t pos) const {
     SlotHeader* s = slot(pos);
-    return s->seq.load(std::memory_order_acquire) == pos + 1 ? s : nullptr;
+    const uint64_t q = s->seq.load(std::memory_order_acquire);
+    if (__builtin_expect(ring_debug_level() > 0, 0)) return checked_peek(s, pos, q);
+    return q == pos + 1 ? s : nullptr;
+  }
+  __attribute__((noinline)) SlotHeader* checked_peek(SlotHeader* s, uint64_t pos, uint64_t q) const {
+    const uint64_t tail = h->tail.load(std::memory_order_acquire);
+    if (pos < tail) {
+      ring_violation(h, "peek behind the consumer's tail", pos, q, tail);
+      return nullptr;
+    }
+    if (q == pos + 1) return s;
+    if (q != pos) ring_violation(h, "peek: sequence number is neither free nor published for this lap", pos, q, 0);
+    return nullptr;
   }
   // Release every slot in [tail, upto).
   void commit(uint64_t upto) {
     uint64_t t = h->tail.load(std::memory_order_relaxed);
+    if (__builtin_expect(ring_debug_level() > 0, 0)) {
+      const uint64_t head = h->head.load(std::memory_order_acquire);
+      if (upto < t || upto > head) {
+        ring_violation(h, "commit outside [tail, head]", upto, t, head);
+        return;
+      }
+      for (uint64_t k = t; k < upto; ++k) {
+        const uint64_t q = slot(k)->seq.load(std::memory_order_acquire);
+        if (q != k + 1) {
+          ring_violation(h, "commit releases an unpublished slot", k, q, 0);
+          return;
+        }
+      }
+    }
     for (; t < upto; ++t) slot(t)->seq.store(t + h->capacity, std::memory_order_release);
     h->tail.store(upto, std::memory_order_release);
   }

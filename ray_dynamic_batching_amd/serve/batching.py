@@ -92,6 +92,8 @@ class _BatchQueue:
         # __del__ (python/ray/serve/batching.py:323-333), which a closed loop
         # can no longer run.
         self._task: Optional[asyncio.Task] = None
+        self._crashed: Optional[BaseException] = None   # what ended the batching loop abnormally
+        self._shut = False
         self.current_iteration_start: Optional[float] = None
 
     def put(self, req: _SingleRequest) -> None:
@@ -101,7 +103,24 @@ class _BatchQueue:
             self._task = self.loop.create_task(self._loop())
 
     def is_alive(self) -> bool:
-        return self._task is not None and not self._task.done()
+        """Whether the batching loop can still serve: True while a batch task runs
+        AND while the queue is idle (the task is started again by the next put),
+        False only once the loop died of an exception or the queue was shut
+        down -- the reference's long-lived task reports exactly that
+        (python/ray/serve/batching.py:400-410), so a health check can tell a
+        crashed loop from an idle one."""
+        return self._crashed is None and not self._shut and not self.loop.is_closed()
+
+    def task_stack(self) -> Optional[str]:
+        """Formatted stack of the running batch task (reference
+        ``_get_handling_task_stack``), or None when idle."""
+        if self._task is None or self._task.done():
+            return None
+        import io
+
+        buf = io.StringIO()
+        self._task.print_stack(file=buf)
+        return buf.getvalue()
 
     async def wait_for_batch(self) -> List[_SingleRequest]:
         """Block for the first item, then keep adding until full or until
@@ -128,6 +147,20 @@ class _BatchQueue:
         return batch
 
     async def _loop(self) -> None:
+        try:
+            await self._loop_body()
+        except asyncio.CancelledError:
+            raise
+        except BaseException as e:   # the loop itself died: report it, fail the queued callers
+            self._crashed = e
+            logger.exception("batching loop crashed: %s", e)
+            while not self.queue.empty():
+                r = self.queue.get_nowait()
+                if not r.future.done():
+                    r.future.set_exception(e)
+            raise
+
+    async def _loop_body(self) -> None:
         while not self.queue.empty():
             batch = await self.wait_for_batch()
             # drop requests whose caller already gave up (cancelled)
@@ -197,6 +230,7 @@ class _BatchQueue:
                 q.put_nowait(("error", e))
 
     def shutdown(self) -> None:
+        self._shut = True
         if self._task is not None and not self._task.done() and not self.loop.is_closed():
             self._task.cancel()
 
@@ -265,7 +299,17 @@ class _LazyBatchQueue:
         return [q.current_iteration_start for q in self._queues.values()]
 
     def _is_batching_task_alive(self) -> bool:
-        return any(q.is_alive() for q in self._queues.values())
+        """False only if a queue's batching loop crashed or was shut down; a
+        queue not created yet (no request so far) counts as alive, as the
+        reference creates its queue on first access."""
+        return all(q.is_alive() for q in self._queues.values() if not q.loop.is_closed())
+
+    def _get_handling_task_stack(self) -> Optional[str]:
+        for q in self._queues.values():
+            st = q.task_stack()
+            if st:
+                return st
+        return None
 
 
 def batch(_func: Optional[Callable] = None, /, max_batch_size: int = 10, batch_wait_timeout_s: float = 0.0):
@@ -322,6 +366,7 @@ def batch(_func: Optional[Callable] = None, /, max_batch_size: int = 10, batch_w
         wrapper._get_batch_wait_timeout_s = lambda: lazy.batch_wait_timeout_s
         wrapper._get_curr_iteration_start_times = lazy._get_curr_iteration_start_times
         wrapper._is_batching_task_alive = lazy._is_batching_task_alive
+        wrapper._get_handling_task_stack = lazy._get_handling_task_stack
         wrapper._rdb_batch_queue = lazy
         return wrapper
 

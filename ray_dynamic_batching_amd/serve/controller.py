@@ -31,7 +31,7 @@ from dataclasses import dataclass, field
 from typing import Any, Dict, List, Optional, Tuple
 
 from .api import Application, Deployment
-from .autoscaling_policy import AutoscalingState
+from .autoscaling_policy import AutoscalingMetrics, AutoscalingState
 from .config import CONTROL_LOOP_INTERVAL_S, DeploymentConfig
 from .exceptions import RayServeException
 from .handle import DeploymentHandle
@@ -127,6 +127,7 @@ class DeploymentState:
     local_replicas: List[LocalReplica] = field(default_factory=list)
     proc_replicas: List[ProcReplica] = field(default_factory=list)
     autoscaler: Optional[AutoscalingState] = None
+    as_metrics: Optional[AutoscalingMetrics] = None   # look-back averaged replica ongoing counts
     init_args: tuple = ()
     init_kwargs: dict = field(default_factory=dict)
     next_index: int = 0
@@ -147,6 +148,7 @@ class ServeController:
         self.grpc_proxy = None
         self.jobs: Dict[str, Any] = {}            # app -> job segment handle (process mode)
         self.lock = threading.RLock()
+        self._clock = time.monotonic          # autoscaling look-back windows (tests may fake it)
         self.workdir = tempfile.mkdtemp(prefix="rdb_serve_")
         # RDB_SERVE_KV names a STABLE checkpoint location (the GCS-KV role): the
         # JSON document for the CLI and, beside it, the agent's persistent KV --
@@ -226,6 +228,7 @@ class ServeController:
                 st.target = cfg.initial_num_replicas()
                 if cfg.autoscaling_config is not None:
                     st.autoscaler = AutoscalingState(cfg.autoscaling_config)
+                    st.as_metrics = AutoscalingMetrics(cfg.autoscaling_config)
                 # composition: bound Applications become handles
                 st.init_args = tuple(self._to_handle(name, x) for x in a.init_args)
                 st.init_kwargs = {k: self._to_handle(name, v) for k, v in a.init_kwargs.items()}
@@ -472,13 +475,12 @@ class ServeController:
     def _health_tick(self, st: DeploymentState, last: Dict) -> None:
         now = time.time()
         if st.mode == "local":
-            key = (st.app_name, st.name)
-            if now - last.get(key, 0) < st.config.health_check_period_s:
-                return
-            last[key] = now
             changed = False
             for r in list(st.local_replicas):
-                if not r.check_health(st.config.health_check_timeout_s):
+                ok = r.poll_health(now, st.config.health_check_period_s, st.config.health_check_timeout_s)
+                if ok is None:
+                    continue                      # no check finished this tick
+                if not ok:
                     r.health_failures = getattr(r, "health_failures", 0) + 1
                     if r.health_failures >= st.config.health_check_failure_threshold:
                         logger.warning("replica %s unhealthy; replacing", r.replica_id)
@@ -508,14 +510,21 @@ class ServeController:
     def _autoscale_tick(self, st: DeploymentState) -> None:
         if st.autoscaler is None:
             return
+        # replica ongoing counts are sampled and look-back averaged
+        # (AutoscalingMetrics), not fed to the policy one raw sample per tick
         if st.mode == "local":
-            total = st.router.total_ongoing()
-            running = len(st.local_replicas)
+            ongoing = {r.replica_id: r.ongoing for r in st.local_replicas}
+            running_ids = list(ongoing)
         else:
             job = self.jobs[st.app_name]
             live = [r for r in st.proc_replicas if not r.draining]
-            total = sum(job.queue_depth(r.slot) for r in live) + st.router.num_queued()
-            running = sum(1 for r in live if r.ready)
+            ongoing = {r.slot: job.queue_depth(r.slot) for r in live}
+            running_ids = [r.slot for r in live if r.ready]
+        if st.as_metrics is None:
+            st.as_metrics = AutoscalingMetrics(st.autoscaler.cfg)
+        st.as_metrics.tick(self._clock(), ongoing)
+        total = st.as_metrics.total_num_requests(running_ids, st.router.num_queued())
+        running = len(running_ids)
         new_target = st.config.cap_replicas(st.autoscaler.step(total, running, st.target))
         if new_target != st.target:
             logger.info("autoscaling %s: %d -> %d (ongoing=%s)", st.name, st.target, new_target, total)

@@ -13,6 +13,7 @@
 from __future__ import annotations
 
 import asyncio
+import collections
 import concurrent.futures
 import itertools
 import queue as _queue
@@ -94,26 +95,97 @@ class DeploymentResponse:
 _END = object()
 
 
+class StreamSink:
+    """Thread-safe FIFO of ``(kind, value)`` stream events that a consumer can
+    wait on synchronously (``get``) or from any asyncio loop (``aget``) without
+    parking an executor thread per pending item.
+
+    The producer (a router's dispatcher thread or loop) calls ``put``; each
+    waiting coroutine is woken with ``call_soon_threadsafe`` on its own loop.
+    Reference behaviour: the streaming ObjectRefGenerator a
+    ``DeploymentResponseGenerator`` wraps (python/ray/serve/handle.py:620-743)
+    is awaited natively on the caller's loop."""
+
+    __slots__ = ("_items", "_cv", "_waiters")
+
+    def __init__(self):
+        self._items: collections.deque = collections.deque()
+        self._cv = threading.Condition(threading.Lock())
+        self._waiters: list = []          # [(loop, future)] of async consumers
+
+    def put(self, ev) -> None:
+        with self._cv:
+            self._items.append(ev)
+            self._cv.notify()
+            waiters, self._waiters = self._waiters, []
+        for loop, fut in waiters:
+            try:
+                loop.call_soon_threadsafe(_wake_future, fut)
+            except RuntimeError:          # the consumer's loop is closed
+                pass
+
+    # queue.Queue-compatible producer / consumer names
+    put_nowait = put
+
+    def get(self, timeout: Optional[float] = None):
+        with self._cv:
+            if not self._cv.wait_for(lambda: self._items, timeout):
+                raise _queue.Empty
+            return self._items.popleft()
+
+    def get_nowait(self):
+        with self._cv:
+            if not self._items:
+                raise _queue.Empty
+            return self._items.popleft()
+
+    async def aget(self):
+        loop = asyncio.get_running_loop()
+        while True:
+            with self._cv:
+                if self._items:
+                    return self._items.popleft()
+                fut = loop.create_future()
+                self._waiters.append((loop, fut))
+            await fut
+
+    def qsize(self) -> int:
+        with self._cv:
+            return len(self._items)
+
+    def empty(self) -> bool:
+        return self.qsize() == 0
+
+
+def _wake_future(fut) -> None:
+    if not fut.done():
+        fut.set_result(None)
+
+
 class DeploymentResponseGenerator:
     """Streaming response: iterate (sync or async) over the items the
-    replica's generator yields."""
+    replica's generator yields.  ``async for`` awaits the sink on the caller's
+    own loop (no thread per pending item)."""
 
-    def __init__(self, q: "_queue.Queue", meta: Optional[RequestMeta] = None, cancel_cb=None):
+    def __init__(self, q: "StreamSink", meta: Optional[RequestMeta] = None, cancel_cb=None):
         self._q = q
         self._meta = meta
         self._cancel_cb = cancel_cb
         self._done = False
 
-    def _next(self, timeout=None):
-        if self._done:
-            raise StopIteration
-        kind, val = self._q.get(timeout=timeout)
+    def _take(self, ev):
+        kind, val = ev
         if kind == "item":
             return val
         self._done = True
         if kind == "error":
             raise val
         raise StopIteration
+
+    def _next(self, timeout=None):
+        if self._done:
+            raise StopIteration
+        return self._take(self._q.get(timeout=timeout))
 
     def __iter__(self):
         return self
@@ -125,9 +197,14 @@ class DeploymentResponseGenerator:
         return self
 
     async def __anext__(self):
-        loop = asyncio.get_running_loop()
+        if self._done:
+            raise StopAsyncIteration
+        if isinstance(self._q, StreamSink):
+            ev = await self._q.aget()
+        else:                              # a plain queue.Queue from user code
+            ev = await asyncio.get_running_loop().run_in_executor(None, self._q.get)
         try:
-            return await loop.run_in_executor(None, self._next)
+            return self._take(ev)
         except StopIteration:
             raise StopAsyncIteration from None
 

@@ -15,14 +15,13 @@ import asyncio
 import concurrent.futures
 import inspect
 import logging
-import queue as _queue
 import threading
 import time
 import traceback
 from typing import Any, Dict, Optional
 
 from .context import ReplicaContext, RequestContext, _set_replica_context, _set_request_context
-from .handle import RequestMeta
+from .handle import RequestMeta, StreamSink
 
 logger = logging.getLogger("ray_dynamic_batching_amd.serve")
 
@@ -180,11 +179,39 @@ class LocalReplica:
             self.errors += 1
             raise
 
-    def call_stream(self, meta: RequestMeta, args, kwargs) -> "_queue.Queue":
-        q: _queue.Queue = _queue.Queue()
+    def call_stream(self, meta: RequestMeta, args, kwargs) -> "StreamSink":
+        q = StreamSink()
         asyncio.run_coroutine_threadsafe(self.user.call_stream(meta, args, kwargs, lambda k, v: q.put((k, v))),
                                          self._loop)
         return q
+
+    def poll_health(self, now: float, period_s: float, timeout_s: float) -> Optional[bool]:
+        """Non-blocking health check for the controller loop (the reference's
+        controller awaits ``check_health`` actor calls with a timeout and never
+        blocks its loop on one): starts a check every ``period_s``; returns
+        True / False once a check finished or timed out, None while none did."""
+        if self.dead:
+            return False
+        f = getattr(self, "_hc_future", None)
+        if f is not None:
+            if f.done():
+                self._hc_future = None
+                try:
+                    f.result()
+                    return True
+                except Exception:
+                    logger.warning("health check failed for %s:\n%s", self.replica_id, traceback.format_exc())
+                    return False
+            if now - self._hc_started > timeout_s:
+                self._hc_future = None
+                f.cancel()
+                logger.warning("health check of %s timed out after %.1fs", self.replica_id, timeout_s)
+                return False
+            return None
+        if now - getattr(self, "_hc_started", float("-inf")) >= period_s:
+            self._hc_started = now
+            self._hc_future = asyncio.run_coroutine_threadsafe(self.user.check_health(), self._loop)
+        return None
 
     def check_health(self, timeout_s: float) -> bool:
         if self.dead:

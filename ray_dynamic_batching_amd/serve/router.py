@@ -15,15 +15,15 @@ import asyncio
 import collections
 import concurrent.futures
 import logging
-import queue as _queue
 import random
 import threading
 import time
 import traceback
 from typing import Any, Callable, Deque, Dict, List, Optional, Tuple
 
-from .exceptions import BackPressureError, DeploymentUnavailableError, RayServeException, ReplicaDiedError
-from .handle import DeploymentResponse, DeploymentResponseGenerator, RequestMeta
+from .exceptions import (BackPressureError, DeploymentUnavailableError, RayServeException, ReplicaDiedError,
+                         RequestCancelledError)
+from .handle import DeploymentResponse, DeploymentResponseGenerator, RequestMeta, StreamSink
 
 logger = logging.getLogger("ray_dynamic_batching_amd.serve")
 
@@ -167,7 +167,7 @@ class LocalRouter:
             r.ongoing -= 1
             self._wake()
 
-    async def _assign_stream(self, meta, args, kwargs, out_q: "_queue.Queue"):
+    async def _assign_stream(self, meta, args, kwargs, out_q: StreamSink):
         try:
             args, kwargs = await _resolve_args(args, kwargs)
             r = await self._acquire(meta)
@@ -177,9 +177,8 @@ class LocalRouter:
         r.ongoing += 1
         try:
             src = r.call_stream(meta, args, kwargs)
-            loop = asyncio.get_running_loop()
             while True:
-                kind, val = await loop.run_in_executor(None, src.get)
+                kind, val = await src.aget()
                 out_q.put((kind, val))
                 if kind != "item":
                     break
@@ -197,7 +196,7 @@ class LocalRouter:
     def assign(self, meta: RequestMeta, args, kwargs):
         self.metrics.num_router_requests += 1
         if meta.stream:
-            q: _queue.Queue = _queue.Queue()
+            q = StreamSink()
             try:
                 self._check_backpressure()
             except BackPressureError as e:
@@ -235,13 +234,17 @@ class ShmRouter:
     _clients_lock = threading.Lock()
 
     def __init__(self, job_name: str, model_id: int, deployment: str, max_queued_requests: int = -1,
-                 tensor_codec=None, max_retries: int = 3):
+                 tensor_codec=None, retry_timeout_s: float = 60.0):
         self.job_name = job_name
         self.model_id = model_id
         self.deployment = deployment
         self.max_queued = max_queued_requests
         self.codec = tensor_codec
-        self.max_retries = max_retries
+        # Requests whose replica died are re-dispatched until this long after
+        # their submission (deadline-based like the reference's retry loop,
+        # python/ray/serve/_private/router.py:452-496, which retries until the
+        # caller gives up), not a fixed number of times.
+        self.retry_timeout_s = retry_timeout_s
         self.metrics = RouterMetrics()
         with ShmRouter._clients_lock:
             hub = ShmRouter._clients.get(job_name)
@@ -265,31 +268,66 @@ class ShmRouter:
             self.metrics.num_rejected_backpressure += 1
             err = BackPressureError(self.hub.pending_for(self.model_id), self.max_queued)
             if meta.stream:
-                q = _queue.Queue()
+                q = StreamSink()
                 q.put(("error", err))
                 return DeploymentResponseGenerator(q, meta)
             f = concurrent.futures.Future()
             f.set_exception(err)
             return DeploymentResponse(f, meta)
+        if _has_response_args(args, kwargs):
+            return self._assign_composed(meta, args, kwargs)
+        return self._assign_resolved(meta, args, kwargs)
+
+    def _assign_composed(self, meta: RequestMeta, args, kwargs):
+        """Composition without a thread per request: a done-callback on every
+        upstream response counts them down; the last one to finish (on whatever
+        thread completed it -- the dispatcher for process-mode upstreams)
+        substitutes the values and submits this request into the SAME future /
+        stream sink the caller already holds.  An upstream error fails the
+        request; cancelling the composed response before submission means it is
+        never sent, after submission the hub drops it if still queued.
+        Reference: argument resolution in python/ray/serve/_private/utils.py:605-660."""
+        ups = [a for a in args if isinstance(a, DeploymentResponse)] + \
+              [v for v in kwargs.values() if isinstance(v, DeploymentResponse)]
+        sink = ("stream", StreamSink()) if meta.stream else ("unary", concurrent.futures.Future())
+        state = {"left": len(ups), "cancelled": False}
+        lock = threading.Lock()
+
+        def submit():
+            try:
+                a = tuple(x._fut.result() if isinstance(x, DeploymentResponse) else x for x in args)
+                k = {kk: (v._fut.result() if isinstance(v, DeploymentResponse) else v) for kk, v in kwargs.items()}
+            except concurrent.futures.CancelledError:
+                _settle_sink(sink, "error", RayServeException("an upstream response of a composed request was cancelled"))
+                return
+            except BaseException as e:      # an upstream failed: so does this request
+                _settle_sink(sink, "error", e)
+                return
+            if not state["cancelled"]:
+                self._assign_resolved(meta, a, k, sink)
+
+        def on_done(_f):
+            with lock:
+                state["left"] -= 1
+                last = state["left"] == 0
+            if last:
+                submit()
+
+        def cancel_cb():
+            state["cancelled"] = True
+            self.hub.cancel(sink)
+
+        for u in ups:
+            u._fut.add_done_callback(on_done)
+        if meta.stream:
+            return DeploymentResponseGenerator(sink[1], meta, cancel_cb=cancel_cb)
+        return DeploymentResponse(sink[1], meta, cancel_cb=cancel_cb)
+
+    def _assign_resolved(self, meta: RequestMeta, args, kwargs, sink=None):
         if self.codec is not None and not meta.stream and meta.method_name == "__call__" and len(args) == 1 \
                 and not kwargs and self.codec.accepts(args[0]):
             payload, kind = self.codec.encode(args[0]), KIND_TENSOR
         else:
-            if _has_response_args(args, kwargs):
-                # composition: resolve upstream responses on a helper thread
-                fut = concurrent.futures.Future()
-
-                def _later():
-                    try:
-                        a = tuple(x.result(_skip_asyncio_check=True) if isinstance(x, DeploymentResponse) else x for x in args)
-                        k = {kk: (v.result(_skip_asyncio_check=True) if isinstance(v, DeploymentResponse) else v)
-                             for kk, v in kwargs.items()}
-                        inner = self.assign(meta, a, k)
-                        fut.set_result(inner.result(_skip_asyncio_check=True))
-                    except BaseException as e:
-                        fut.set_exception(e)
-                threading.Thread(target=_later, daemon=True).start()
-                return DeploymentResponse(fut, meta)
             import cloudpickle
 
             payload = cloudpickle.dumps((meta.method_name, args, kwargs, meta.multiplexed_model_id, meta.stream,
@@ -297,13 +335,13 @@ class ShmRouter:
             kind = KIND_PICKLE
         route = _Route(self.model_id, mux_hash(meta.multiplexed_model_id)) if meta.multiplexed_model_id \
             else self.model_id
+        deadline = time.monotonic() + self.retry_timeout_s
+        if sink is None:
+            sink = ("stream", StreamSink()) if meta.stream else ("unary", concurrent.futures.Future())
+        self.hub.submit(route, payload, kind, sink, self.codec, deadline)
         if meta.stream:
-            q = _queue.Queue()
-            self.hub.submit(route, payload, kind, ("stream", q), self.codec, self.max_retries)
-            return DeploymentResponseGenerator(q, meta)
-        fut = concurrent.futures.Future()
-        self.hub.submit(route, payload, kind, ("unary", fut), self.codec, self.max_retries)
-        return DeploymentResponse(fut, meta)
+            return DeploymentResponseGenerator(sink[1], meta, cancel_cb=lambda: self.hub.cancel(sink))
+        return DeploymentResponse(sink[1], meta, cancel_cb=lambda: self.hub.cancel(sink))
 
 
 def mux_hash(model_id: str) -> int:
@@ -326,7 +364,13 @@ class _Route(int):
 
 
 class _ShmClientHub:
-    """Per-process native Client + dispatcher thread for one job segment."""
+    """Per-process native Client + dispatcher thread for one job segment.
+
+    Request state (pending FIFO, in-flight table) is guarded by ``lock``; the
+    futures / stream sinks of callers are settled only AFTER the lock is
+    released (``_settle`` defers, ``_flush`` runs), so a done-callback that
+    submits a composed request -- possibly into another hub -- never runs
+    under this hub's lock (no lock-order inversion between hubs)."""
 
     def __init__(self, job_name: str):
         from ..runtime import job as rjob
@@ -337,34 +381,89 @@ class _ShmClientHub:
         self.client = rjob.Client(self.job)
         self.lock = threading.Lock()
         self.inflight: Dict[int, Tuple] = {}
+        self.retries = 0
         self.pending: Deque[Tuple] = collections.deque()
         self.closed = False
         self._pending_by_model: Dict[int, int] = collections.Counter()
+        self._deferred: List[Callable[[], None]] = []
+        self._deferred_lock = threading.Lock()
         from ..utils.faults import injector
 
         self.faults = injector()
         self.thread = threading.Thread(target=self._run, name=f"rdb-dispatch-{job_name}", daemon=True)
         self.thread.start()
 
+    # -- settlement outside the lock ------------------------------------------
+    def _settle(self, fn: Callable[[], None]) -> None:
+        with self._deferred_lock:
+            self._deferred.append(fn)
+
+    def _flush(self) -> None:
+        while True:
+            with self._deferred_lock:
+                todo, self._deferred = self._deferred, []
+            if not todo:
+                return
+            for fn in todo:
+                try:
+                    fn()
+                except Exception:  # pragma: no cover - a user callback raised
+                    logger.exception("completion callback failed")
+
+    def _fail(self, sink, exc) -> None:
+        self._settle(lambda: _settle_sink(sink, "error", exc))
+
+    # -- public entry points ---------------------------------------------------
     def pending_for(self, model_id: int) -> int:
         return self._pending_by_model[model_id]
 
     def kick(self) -> None:
         with self.lock:
             self._drain_pending()
+        self._flush()
 
-    def submit(self, model_id, payload, kind, sink, codec, retries_left) -> None:
+    def submit(self, model_id, payload, kind, sink, codec, retry_deadline) -> None:
         with self.lock:
-            if self.pending:
-                self.pending.append((model_id, payload, kind, sink, codec, retries_left))
+            item = (model_id, payload, kind, sink, codec, retry_deadline)
+            if self.pending or not self._try_submit(*item):
+                self.pending.append(item)
                 self._pending_by_model[model_id] += 1
                 self._drain_pending()
-                return
-            if not self._try_submit(model_id, payload, kind, sink, codec, retries_left):
-                self.pending.append((model_id, payload, kind, sink, codec, retries_left))
-                self._pending_by_model[model_id] += 1
+        self._flush()
 
-    def _try_submit(self, model_id, payload, kind, sink, codec, retries_left) -> bool:
+    def cancel(self, sink) -> None:
+        """Cancel a request: a queued one is never sent; an in-flight one's
+        result is discarded (the replica still finishes the batch it is in)."""
+        kind, obj = sink
+        if kind == "unary":
+            obj.cancel()
+        else:
+            obj.put(("error", RequestCancelledError("stream cancelled")))
+        with self.lock:
+            for rid in [r for r, e in self.inflight.items() if e[3] is sink]:
+                del self.inflight[rid]
+
+    # -- internals (lock held) -------------------------------------------------
+    @staticmethod
+    def _sink_cancelled(sink) -> bool:
+        return sink[0] == "unary" and sink[1].cancelled()
+
+    def _retry(self, entry, why: str) -> None:
+        """Re-dispatch a request whose replica died, at the front of the FIFO,
+        while its retry deadline has not passed; fail it after that."""
+        model_id, payload, kind, sink, codec, deadline = entry[:6]
+        if self._sink_cancelled(sink):
+            return
+        if time.monotonic() < deadline:
+            self.retries += 1
+            self.pending.appendleft((model_id, payload, kind, sink, codec, deadline))
+            self._pending_by_model[model_id] += 1
+        else:
+            self._fail(sink, ReplicaDiedError(f"{why}; retry window exhausted"))
+
+    def _try_submit(self, model_id, payload, kind, sink, codec, retry_deadline) -> bool:
+        if self._sink_cancelled(sink):
+            return True                    # cancelled while queued: drop it
         q = self.client.choose_queue(int(model_id), getattr(model_id, "mux", 0))
         if q == -2:
             self._fail(sink, DeploymentUnavailableError(f"no replica serves model id {int(model_id)}"))
@@ -381,7 +480,7 @@ class _ShmClientHub:
         if rid < 0:
             return False
         rep = self.job.queue_replica(q)
-        self.inflight[rid] = (model_id, payload, kind, sink, codec, retries_left, q, rep,
+        self.inflight[rid] = (model_id, payload, kind, sink, codec, retry_deadline, q, rep,
                               self.job.replica_generation(rep))
         return True
 
@@ -393,14 +492,33 @@ class _ShmClientHub:
             self.pending.popleft()
             self._pending_by_model[item[0]] -= 1
 
-    @staticmethod
-    def _fail(sink, exc) -> None:
-        kind, obj = sink
-        if kind == "unary":
-            if not obj.done():
-                obj.set_exception(exc)
-        else:
-            obj.put(("error", exc))
+    def _complete(self, entry, st, kind, payload) -> None:
+        import cloudpickle
+
+        St = self.Status
+        sink, codec = entry[3], entry[4]
+        try:
+            if st == St.OK:
+                if sink[0] == "stream":
+                    self._settle(lambda: _settle_sink(sink, "end", None))
+                else:
+                    val = codec.decode(payload) if kind == KIND_TENSOR else (
+                        cloudpickle.loads(payload) if payload else None)
+                    self._settle(lambda: _settle_sink(sink, "ok", val))
+            elif st == St.ERROR:
+                self._fail(sink, cloudpickle.loads(payload) if payload else RayServeException("replica error"))
+            elif st == St.DROPPED_STALE:
+                from .exceptions import RequestDroppedError
+
+                self._fail(sink, RequestDroppedError("request dropped: its SLO deadline could not be met"))
+            elif st in (St.REPLICA_DIED, St.SHUTDOWN):
+                self._retry(entry, f"replica failed the request (status {int(st)})")
+            elif st == St.TOO_LARGE:
+                self._fail(sink, RayServeException("result larger than the completion slot"))
+            else:
+                self._fail(sink, ReplicaDiedError(f"request failed with status {int(st)}"))
+        except Exception as e:  # pragma: no cover - decode failure
+            self._fail(sink, e)
 
     def _run(self) -> None:
         import cloudpickle
@@ -416,62 +534,36 @@ class _ShmClientHub:
                 last_check = time.time()
                 with self.lock:
                     self._reap_lost()
+                self._flush()
             if not comps:
                 if self.pending:
-                    with self.lock:
-                        self._drain_pending()
+                    self.kick()
                 continue
             with self.lock:
                 for rid, st, q, ts, td, tr, kind, payload in comps:
                     entry = self.inflight.get(rid)
                     if entry is None:
-                        continue
-                    model_id, req_payload, req_kind, sink, codec, retries = entry[:6]
+                        continue              # cancelled, or already retried
                     if kind == KIND_STREAM_ITEM and st == St.OK:
-                        sink[1].put(("item", cloudpickle.loads(payload)))
+                        item = cloudpickle.loads(payload)
+                        entry[3][1].put(("item", item))   # stream sinks are thread-safe
                         continue
                     del self.inflight[rid]
-                    try:
-                        if st == St.OK:
-                            if sink[0] == "stream":
-                                sink[1].put(("end", None))
-                            elif kind == KIND_TENSOR:
-                                sink[1].set_result(codec.decode(payload))
-                            else:
-                                sink[1].set_result(cloudpickle.loads(payload) if payload else None)
-                        elif st == St.ERROR:
-                            exc = cloudpickle.loads(payload) if payload else RayServeException("replica error")
-                            self._fail(sink, exc)
-                        elif st == St.DROPPED_STALE:
-                            from .exceptions import RequestDroppedError
-
-                            self._fail(sink, RequestDroppedError("request dropped: its SLO deadline could not be met"))
-                        elif st in (St.REPLICA_DIED, St.SHUTDOWN) and retries > 0:
-                            self.pending.appendleft((model_id, req_payload, req_kind, sink, codec, retries - 1))
-                            self._pending_by_model[model_id] += 1
-                        elif st == St.TOO_LARGE:
-                            self._fail(sink, RayServeException("result larger than the completion slot"))
-                        else:
-                            self._fail(sink, ReplicaDiedError(f"request failed with status {int(st)}"))
-                    except Exception as e:  # pragma: no cover - decode failure
-                        self._fail(sink, e)
+                    self._complete(entry, st, kind, payload)
                 self._drain_pending()
+            self._flush()
 
     def _reap_lost(self) -> None:
         """Requests a replica popped but never answered because it died (its
-        generation changed or it is DEAD) are re-dispatched (idempotent forward)."""
+        generation changed or it is DEAD) are re-dispatched (idempotent forward)
+        within their retry window."""
         lost = []
         for rid, e in self.inflight.items():
             rep, gen = e[7], e[8]
             if self.job.replica_generation(rep) != gen or self.job.replica_status(rep) == 4:
                 lost.append(rid)
         for rid in lost:
-            model_id, payload, kind, sink, codec, retries = self.inflight.pop(rid)[:6]
-            if retries > 0:
-                self.pending.appendleft((model_id, payload, kind, sink, codec, retries - 1))
-                self._pending_by_model[model_id] += 1
-            else:
-                self._fail(sink, ReplicaDiedError("replica died while processing the request"))
+            self._retry(self.inflight.pop(rid), "replica died while processing the request")
         if lost:
             self._drain_pending()
 
@@ -479,6 +571,19 @@ class _ShmClientHub:
         self.closed = True
         if self.thread.is_alive() and self.thread is not threading.current_thread():
             self.thread.join(2.0)
+
+
+def _settle_sink(sink, what: str, val) -> None:
+    kind, obj = sink
+    if kind == "unary":
+        if obj.done():
+            return
+        if what == "ok":
+            obj.set_result(val)
+        else:
+            obj.set_exception(val)
+    else:
+        obj.put(("error", val) if what == "error" else ("end", None))
 
 
 def _close_all_hubs() -> None:

@@ -224,7 +224,8 @@ def test_autoscaling_local_scales_up_and_down():
     gate = threading.Event()
 
     @serve.deployment(max_ongoing_requests=2, autoscaling_config=dict(
-        min_replicas=1, max_replicas=3, target_ongoing_requests=1, upscale_delay_s=0.0, downscale_delay_s=0.3))
+        min_replicas=1, max_replicas=3, target_ongoing_requests=1, upscale_delay_s=0.0, downscale_delay_s=0.3,
+        metrics_interval_s=0.1, look_back_period_s=0.3))
     class AS:
         def __call__(self):
             gate.wait(10)

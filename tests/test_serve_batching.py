@@ -200,11 +200,38 @@ def test_idle_queue_leaves_no_pending_task_and_dead_loops_are_pruned():
         loop = asyncio.new_event_loop()
         async def main():
             return await asyncio.gather(*[f(i) for i in range(6)])
+        assert f._is_batching_task_alive()        # idle is not dead
         assert loop.run_until_complete(main()) == list(range(6))
-        assert not f._is_batching_task_alive()
+        assert f._is_batching_task_alive()        # idle again: still alive (reference semantics)
+        assert f._get_handling_task_stack() is None
         assert not [t for t in asyncio.all_tasks(loop) if not t.done()]
         loop.close()
     loop = asyncio.new_event_loop()
     assert loop.run_until_complete(f(7)) == 7
     assert len(lazy._queues) == 1
     loop.close()
+
+
+def test_batching_task_alive_reports_a_crashed_loop():
+    """``_is_batching_task_alive`` is True before the first request and while
+    idle, False once the batching loop itself died (reference
+    tests/test_batching.py:190-206 and batching.py:400-410)."""
+    @serve.batch(max_batch_size=4, batch_wait_timeout_s=0.01)
+    async def f(xs):
+        return xs
+
+    loop = asyncio.new_event_loop()
+    try:
+        assert f._is_batching_task_alive()
+        assert loop.run_until_complete(f(1)) == 1
+        assert f._is_batching_task_alive()
+        q = next(iter(f._rdb_batch_queue._queues.values()))
+
+        async def boom():
+            raise RuntimeError("loop died")
+        q.wait_for_batch = boom
+        with pytest.raises(RuntimeError, match="loop died"):
+            loop.run_until_complete(f(2))
+        assert not f._is_batching_task_alive()
+    finally:
+        loop.close()
