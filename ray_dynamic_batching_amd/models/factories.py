@@ -96,3 +96,40 @@ def shufflenet_v2(backend: str = "hip") -> Factory:
 
 def efficientnet_v2s(backend: str = "hip") -> Factory:
     return Factory(_efficientnet, ((384, 384, 3), torch.uint8, (10,), torch.float32), backend=backend)
+
+
+class TPFactory(Factory):
+    """Factory of a tensor-parallel servable: Serve's TP replicas call it on
+    every rank with the rank's shard coordinates."""
+
+    def __call__(self, device="cuda", tp_rank: int = 0, tp_size: int = 1, group_name=None):
+        return self.fn(device=device, tp_rank=tp_rank, tp_size=tp_size, group_name=group_name, **self.kw)
+
+
+def _tp_echo(device, tp_rank, tp_size, group_name, d, d_out):
+    from .tp_echo import TPEcho
+
+    return TPEcho(d, d_out, tp_rank, tp_size, group_name, device=device)
+
+
+def tp_echo(d: int = 16, d_out: int = 8) -> TPFactory:
+    """Row-parallel linear + all-reduce (CPU / gloo or GPU / RCCL): Serve TP plumbing."""
+    return TPFactory(_tp_echo, ((d,), torch.float32, (d_out + 1,), torch.float32), d=d, d_out=d_out)
+
+
+def _llama(device, tp_rank, tp_size, group_name, config, backend, seq_len, overrides):
+    from .llama import LlamaConfig, LlamaTP
+
+    kw = dict(overrides or {}, seq_len=seq_len)
+    cfg = LlamaConfig.llama3_8b(**kw) if config == "8b" else LlamaConfig.tiny(**kw)
+    return LlamaTP(cfg, tp_rank=tp_rank, tp_size=tp_size, group_name=group_name, device=device, backend=backend,
+                   init="full" if config != "8b" else "shard")
+
+
+def llama3(config: str = "8b", seq_len: int = 128, backend: str = "hip", **overrides) -> TPFactory:
+    """Llama-3 prefill servable (next-token id per prompt of ``seq_len`` tokens),
+    sharded over the TP group (BASELINE config 4).  ``config``: "8b" (random
+    shards) or "tiny" (full-matrix init, identical for every TP size);
+    ``overrides``: LlamaConfig fields (layers, heads, ...)."""
+    return TPFactory(_llama, ((seq_len,), torch.int32, (2,), torch.int32), config=config, backend=backend,
+                     seq_len=seq_len, overrides=dict(overrides))

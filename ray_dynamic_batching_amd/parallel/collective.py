@@ -55,9 +55,11 @@ def _backend(backend: str) -> str:
 
 
 def init_collective_group(world_size: int, rank: int, backend: str = "nccl", group_name: str = "default",
-                          master_addr: Optional[str] = None, master_port: Optional[int] = None) -> None:
+                          master_addr: Optional[str] = None, master_port: Optional[int] = None,
+                          store=None) -> None:
     """Join a named collective group.  The first group initialises the default
-    torch process group (rendezvous via MASTER_ADDR/MASTER_PORT or the args)."""
+    torch process group (rendezvous via ``store`` -- e.g. the node agent's
+    ``parallel.rendezvous.agent_store`` -- or MASTER_ADDR/MASTER_PORT / the args)."""
     b = _backend(backend)
     with _lock:
         if group_name in _groups:
@@ -68,7 +70,7 @@ def init_collective_group(world_size: int, rank: int, backend: str = "nccl", gro
             if master_port:
                 os.environ["MASTER_PORT"] = str(master_port)
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-            kw = {}
+            kw = {} if store is None else {"store": store}
             if b == "nccl":
                 dev = torch.device("cuda", torch.cuda.current_device())
                 kw["device_id"] = dev

@@ -502,6 +502,35 @@ struct Proc {
   Job* job = nullptr;
   int replica = -1;
   std::vector<uint32_t> queues;
+  int group = 0;   // > 0: member of a gang-spawned process group (never restarts alone)
+  int rank = -1;
+};
+
+// A gang of processes that live and die together: one tensor-parallel replica
+// (rank 0 owns the replica slot in the job; ranks 1..N-1 follow it over RCCL).
+// If ANY member exits (or rank 0 misses heartbeats) every member is killed, the
+// replica's pending and in-flight requests are failed / re-dispatched once, the
+// group's epoch is bumped (rendezvous keys of the old epoch, "tp/<owner>/...",
+// are deleted from the KV) and the whole group restarts after a back-off.
+// Reference: placement-group bundles of a Serve deployment
+// (python/ray/serve/api.py:240-259) whose ranks rendezvous through a named
+// store (collective_group/nccl_collective_group.py:555-577); Ray restarts the
+// replica actor, this agent restarts the gang.
+struct Group {
+  int id = 0;
+  std::string owner;
+  std::vector<int> members;   // proc ids, rank order
+  int epoch = 0;
+  int state = 0;              // ProcState of the gang
+  int restarts = 0;
+  int max_restarts = -1;
+  double backoff_initial_s = 0.5, backoff_max_s = 30.0;
+  int64_t next_start_ns = 0;
+  std::string last_exit;
+  bool restart = true;
+  Job* job = nullptr;
+  int replica = -1;
+  std::vector<uint32_t> queues;
 };
 
 class NodeAgent {
@@ -552,6 +581,106 @@ class NodeAgent {
       procs_[id] = std::move(p);
       return id;
     }
+  }
+  // Gang spawn (see Group): argvs / envs / logs per rank.  Every member gets
+  // RDB_TP_RANK, RDB_TP_WORLD, RDB_TP_GROUP (= owner) and RDB_TP_EPOCH in its
+  // environment; rank 0 carries the replica slot (heartbeats, queues).
+  int spawn_group(const std::string& owner, std::vector<std::vector<std::string>> argvs,
+                  std::vector<py::dict> envs, std::vector<std::string> logs, const std::string& job_name,
+                  int replica, std::vector<uint32_t> queues, double hb_timeout_s, int max_restarts,
+                  double backoff_initial_s, double backoff_max_s) {
+    const size_t n = argvs.size();
+    if (n == 0) throw std::invalid_argument("spawn_group: no ranks");
+    if (envs.size() != n || logs.size() != n) throw std::invalid_argument("spawn_group: argvs/envs/logs sizes differ");
+    std::vector<std::unique_ptr<Proc>> ps;
+    for (size_t r = 0; r < n; ++r) {
+      if (argvs[r].empty()) throw std::invalid_argument("spawn_group: empty argv");
+      auto p = std::make_unique<Proc>();
+      p->owner = owner + "/rank" + std::to_string(r);
+      p->argv = argvs[r];
+      std::map<std::string, std::string> env;
+      for (char** e = environ; *e; ++e) {
+        std::string kv(*e);
+        auto eq = kv.find('=');
+        if (eq != std::string::npos) env[kv.substr(0, eq)] = kv.substr(eq + 1);
+      }
+      for (auto item : envs[r]) {
+        const std::string k = py::str(item.first);
+        if (item.second.is_none()) env.erase(k);
+        else env[k] = py::str(item.second);
+      }
+      env["RDB_TP_RANK"] = std::to_string(r);
+      env["RDB_TP_WORLD"] = std::to_string(n);
+      env["RDB_TP_GROUP"] = owner;
+      env["RDB_TP_EPOCH"] = "0";
+      for (auto& kv : env) p->env.push_back(kv.first + "=" + kv.second);
+      p->log_path = logs[r];
+      p->replica = r == 0 ? replica : -1;
+      if (r == 0) p->queues = queues;
+      p->hb_timeout_s = r == 0 ? hb_timeout_s : 0.0;
+      p->max_restarts = max_restarts;
+      p->rank = (int)r;
+      ps.push_back(std::move(p));
+    }
+    std::lock_guard<std::mutex> lk(mu_);
+    auto g = std::make_unique<Group>();
+    g->id = next_group_++;
+    g->owner = owner;
+    g->max_restarts = max_restarts;
+    g->backoff_initial_s = backoff_initial_s;
+    g->backoff_max_s = backoff_max_s;
+    g->replica = replica;
+    g->queues = queues;
+    if (!job_name.empty()) g->job = attach_job(job_name);
+    for (auto& p : ps) {
+      p->job = g->job;
+      p->group = g->id;
+      p->id = next_id_++;
+      g->members.push_back(p->id);
+      start_locked(*p);
+      procs_[p->id] = std::move(p);
+    }
+    g->state = P_STARTING;
+    const int gid = g->id;
+    groups_[gid] = std::move(g);
+    events_.emplace_back(gid, "group_started", owner);
+    return gid;
+  }
+  // Stop a whole group for good.
+  bool terminate_group(int gid, double grace_s) {
+    std::vector<int> ids;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      auto it = groups_.find(gid);
+      if (it == groups_.end()) return false;
+      it->second->restart = false;
+      it->second->state = P_STOPPED;
+      ids = it->second->members;
+    }
+    bool ok = true;
+    for (int id : ids) ok = terminate(id, grace_s) && ok;
+    return ok;
+  }
+  py::dict group_info(int gid) {
+    std::lock_guard<std::mutex> lk(mu_);
+    auto it = groups_.find(gid);
+    if (it == groups_.end()) throw std::out_of_range("unknown group id");
+    const Group& g = *it->second;
+    py::dict d;
+    d["id"] = g.id;
+    d["owner"] = g.owner;
+    d["epoch"] = g.epoch;
+    d["state"] = state_name(g.state);
+    d["restarts"] = g.restarts;
+    d["last_exit"] = g.last_exit;
+    d["members"] = g.members;
+    py::list pids;
+    for (int id : g.members) {
+      auto pit = procs_.find(id);
+      pids.append(pit == procs_.end() ? -1 : (int)pit->second->pid);
+    }
+    d["pids"] = pids;
+    return d;
   }
   // Stop a process for good (no restart): SIGTERM its group, SIGKILL after grace.
   bool terminate(int id, double grace_s) {
@@ -733,6 +862,12 @@ class NodeAgent {
     return raw;
   }
   void start_locked(Proc& p) {
+    if (p.group > 0) {   // a (re)started gang member sees the group's current epoch
+      auto git = groups_.find(p.group);
+      if (git != groups_.end())
+        for (auto& e : p.env)
+          if (e.rfind("RDB_TP_EPOCH=", 0) == 0) e = "RDB_TP_EPOCH=" + std::to_string(git->second->epoch);
+    }
     posix_spawn_file_actions_t fa;
     posix_spawn_file_actions_init(&fa);
     if (!p.log_path.empty()) {
@@ -801,6 +936,58 @@ class NodeAgent {
     p.state = P_BACKOFF;
     events_.emplace_back(p.id, "died", why + "; restart in " + std::to_string(back) + " s");
   }
+  // A member of gang g died (or was killed for missed heartbeats): take the
+  // whole gang down, fail the replica's requests once, bump the epoch and
+  // schedule the gang's restart.
+  void group_death_locked(int gid, Proc& dead, const std::string& why) {
+    auto it = groups_.find(gid);
+    if (it == groups_.end()) return;
+    Group& g = *it->second;
+    dead.pid = -1;
+    dead.last_exit = why;
+    for (int id : g.members) {
+      auto pit = procs_.find(id);
+      if (pit == procs_.end() || pit->second->pid <= 0) continue;
+      Proc& m = *pit->second;
+      kill(-m.pid, SIGKILL);
+      int st = 0;
+      for (int i = 0; i < 500 && waitpid(m.pid, &st, WNOHANG) == 0; ++i) usleep(1000);
+      m.pid = -1;
+      m.last_exit = "killed with its group (rank " + std::to_string(dead.rank) + ": " + why + ")";
+    }
+    if (g.job && g.replica >= 0 && (uint32_t)g.replica < g.job->hdr()->n_replicas) {
+      ReplicaState* rs = g.job->replica(g.replica);
+      rs->status.store(RS_DEAD);
+      for (uint32_t q : g.queues)
+        if (q < g.job->hdr()->n_queues) {
+          fail_pending(*g.job, q, ST_REPLICA_DIED);
+          forget_inflight(*g.job, q);
+        }
+      rs->restarts.fetch_add(1);  // generation bump: routers re-dispatch what was in flight
+    }
+    ++g.epoch;
+    for (auto& k : kv_.keys("tp/" + g.owner + "/")) kv_.del(k);
+    g.last_exit = "rank " + std::to_string(dead.rank) + ": " + why;
+    const bool again = g.restart && !stopped_.load() && !(g.max_restarts >= 0 && g.restarts >= g.max_restarts);
+    int st_new = P_STOPPED;
+    if (again) {
+      ++g.restarts;
+      const double back = std::min(g.backoff_max_s, g.backoff_initial_s * std::pow(2.0, std::min(g.restarts - 1, 20)));
+      g.next_start_ns = now_ns() + (int64_t)(back * 1e9);
+      st_new = P_BACKOFF;
+      events_.emplace_back(g.id, "group_died", g.last_exit + "; restart in " + std::to_string(back) + " s");
+    } else {
+      st_new = g.restart ? P_EXITED : P_STOPPED;
+      events_.emplace_back(g.id, "group_stopped", g.last_exit);
+    }
+    g.state = st_new;
+    for (int id : g.members) {
+      auto pit = procs_.find(id);
+      if (pit == procs_.end()) continue;
+      pit->second->state = st_new;
+      pit->second->restarts = g.restarts;
+    }
+  }
   void monitor_loop() {
     const int interval_ms = std::max(1, (int)Config::instance().get_double("agent_monitor_interval_ms"));
     while (!stop_.load()) {
@@ -816,7 +1003,8 @@ class NodeAgent {
               std::string why = WIFEXITED(st) ? "exit code " + std::to_string(WEXITSTATUS(st))
                                               : "signal " + std::to_string(WTERMSIG(st));
               kill(-p.pid, SIGKILL);  // reap stragglers of its process group
-              on_death_locked(p, why);
+              if (p.group > 0) group_death_locked(p.group, p, why);
+              else on_death_locked(p, why);
               continue;
             }
             if (p.job && p.replica >= 0 && (uint32_t)p.replica < p.job->hdr()->n_replicas) {
@@ -828,14 +1016,34 @@ class NodeAgent {
                 kill(-p.pid, SIGKILL);
                 int st2 = 0;
                 for (int i = 0; i < 200 && waitpid(p.pid, &st2, WNOHANG) == 0; ++i) usleep(1000);
-                on_death_locked(p, "missed heartbeats for " + std::to_string(age) + " s");
+                const std::string why = "missed heartbeats for " + std::to_string(age) + " s";
+                if (p.group > 0) group_death_locked(p.group, p, why);
+                else on_death_locked(p, why);
               }
             } else if (p.state == P_STARTING) {
               p.state = P_RUNNING;
             }
-          } else if (p.state == P_BACKOFF && now >= p.next_start_ns) {
+          } else if (p.group == 0 && p.state == P_BACKOFF && now >= p.next_start_ns) {
             start_locked(p);
           }
+        }
+        for (auto& gkv : groups_) {   // gangs restart together
+          Group& g = *gkv.second;
+          if (g.state == P_STARTING) {
+            bool all = true;
+            for (int id : g.members) {
+              auto pit = procs_.find(id);
+              all = all && pit != procs_.end() && pit->second->state == P_RUNNING;
+            }
+            if (all) g.state = P_RUNNING;
+          }
+          if (g.state != P_BACKOFF || now < g.next_start_ns) continue;
+          for (int id : g.members) {
+            auto pit = procs_.find(id);
+            if (pit != procs_.end()) start_locked(*pit->second);
+          }
+          g.state = P_STARTING;
+          events_.emplace_back(g.id, "group_restarted", "epoch " + std::to_string(g.epoch));
         }
       }
       std::this_thread::sleep_for(std::chrono::milliseconds(interval_ms));
@@ -893,6 +1101,8 @@ class NodeAgent {
   KvStore kv_;
   std::mutex mu_;
   std::map<int, std::unique_ptr<Proc>> procs_;
+  std::map<int, std::unique_ptr<Group>> groups_;
+  int next_group_ = 1;
   std::map<std::string, std::unique_ptr<Job>> jobs_;
   std::deque<std::tuple<int, std::string, std::string>> events_;
   int next_id_ = 1;
@@ -995,6 +1205,13 @@ void register_node_agent(py::module_& m) {
            py::arg("max_restarts") = -1, py::arg("backoff_initial_s") = 0.5, py::arg("backoff_max_s") = 30.0)
       .def("terminate", &NodeAgent::terminate, py::arg("id"), py::arg("grace_s") = 5.0,
            py::call_guard<py::gil_scoped_release>())
+      .def("spawn_group", &NodeAgent::spawn_group, py::arg("owner"), py::arg("argvs"), py::arg("envs"),
+           py::arg("logs"), py::arg("job") = "", py::arg("replica") = -1,
+           py::arg("queues") = std::vector<uint32_t>{}, py::arg("health_timeout_s") = 30.0,
+           py::arg("max_restarts") = -1, py::arg("backoff_initial_s") = 0.5, py::arg("backoff_max_s") = 30.0)
+      .def("terminate_group", &NodeAgent::terminate_group, py::arg("group"), py::arg("grace_s") = 5.0,
+           py::call_guard<py::gil_scoped_release>())
+      .def("group_info", &NodeAgent::group_info)
       .def("kill", &NodeAgent::kill_proc, py::arg("id"), py::arg("sig") = 9)
       .def("info", &NodeAgent::info)
       .def("list", &NodeAgent::list)

@@ -10,7 +10,11 @@ One process per GPU (torchrun); the group is ONE replica of the serving job:
   (column/row-parallel linears with RCCL all-reduces captured in the graph);
 * rank 0 writes each prompt's next-token id into the completion ring.
 
-Used by bench/llama_tp_bench.py --serve and tests (TP=1 on one GPU).
+Used by Serve's tensor-parallel deployments (``serve.model_deployment(...,
+tensor_parallel_size=N)``: the node agent gang-spawns the ranks and they meet
+through its KV, serve/replica_main.py ``_run_tp``), by bench/llama_tp_bench.py
+--serve and by tests.  Any servable works: requests are ``input_shape`` x
+``input_dtype`` tensors, results ``output_shape`` x ``output_dtype`` rows.
 """
 from __future__ import annotations
 
@@ -22,7 +26,8 @@ import torch
 
 class TPReplica:
     def __init__(self, model, job_name: Optional[str], replica: int, queue: int, buckets: List[int],
-                 group: Optional[str] = None, max_wait_s: float = 0.002, use_graphs: bool = True):
+                 group: Optional[str] = None, max_wait_s: float = 0.002, use_graphs: bool = True,
+                 gpu_index: int = -1):
         """``use_graphs=False`` runs each batch eagerly instead of replaying the
         bucket's hipGraph (tests with several TP ranks sharing one GPU)."""
         from ..parallel import collective as col
@@ -36,9 +41,12 @@ class TPReplica:
         self.max_wait_s = max_wait_s
         self.queue = queue
         self.replica = replica
-        self.dev = model.device
-        S = model.cfg.seq_len
-        self.ids: Dict[int, torch.Tensor] = {b: torch.zeros(b, S, dtype=torch.int32, device=self.dev)
+        self.dev = torch.device(getattr(model, "device", "cpu"))
+        self.in_shape = tuple(model.input_shape)
+        self.in_dtype = model.input_dtype
+        self.gpu_index = gpu_index if gpu_index >= 0 else (
+            torch.cuda.current_device() if self.dev.type == "cuda" else -1)
+        self.ids: Dict[int, torch.Tensor] = {b: torch.zeros(b, *self.in_shape, dtype=self.in_dtype, device=self.dev)
                                              for b in self.buckets}
         self.out: Dict[int, torch.Tensor] = {}
         self.graphs: Dict[int, torch.cuda.CUDAGraph] = {}
@@ -57,7 +65,7 @@ class TPReplica:
     def capture(self) -> "TPReplica":
         if not self.use_graphs:
             if self.job is not None:
-                self.job.set_replica_status(self.replica, 2, torch.cuda.current_device(), 0)
+                self.job.set_replica_status(self.replica, 2, self.gpu_index, 0)
             return self
         with torch.no_grad():
             for b in self.buckets:
@@ -77,7 +85,7 @@ class TPReplica:
                 self.graphs[b] = g
         torch.cuda.synchronize()
         if self.job is not None:
-            self.job.set_replica_status(self.replica, 2, torch.cuda.current_device(), 0)
+            self.job.set_replica_status(self.replica, 2, self.gpu_index, 0)
         return self
 
     def _bucket(self, n: int) -> int:
@@ -89,7 +97,6 @@ class TPReplica:
     def step(self, timeout_s: float = 0.05) -> int:
         """One serving step on every rank; returns the number of prompts served
         (0 = idle, -1 = stop)."""
-        S = self.model.cfg.seq_len
         reqs = []
         if self.rank == 0:
             t_end = time.perf_counter() + timeout_s
@@ -102,9 +109,9 @@ class TPReplica:
             b = self._bucket(n) if n else 0
             self.hdr[0], self.hdr[1] = b, n
             if n:
-                host = torch.zeros(b, S, dtype=torch.int32)
+                host = torch.zeros(b, *self.in_shape, dtype=self.in_dtype)
                 for i, r in enumerate(reqs):
-                    host[i] = torch.frombuffer(bytearray(r[6]), dtype=torch.int32)
+                    host[i] = torch.frombuffer(bytearray(r[6]), dtype=self.in_dtype).view(self.in_shape)
                 self.ids[b].copy_(host, non_blocking=False)
         if self.world > 1:
             self.col.broadcast(self.hdr, 0, self.group)

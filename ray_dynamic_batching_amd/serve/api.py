@@ -124,7 +124,8 @@ def deployment(_func_or_class: Optional[Union[Callable, type]] = None, *, name: 
                health_check_period_s: Optional[float] = None, health_check_timeout_s: Optional[float] = None,
                logging_config=None, slo_ms: Optional[float] = None, profile_csv: Optional[str] = None,
                priority: Optional[int] = None, drop_stale: Optional[bool] = None,
-               engine: Union[Dict, EngineConfig, None] = None):
+               engine: Union[Dict, EngineConfig, None] = None, tensor_parallel_size: Optional[int] = None,
+               tp_backend: Optional[str] = None):
     """Decorator turning a class or function into a Deployment
     (signature of serve/api.py:240-259 plus the Nexus SLO fields)."""
     given = {k: v for k, v in dict(
@@ -135,7 +136,8 @@ def deployment(_func_or_class: Optional[Union[Callable, type]] = None, *, name: 
         autoscaling_config=autoscaling_config, graceful_shutdown_wait_loop_s=graceful_shutdown_wait_loop_s,
         graceful_shutdown_timeout_s=graceful_shutdown_timeout_s, health_check_period_s=health_check_period_s,
         health_check_timeout_s=health_check_timeout_s, logging_config=logging_config, slo_ms=slo_ms,
-        profile_csv=profile_csv, priority=priority, drop_stale=drop_stale, engine=engine).items() if v is not None}
+        profile_csv=profile_csv, priority=priority, drop_stale=drop_stale, engine=engine,
+        tensor_parallel_size=tensor_parallel_size, tp_backend=tp_backend).items() if v is not None}
     if isinstance(given.get("autoscaling_config"), AutoscalingConfig):
         given["autoscaling_config"] = given["autoscaling_config"].model_dump()
     if isinstance(given.get("engine"), EngineConfig):

@@ -84,6 +84,12 @@ class DeploymentConfig(BaseModel):
     priority: int = 0
     drop_stale: bool = False
     engine: EngineConfig = Field(default_factory=EngineConfig)
+    # Tensor-parallel replica: the node agent gang-spawns `tensor_parallel_size`
+    # rank processes (one per placement bundle; default: that many bundles of
+    # ray_actor_options' num_gpus / hbm each), they rendezvous through the
+    # agent's KV, rank 0 serves the replica's queue and the group restarts as one.
+    tensor_parallel_size: int = 1
+    tp_backend: Optional[str] = None       # "nccl" (= RCCL) / "gloo"; default: nccl when ranks hold GPUs
 
     @field_validator("logging_config", mode="before")
     @classmethod
@@ -148,6 +154,13 @@ class DeploymentConfig(BaseModel):
             st = self.placement_group_strategy or "PACK"
             if st not in ("PACK", "SPREAD", "STRICT_PACK", "STRICT_SPREAD"):
                 raise ValueError("placement_group_strategy must be PACK, SPREAD, STRICT_PACK or STRICT_SPREAD")
+        if not isinstance(self.tensor_parallel_size, int) or self.tensor_parallel_size < 1:
+            raise ValueError("tensor_parallel_size must be an int >= 1")
+        if self.tensor_parallel_size > 1 and self.placement_group_bundles is not None \
+                and len(self.placement_group_bundles) != self.tensor_parallel_size:
+            raise ValueError("a tensor-parallel deployment needs one placement bundle per rank")
+        if self.tp_backend is not None and self.tp_backend not in ("nccl", "rccl", "gloo"):
+            raise ValueError("tp_backend must be nccl / rccl / gloo")
         if self.max_replicas_per_node is not None and not (1 <= self.max_replicas_per_node <= 100):
             raise ValueError("max_replicas_per_node must be in [1, 100]")
         return self
@@ -170,6 +183,10 @@ class DeploymentConfig(BaseModel):
             return None
         return [(float(b.get("GPU", 0)), float(b.get("hbm_gb", b.get("memory_gb", 0)) or 0))
                 for b in self.placement_group_bundles]
+
+    def tp_bundles(self):
+        """[(num_gpus, hbm_gb)] per rank of a tensor-parallel replica."""
+        return self.placement_bundles() or [(self.num_gpus, self.hbm_gb)] * self.tensor_parallel_size
 
     @property
     def num_gpus(self) -> float:

@@ -103,7 +103,8 @@ def lookup_router(app_name: str, deployment: str):
 @dataclass
 class ProcReplica:
     slot: int                 # replica index in the job segment (== queue id)
-    proc_id: int = -1         # node-agent process handle
+    proc_id: int = -1         # node-agent process handle (rank 0's, for a TP replica)
+    group_id: int = -1        # node-agent gang of a tensor-parallel replica
     alloc: Any = None
     started_at: float = 0.0
     ready: bool = False
@@ -309,11 +310,72 @@ class ServeController:
         self._routes_path = path
         self.jobs[app_name].publish(json.dumps(routes).encode())   # live copy for replicas
 
+    def _replica_env(self, st: DeploymentState, rep: ProcReplica, job) -> Dict[str, str]:
+        env = {"RDB_ROUTING_TABLE": self._routes_path, "RDB_JOB": job.info()["name"]}
+        if self.agent_socket:   # user metrics (utils.user_metrics) are published through the agent KV
+            env["RDB_AGENT_SOCKET"] = self.agent_socket
+            env["RDB_METRICS_KEY"] = f"{st.app_name}/{st.name}/{rep.slot}"
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+        pkg_root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        env["PYTHONPATH"] = pkg_root + os.pathsep + os.environ.get("PYTHONPATH", "")
+        return env
+
+    def _spawn_tp(self, st: DeploymentState, rep: ProcReplica, owner: str) -> bool:
+        """A tensor-parallel replica: one placement bundle per rank, gang-reserved;
+        the agent spawns the ranks as one group (each pinned to its bundle's
+        GPUs), they rendezvous through the agent KV (parallel/rendezvous.py),
+        rank 0 owns the replica slot and the group restarts as one.  Reference:
+        placement_group_bundles (python/ray/serve/api.py:240-259)."""
+        from ..runtime.resources import visible_devices_env
+
+        if not self.agent_socket:
+            raise RayServeException("tensor-parallel replicas need the node agent's control socket (KV rendezvous)")
+        n = st.config.tensor_parallel_size
+        alloc = self.agent.allocate_bundles(owner, st.config.tp_bundles(),
+                                            st.config.placement_group_strategy or "PACK")
+        if alloc is None:
+            logger.warning("no GPU capacity for TP replica %s (%d ranks)", owner, n)
+            return False
+        rep.alloc = alloc
+        job = self.jobs[st.app_name]
+        gpus = list(alloc["gpus"])
+        job.configure_queue(rep.slot, rep.slot, st.model_id, st.config.max_ongoing_requests,
+                            float(st.config.slo_ms or 0.0), True)
+        job.set_replica_status(rep.slot, 1, gpus[0] if gpus else -1, 0)
+        base = self._replica_env(st, rep, job)
+        argvs, envs, logs = [], [], []
+        for i, g in enumerate(alloc["bundle_gpus"]):
+            env = dict(base)
+            env.update(visible_devices_env(list(g)))
+            envs.append(env)
+            argvs.append([sys.executable, "-m", "ray_dynamic_batching_amd.serve.replica_main", "--spec",
+                          st.spec_path, "--replica", str(rep.slot), "--gpu", ",".join(map(str, g))])
+            logs.append(os.path.join(self.workdir, f"{owner.replace('#', '.')}.rank{i}.log"))
+        rep.group_id = self.agent.spawn_group(owner, argvs, envs, logs, job.info()["name"], rep.slot, [rep.slot],
+                                              float(st.config.health_check_timeout_s), -1, 0.5, 30.0)
+        rep.proc_id = self.agent.group_info(rep.group_id)["members"][0]
+        rep.started_at = time.time()
+        rep.ready = False
+        rep.health_failures = 0
+        return True
+
+    def _stop_replica_procs(self, rep: ProcReplica, grace_s: float) -> None:
+        if rep.group_id >= 0:
+            members = self.agent.group_info(rep.group_id)["members"]
+            self.agent.terminate_group(rep.group_id, grace_s)
+            for m in members:
+                self.agent.forget(m)
+        elif rep.proc_id >= 0:
+            self.agent.terminate(rep.proc_id, grace_s)
+            self.agent.forget(rep.proc_id)
+
     def _spawn(self, st: DeploymentState, rep: ProcReplica) -> bool:
         from ..runtime.resources import visible_devices_env
 
         owner = f"{st.app_name}#{st.name}#{rep.slot}"
         self.agent.release(owner)
+        if st.config.tensor_parallel_size > 1:
+            return self._spawn_tp(st, rep, owner)
         bundles = st.config.placement_bundles()
         if bundles is not None:
             # gang reservation of every bundle (placement group); the replica
@@ -331,14 +393,7 @@ class ServeController:
                             float(st.config.slo_ms or 0.0), True)
         job.set_replica_status(rep.slot, 1, gpus[0] if gpus else -1, 0)
         env = dict(visible_devices_env(gpus))
-        env["RDB_ROUTING_TABLE"] = self._routes_path
-        env["RDB_JOB"] = job.info()["name"]
-        if self.agent_socket:   # user metrics (utils.user_metrics) are published through the agent KV
-            env["RDB_AGENT_SOCKET"] = self.agent_socket
-            env["RDB_METRICS_KEY"] = f"{st.app_name}/{st.name}/{rep.slot}"
-        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
-        pkg_root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-        env["PYTHONPATH"] = pkg_root + os.pathsep + os.environ.get("PYTHONPATH", "")
+        env.update(self._replica_env(st, rep, job))
         cmd = [sys.executable, "-m", "ray_dynamic_batching_amd.serve.replica_main", "--spec", st.spec_path,
                "--replica", str(rep.slot), "--gpu", ",".join(map(str, gpus))]
         log = os.path.join(self.workdir, f"{owner.replace('#', '.')}.log")
@@ -418,9 +473,7 @@ class ServeController:
             deadline = time.time() + st.config.graceful_shutdown_timeout_s
             while time.time() < deadline and job.queue_depth(rep.slot) > 0:
                 time.sleep(st.config.graceful_shutdown_wait_loop_s / 20)
-            if rep.proc_id >= 0:
-                self.agent.terminate(rep.proc_id, 5.0)
-                self.agent.forget(rep.proc_id)
+            self._stop_replica_procs(rep, 5.0)
             job.fail_queue(rep.slot, 6)
             job.set_replica_status(rep.slot, 4, -1, 0)
             self.agent.release(f"{st.app_name}#{st.name}#{rep.slot}")
@@ -621,9 +674,7 @@ class ServeController:
                 for r in st.local_replicas:
                     r.shutdown(st.config.graceful_shutdown_timeout_s)
                 for rep in st.proc_replicas:
-                    if rep.proc_id >= 0:
-                        self.agent.terminate(rep.proc_id, 10.0)
-                        self.agent.forget(rep.proc_id)
+                    self._stop_replica_procs(rep, 10.0)
                     self.agent.release(f"{st.app_name}#{st.name}#{rep.slot}")
             job = self.jobs.pop(name, None)
             if job is not None:

@@ -49,13 +49,22 @@ def main(argv=None) -> int:
     job = rjob.Job(spec["job"], create=False)
     r = a.replica
     gpu = int(a.gpu.split(",")[0]) if a.gpu else -1
-    job.set_replica_status(r, 1, gpu, os.getpid())
-    stop = threading.Event()
+    from ..parallel.rendezvous import TPEnv
 
-    def _term(*_):
-        stop.set()
-    signal.signal(signal.SIGTERM, _term)
-    if os.environ.get("RDB_AGENT_SOCKET") and os.environ.get("RDB_METRICS_KEY"):
+    tp = TPEnv.from_env()
+    follower = tp is not None and tp.rank > 0     # TP ranks 1..N-1: no replica slot of their own
+    stop = threading.Event()
+    if follower:
+        # a follower blocks inside collectives: let SIGTERM end it at once (the
+        # agent stops / restarts the whole group together)
+        signal.signal(signal.SIGTERM, signal.SIG_DFL)
+    else:
+        job.set_replica_status(r, 1, gpu, os.getpid())
+
+        def _term(*_):
+            stop.set()
+        signal.signal(signal.SIGTERM, _term)
+    if not follower and os.environ.get("RDB_AGENT_SOCKET") and os.environ.get("RDB_METRICS_KEY"):
         from ..utils import user_metrics
 
         user_metrics.start_publisher(os.environ["RDB_AGENT_SOCKET"], os.environ["RDB_METRICS_KEY"])
@@ -64,7 +73,8 @@ def main(argv=None) -> int:
 
     def heartbeat():
         while not stop.is_set():
-            job.heartbeat(r)
+            if not follower:
+                job.heartbeat(r)
             # orphaned (the controller / node agent process died without
             # terminating us): leave instead of serving a job nobody supervises;
             # a recovering controller starts its own replicas
@@ -85,13 +95,70 @@ def main(argv=None) -> int:
                                           capture_user_logs=True)
     ctx.logger.info("replica starting (pid %d, gpu %s)", os.getpid(), gpu)
     try:
+        if tp is not None:
+            return _run_tp(spec, cfg, r, stop, tp, gpu)
         if spec.get("servable"):
             return _run_engine(spec, cfg, job, r, stop)
         return _run_python(spec, cfg, job, r, stop, ctx)
     except Exception:
         logger.error("replica failed:\n%s", traceback.format_exc())
-        job.set_replica_status(r, 4, gpu, os.getpid())
+        if not follower:
+            job.set_replica_status(r, 4, gpu, os.getpid())
         return 1
+
+
+def _run_tp(spec, cfg, r, stop, tp, gpu) -> int:
+    """One rank of a tensor-parallel replica (the agent gang-spawned every rank
+    of the group).  Ranks meet through the agent's KV, build their model shard
+    and run the TPReplica loop: rank 0 pops batches from the replica's queue and
+    broadcasts them, every rank runs its shard's forward (collectives inside),
+    rank 0 answers.  Any rank failing ends the process, and the agent restarts
+    the whole group."""
+    import torch
+
+    from ..parallel import collective as col
+    from ..parallel.rendezvous import init_tp_group
+    from ..runtime.tp_replica import TPReplica
+
+    sv = spec.get("servable")
+    if not sv:
+        raise RuntimeError("tensor_parallel_size > 1 needs a servable model deployment (serve.model_deployment)")
+    use_gpu = gpu >= 0 and not os.environ.get("RDB_NO_GPU") and torch.cuda.is_available()
+    if use_gpu:
+        torch.cuda.set_device(0)
+    backend = cfg.tp_backend or ("nccl" if use_gpu else "gloo")
+    t0 = time.time()
+    init_tp_group(backend, "tp", tp)
+    logger.info("TP rank %d/%d joined group %s epoch %d over %s in %.2fs", tp.rank, tp.world, tp.group, tp.epoch,
+                backend, time.time() - t0)
+    if use_gpu and backend == "nccl" and os.environ.get("RDB_TP_XGMI", "0") == "1":
+        col.enable_xgmi("tp")           # the custom xGMI all-reduce (fused residual + RMSNorm)
+    factory = sv["factory"]
+    model = factory(device="cuda" if use_gpu else "cpu", tp_rank=tp.rank, tp_size=tp.world, group_name="tp")
+    if use_gpu and tp.world > 1 and os.environ.get("RDB_TP_LINE_UP", "0") == "1" and hasattr(model, "pre_collective"):
+        # rehearsal of a TP group on ONE GPU: every rank drains its stream and
+        # meets the others before each all-reduce (a rank spinning in the xGMI
+        # kernel would hold the CU slots a peer's GEMM needs); never on a node
+        # where each rank has its own GPU
+        def _line_up():
+            torch.cuda.synchronize()
+            col.barrier("tp")
+        model.pre_collective = _line_up
+    eng = cfg.engine
+    buckets = eng.buckets or [1, 2, 4, 8, 16, 32][: max(1, sv["max_batch_size"].bit_length())]
+    buckets = sorted({min(b, sv["max_batch_size"]) for b in buckets} | {sv["max_batch_size"]})
+    rep = TPReplica(model, spec["job"] if tp.rank == 0 else None, r, r, buckets, group="tp",
+                    max_wait_s=sv["batch_wait_timeout_s"],
+                    use_graphs=use_gpu and os.environ.get("RDB_TP_GRAPHS", "1") == "1", gpu_index=gpu)
+    rep.capture()                      # rank 0 marks the replica READY
+    while True:
+        if tp.rank == 0 and stop.is_set():
+            rep.stop_all()
+            break
+        if rep.step(0.05) < 0:
+            break
+    logger.info("TP rank %d leaves after %d batches / %d requests", tp.rank, rep.batches, rep.requests)
+    return 0
 
 
 def _run_engine(spec, cfg, job, r, stop) -> int:
