@@ -141,13 +141,20 @@ def main():
         print(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={os.environ['WORLD_SIZE']} ranks",
               file=sys.stderr)
         sys.exit(2)
-    import torch
-    import torch.distributed as dist
-
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     echo = args.backend == "echo"
+    # NUMA placement BEFORE the HIP runtime or any native thread starts: this
+    # rank's process (engine launcher, completer, load generator threads all
+    # inherit it) is pinned to its own share of the CPUs local to its GPU
+    from ray_dynamic_batching_amd.runtime import numa
+
+    rank_gpus = [0] * world if (args.rehearse_one_gpu or world == 1) else list(range(world))
+    placement = dict(rank=rank, gpu=rank_gpus[rank], **numa.place_rank(rank, rank_gpus))
+    import torch
+    import torch.distributed as dist
+
     if echo:
         if world > 1:
             dist.init_process_group("gloo")
@@ -184,12 +191,15 @@ def main():
     name = f"bench_{port}"
     n = world
     if rank == 0:
+        # request rings deferred: each rank first-touches its own ring from its
+        # pinned CPUs, with the pages bound to its GPU's NUMA node
         job = rjob.Job(name, create=True, n_replicas=n, n_queues=n, n_clients=max(8, n * max(4, args.ingress_threads)), req_capacity=4096,
-                       req_slot_bytes=args.seq * 4, cmp_capacity=16384, cmp_slot_bytes=64)
+                       req_slot_bytes=args.seq * 4, cmp_capacity=16384, cmp_slot_bytes=64, defer_req_rings=True)
     barrier()
     if rank != 0:
         job = rjob.Job(name, create=False)
     # each rank owns queue `rank` (model 0) on replica `rank`
+    placement["arena_mbind"] = job.init_req_ring(rank, placement["numa_node"])
     job.configure_queue(rank, rank, 0, args.concurrency * 2, 0.0, True)
 
     cfg = BertConfig(seq_len=args.seq, layers=args.layers)
@@ -287,6 +297,10 @@ def main():
                 for r, st in enumerate(states):
                     if r != 0 and st is not None:
                         gens[0].merge_state(*st)
+    placements = [placement]
+    if world > 1:
+        placements = [None] * world
+        dist.all_gather_object(placements, placement, group=host_pg)
     if rank == 0:
         result["latency"] = gens[0].latency()
     if rank == 0 and args.trace_out:
@@ -331,6 +345,7 @@ def main():
             "gpu_busy_frac": round(sum(r["busy_ms"] for r in rep) / (n * elapsed * 1e3), 3) if elapsed > 0 else None,
             "per_replica_requests": [r["batch_items"] for r in rep],
             "ingress": f"{args.ingress} x{G} thread(s)",
+            "placement": placements,
         }
         if os.environ.get("RDB_ABLATE"):
             line["metric"] = f"ABLATION (skips {os.environ['RDB_ABLATE']}: wrong outputs, not a measurement): " + METRIC

@@ -63,9 +63,10 @@ class JobHandle {
  public:
   JobHandle(const std::string& name, bool create, uint32_t n_replicas, uint32_t n_queues,
             uint32_t n_clients, uint32_t req_capacity, uint32_t req_slot_bytes,
-            uint32_t cmp_capacity, uint32_t cmp_slot_bytes, double attach_timeout_s) {
+            uint32_t cmp_capacity, uint32_t cmp_slot_bytes, double attach_timeout_s, bool defer_req_rings) {
     if (create) {
       JobConfig c;
+      c.defer_req_rings = defer_req_rings;
       c.n_replicas = n_replicas;
       c.n_queues = n_queues;
       c.n_clients = n_clients;
@@ -82,6 +83,10 @@ class JobHandle {
   Job& job() { return job_; }
   void close() { job_.close(); }
   void unlink_on_close(bool v) { job_.set_unlink_on_close(v); }
+  int init_req_ring(uint32_t q, int numa_node) {
+    check_q(q);
+    return job_.init_req_ring(q, numa_node);
+  }
 
   void configure_queue(uint32_t q, uint32_t replica, uint32_t model, uint32_t max_ongoing,
                        double slo_ms, bool active) {
@@ -867,11 +872,14 @@ PYBIND11_MODULE(_rdb_runtime, m) {
 
   py::class_<JobHandle>(m, "Job")
       .def(py::init<const std::string&, bool, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t,
-                    uint32_t, uint32_t, double>(),
+                    uint32_t, uint32_t, double, bool>(),
            py::arg("name"), py::arg("create") = false, py::arg("n_replicas") = 1,
            py::arg("n_queues") = 1, py::arg("n_clients") = 8, py::arg("req_capacity") = 4096,
            py::arg("req_slot_bytes") = 1024, py::arg("cmp_capacity") = 8192,
-           py::arg("cmp_slot_bytes") = 256, py::arg("attach_timeout_s") = 30.0)
+           py::arg("cmp_slot_bytes") = 256, py::arg("attach_timeout_s") = 30.0,
+           py::arg("defer_req_rings") = false)
+      .def("init_req_ring", &JobHandle::init_req_ring, py::arg("queue"), py::arg("numa_node") = -1,
+           "consumer-side init of a deferred request ring, its pages bound to numa_node first")
       .def("close", &JobHandle::close)
       .def("unlink_on_close", &JobHandle::unlink_on_close)
       .def("configure_queue", &JobHandle::configure_queue, py::arg("queue"), py::arg("replica"),

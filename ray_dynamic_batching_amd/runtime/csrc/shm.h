@@ -477,7 +477,22 @@ struct JobConfig {
   uint32_t n_replicas = 1, n_queues = 1, n_clients = 8;
   uint32_t req_capacity = 4096, req_slot_bytes = 1024;
   uint32_t cmp_capacity = 8192, cmp_slot_bytes = 256;
+  // Leave the request rings' slot pages untouched at creation: each queue's
+  // consumer initialises its own ring (Job::init_req_ring) after binding those
+  // pages to its GPU's NUMA node, so payloads are first-touched -- and later
+  // gathered by the GPU -- on the consumer's socket, not the creator's.
+  bool defer_req_rings = false;
 };
+
+// Bind [addr, addr + len) to one NUMA node (MPOL_PREFERRED; no libnuma
+// needed).  Returns 0 or -errno.  A node < 0 is a no-op.
+inline int mbind_preferred(void* addr, size_t len, int node) {
+  if (node < 0 || node >= 1024) return 0;
+  unsigned long mask[1024 / (8 * sizeof(unsigned long))] = {0};
+  mask[node / (8 * sizeof(unsigned long))] = 1UL << (node % (8 * sizeof(unsigned long)));
+  const long rc = syscall(SYS_mbind, addr, len, 1 /* MPOL_PREFERRED */, mask, (unsigned long)1024, 0);
+  return rc == 0 ? 0 : -errno;
+}
 
 inline uint32_t round_pow2(uint32_t v) {
   uint32_t p = 1;
@@ -540,7 +555,15 @@ class Job {
     h->next_req_id.store(1);
     h->created_ns.store(now_ns());
     strncpy(h->name, name.c_str(), sizeof(h->name) - 1);
-    for (uint32_t q = 0; q < cfg.n_queues; ++q) req_ring(q).init(cfg.req_capacity, cfg.req_slot_bytes);
+    for (uint32_t q = 0; q < cfg.n_queues; ++q) {
+      if (cfg.defer_req_rings) {       // header only (one page); slots wait for init_req_ring
+        Ring r = req_ring(q);
+        r.h->capacity = cfg.req_capacity;
+        r.h->slot_bytes = cfg.req_slot_bytes;
+      } else {
+        req_ring(q).init(cfg.req_capacity, cfg.req_slot_bytes);
+      }
+    }
     for (uint32_t c = 0; c < cfg.n_clients; ++c) cmp_ring(c).init(cfg.cmp_capacity, cfg.cmp_slot_bytes);
     h->magic.store(kMagic, std::memory_order_release);
   }
@@ -604,6 +627,17 @@ class Job {
   char* base() const { return base_; }
   size_t size() const { return size_; }
   const std::string& name() const { return name_; }
+  // Consumer-side initialisation of request ring q (JobConfig::defer_req_rings):
+  // bind its pages to `numa_node` (< 0: leave the policy alone), then write the
+  // slot sequence numbers from this (CPU-pinned) process: first touch is local.
+  // Must run before any producer can pick the queue.  Returns the mbind result.
+  int init_req_ring(uint32_t q, int numa_node) {
+    Ring r = req_ring(q);
+    const uint64_t sz = (Ring::bytes(hdr()->req_capacity, hdr()->req_slot_bytes) + 4095) & ~4095ULL;
+    const int rc = mbind_preferred(reinterpret_cast<char*>(r.h), sz, numa_node);
+    r.init(hdr()->req_capacity, hdr()->req_slot_bytes);
+    return rc;
+  }
   // Byte range of the request rings (what a GPU replica pins for zero-copy H2D).
   std::pair<char*, size_t> request_region() const {
     return {base_ + hdr()->off_req, (size_t)(hdr()->off_cmp - hdr()->off_req)};
