@@ -94,7 +94,7 @@ class XgmiCommunicator:
         # Store flavour of the fused-norm output: 0 plain (default), 1 nontemporal, 2
         # write-through (sc1).  Plain stores keep the normalised rows in the XCD's L2
         # for the GEMM that reads them next.  (Round 2 made sc1 the default after a
-        # graph-replay test read "unwritten" rows; tools/gpu_xgmi_cause*.sh showed the
+        # graph-replay test read "unwritten" rows; tools/archive/gpu_xgmi_cause*.sh showed the
         # rows were unwritten because the two in-process ranks' streams shared one
         # hardware queue and the barrier timed out -- every store flavour and both
         # copy engines pass once the ranks run concurrently, tests/test_xgmi_gpu.py.)

@@ -45,7 +45,7 @@ def _streams(n):
     stream the process created before): rank 1's kernel then starts only after
     rank 0's has timed out in its barrier (error 1, rows never written).  That
     was the round-2 "unwritten fused-norm rows" finding: it followed the test
-    ORDER, not the store flavour or the copy engine (tools/gpu_xgmi_cause*.sh).
+    ORDER, not the store flavour or the copy engine (tools/archive/gpu_xgmi_cause*.sh).
     Streams of DIFFERENT priorities always get different hardware queues."""
     if n > 2:
         raise ValueError("in-process ranks: at most 2 (one stream per priority level)")

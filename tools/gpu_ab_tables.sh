@@ -5,7 +5,7 @@ mkdir -p gpurun_out/abt
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 R=$1; shift
 for r in $(seq 1 $R); do
-  for t in ${AB_TABLES:-tools/ab_tables}/*.json; do
+  for t in ${AB_TABLES:-tools/archive/ab_tables}/*.json; do
     n=$(basename $t .json)
     timeout -k 10 150 python -u bench.py --steps 2000 --warmup 50 --tile-table $t "$@" > gpurun_out/abt/${n}_r$r.log 2>&1
     rc=$?
