@@ -55,6 +55,10 @@ def test_tp_deployment_serves_through_serve_run(world):
         np.testing.assert_allclose(y[:8], x @ w.T, rtol=1e-4, atol=1e-4)   # sum of the N row-parallel partials
         assert y[8] == world                                               # every rank contributed
     c, info = _group(world)
+    deadline = time.time() + 10           # the agent's monitor marks the gang RUNNING on its next pass
+    while info["state"] != "RUNNING" and time.time() < deadline:
+        time.sleep(0.05)
+        info = c.agent.group_info(info["id"])
     assert info["state"] == "RUNNING" and info["epoch"] == 0 and all(p > 0 for p in info["pids"])
     # the store address was published under the group's epoch in the agent KV
     assert any(k.startswith("tp/default#tpecho#") and k.endswith("/0/store") for k in c.agent.kv_keys("tp/"))
