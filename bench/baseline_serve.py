@@ -84,7 +84,8 @@ def main(argv=None):
     pending = asyncio.all_tasks(loop)
     for t in pending:
         t.cancel()
-    loop.run_until_complete(asyncio.gather(*pending, return_exceptions=True))
+    if pending:   # (an idle @serve.batch queue leaves no task behind)
+        loop.run_until_complete(asyncio.gather(*pending, return_exceptions=True))
     loop.close()
     lat_ms = np.array(lat) * 1e3
     out = {"metric": "baseline req/s (1 GPU, Python @serve.batch + eager forward, no RPC)", "backend": a.backend,
