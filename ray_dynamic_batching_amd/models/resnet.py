@@ -188,24 +188,43 @@ class ResNet50:
         pooled = ops.avgpool_nhwc(x)
         return ops.linear(pooled, self.fc_w, self.fc_b, out_dtype=torch.float32)
 
+    def _torch_params(self):
+        """The torch arm's weights, converted ONCE (NCHW tensors in channels_last
+        memory, i.e. the NHWC layout MIOpen's fp16 convolutions run on) -- never
+        inside a forward, so a captured graph holds only the convolutions."""
+        tp = getattr(self, "_tp", None)
+        if tp is None:
+            dt = self.dtype if self.device.type == "cuda" else torch.float32
+            cl = torch.channels_last
+
+            def w(x):
+                return x.permute(0, 3, 1, 2).to(dt).contiguous(memory_format=cl)
+            tp = dict(dt=dt, mean=torch.tensor([0.485, 0.456, 0.406], device=self.device).view(1, 1, 1, 3),
+                      std=torch.tensor([0.229, 0.224, 0.225], device=self.device).view(1, 1, 1, 3),
+                      stem=(w(self.stem_w[..., :3]), self.stem_b.to(dt)),
+                      blocks=[{k: (w(blk[k]), blk["b" + k[1:]].to(dt)) for k in ("w1", "w2", "w3", "wd") if k in blk}
+                              for blk in self.blocks])
+            self._tp = tp
+        return tp
+
     def _logits_torch(self, img):
-        """Eager PyTorch baseline (NCHW via channels_last, same folded weights)."""
-        dt = self.dtype if self.device.type == "cuda" else torch.float32
-        mean = torch.tensor([0.485, 0.456, 0.406], device=img.device)
-        std = torch.tensor([0.229, 0.224, 0.225], device=img.device)
-        x = ((img.float() / 255.0 - mean) / std).permute(0, 3, 1, 2).to(dt)
+        """Eager PyTorch baseline (NCHW tensors in channels_last memory = MIOpen's
+        NHWC fp16 convolutions, same folded weights)."""
+        tp = self._torch_params()
+        dt = tp["dt"]
+        x = ((img.float() / 255.0 - tp["mean"]) / tp["std"]).to(dt).permute(0, 3, 1, 2)
 
-        def cv(x, w, b, s=1, p=0):
-            return F.conv2d(x, w.permute(0, 3, 1, 2).to(dt), b.to(dt), stride=s, padding=p)
+        def cv(x, wb, s=1, p=0):
+            return F.conv2d(x, wb[0], wb[1], stride=s, padding=p)
 
-        x = F.relu(cv(x, self.stem_w[..., :3], self.stem_b, 2, 3))
+        x = F.relu(cv(x, tp["stem"], 2, 3))
         x = F.max_pool2d(x, 3, 2, 1)
-        for blk in self.blocks:
+        for blk, tb in zip(self.blocks, tp["blocks"]):
             s = blk["stride"]
-            h = F.relu(cv(x, blk["w1"], blk["b1"]))
-            h = F.relu(cv(h, blk["w2"], blk["b2"], s, 1))
-            sc = cv(x, blk["wd"], blk["bd"], s) if "wd" in blk else x
-            x = F.relu(cv(h, blk["w3"], blk["b3"]) + sc)
+            h = F.relu(cv(x, tb["w1"]))
+            h = F.relu(cv(h, tb["w2"], s, 1))
+            sc = cv(x, tb["wd"], s) if "wd" in tb else x
+            x = F.relu(cv(h, tb["w3"]) + sc)
         pooled = x.float().mean(dim=(2, 3))
         return (pooled @ self.fc_w.float().t() + self.fc_b.float()).float()
 
