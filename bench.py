@@ -77,6 +77,9 @@ def parse():
                          "exists; none = tune per shape and in context at start-up)")
     ap.add_argument("--json-out", default="")
     ap.add_argument("--trace-out", default="", help="write a Chrome trace of the replicas' batches")
+    ap.add_argument("--stamps-out", default="",
+                    help="diagnostic: with the RDB_BLOCK_STAMPS kernel build (RDB_OPS_SO), save every block's start / "
+                         "end / CU of the timed region to this .npy (bench/stamp_timeline.py); never a measurement")
     return ap.parse_args()
 
 
@@ -267,8 +270,15 @@ def main():
             return {k: sum(r[k] for r in res) for k in ("ok", "completed", "dropped", "errors", "issued")}
 
         drive(args.warmup * per_step, False, 600.0)
+    stamps = None
+    if args.stamps_out:
+        from ray_dynamic_batching_amd import ops as _ops_mod
+
+        stamps = _ops_mod.BlockStamps()
     barrier()
     sync()
+    if stamps is not None:
+        stamps.reset()
     if rank == 0:
         job.reset_stats()
         rep0 = [job.replica_stats(r) for r in range(n)]
@@ -279,6 +289,13 @@ def main():
     barrier()
     sync()
     elapsed = time.perf_counter() - t0
+    if stamps is not None:
+        import numpy as np
+
+        path = args.stamps_out if world == 1 else args.stamps_out.replace(".npy", f".rank{rank}.npy")
+        np.save(path, stamps.read())
+        print(json.dumps({"rank": rank, "stamps": path, "dropped": stamps.dropped}), file=sys.stderr, flush=True)
+        stamps.close()
     barrier()
     err = runner.error()
     if world > 1:
@@ -352,6 +369,9 @@ def main():
             line["vs_baseline"] = None
         if args.rehearse_one_gpu:
             line["metric"] = "REHEARSAL (all ranks on one GPU, gloo): " + METRIC
+            line["vs_baseline"] = None
+        if args.stamps_out:
+            line["metric"] = "DIAGNOSTIC (block-stamp kernel build; barriers added per block): " + METRIC
             line["vs_baseline"] = None
         if err:
             line["engine_error"] = err

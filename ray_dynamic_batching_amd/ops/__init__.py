@@ -164,6 +164,11 @@ def _cu_share(c: int, M: int, N: int, cus: int = 256) -> float:
     """Share of the GPU's CUs a GEMM launch with tile choice ``c`` holds (split-K
     multiplies the blocks, DEEP holds a whole CU per block)."""
     t = c & 255
+    if c >= 0 and c & CONV_PP:
+        if not 0 <= t < len(_CONV_PP_BM):
+            return 1.0
+        blocks = -(-M // _CONV_PP_BM[t]) * -(-N // _CONV_PP_BN[t]) * max(1, (c >> 8) & 15)
+        return min(1.0, blocks / (cus * (2 if _CONV_PP_BK[t] == 32 else 1)))   # BK 32 tiles: 2 blocks / CU
     if not 0 <= t < len(_ALL_BM):
         return 1.0
     blocks = -(-M // _ALL_BM[t]) * -(-N // _ALL_BN[t]) * max(1, (c >> 8) & 15)
@@ -1160,6 +1165,14 @@ _GEMM_DEEP = os.environ.get("RDB_GEMM_DEEP", "1") != "0"
 #   CONV_LINEAR | cfg    (1x1 / stride 1) the dense GEMM `linear` on tile cfg (0..25)
 #   ... | DEEP           tiles 0, 1, 2, 3, 9, 10 with one block per CU and up to 8 LDS stages
 CONV_LINEAR = 1 << 16
+#   CONV_PP | v [| splits << 8]   (R x S / strided convs, C % BK == 0, with bias) the
+#                        8-wave ping-pong kernel with the im2col operand, tile v (conv.hip)
+CONV_PP = 1 << 17
+_CONV_PP_BM = (256, 128, 256, 256, 128)          # conv.hip kConvPPBM / BN / BK
+_CONV_PP_BN = (128, 256, 128, 64, 128)
+_CONV_PP_BK = (64, 64, 32, 64, 32)
+# RDB_CONV_PP=0: no ping-pong conv candidates
+_CONV_PP = os.environ.get("RDB_CONV_PP", "1") != "0"
 DEEP = 1 << 12                        # gemm_core.h kDeepFlag: one block per CU, up to 8 LDS stages
 _DEEP_TILES = (0, 1, 2, 3, 9, 10, 6, 7)
 _DEEP_BIG = (6, 7)                    # 256x128 / 128x256: one block per CU at any grid size
@@ -1176,8 +1189,9 @@ _priv_ws: Dict[tuple, torch.Tensor] = {}
 def splits_of(c: int) -> int:
     """Split-K factor of an encoded tile choice (0 / 1: not split).  The factor is
     the 4-bit field at bit 8 (gemm_core.h decodes ``(cfg >> 8) & 15``): the DEEP
-    flag (bit 12) and CONV_LINEAR (bit 16) are not part of it."""
-    return 0 if c < 0 or c >= CONV_LINEAR else (c >> 8) & 15
+    flag (bit 12), CONV_LINEAR (bit 16) and CONV_PP (bit 17) are not part of it;
+    a CONV_LINEAR choice is never split."""
+    return 0 if c < 0 or (c & CONV_LINEAR) else (c >> 8) & 15
 
 
 def _private_splitk_ws(device, need: int) -> torch.Tensor:
@@ -1205,10 +1219,37 @@ def splitk_workspace(device, nbytes: int = SPLITK_WS_BYTES, zeroed: bool = True)
     return ws
 
 
-def _conv_candidates(M: int, K_out: int, Kg: int, one_by_one: bool):
+def _conv_pp_candidates(M: int, K_out: int, Kg: int, C: int):
+    """Ping-pong conv tiles (CONV_PP) for an im2col conv: every tile whose BK
+    divides C, split-K where the grid is under ~one block per CU."""
+    out = []
+    if K_out % 8:
+        return out
+    for v in range(len(_CONV_PP_BM)):
+        bm, bn, bk = _CONV_PP_BM[v], _CONV_PP_BN[v], _CONV_PP_BK[v]
+        if C % bk:
+            continue
+        tiles = -(-M // bm) * -(-K_out // bn)
+        out.append(CONV_PP | v)
+        if not _CONV_SPLITK or tiles >= 256:
+            continue
+        nk = Kg // bk
+        for sp in _SPLITS + (12,):
+            kper = -(-nk // sp)
+            eff = -(-nk // kper)
+            if eff < 2 or kper < 3 or tiles * eff > 1024:
+                continue
+            if SPLITK_HEADER + tiles * eff * bm * bn * 4 > SPLITK_WS_BYTES:
+                continue
+            out.append(CONV_PP | v | (sp << 8))
+    return out
+
+
+def _conv_candidates(M: int, K_out: int, Kg: int, one_by_one: bool, C: int = 0, has_bias: bool = False):
     """Tile choices for a conv of output [M, K_out] over a Kg-long reduction:
     every 4-wave tile; split-K where the tile grid leaves CUs idle (< 2 blocks
-    per CU) and each split keeps >= 4 K-steps; the dense GEMM tiles for 1x1."""
+    per CU) and each split keeps >= 4 K-steps; the dense GEMM tiles for 1x1;
+    the ping-pong conv tiles for the im2col convs (with a bias)."""
     cands = list(range(NUM_CONV_TILE_CFGS))
     nk = -(-Kg // 64)
 
@@ -1234,6 +1275,8 @@ def _conv_candidates(M: int, K_out: int, Kg: int, one_by_one: bool):
                     cands.append(c | (sp << 8) | DEEP)
     if one_by_one and _CONV1X1_GEMM and K_out % 8 == 0:
         cands += [CONV_LINEAR | c for c in _gemm_candidates(M, K_out, Kg)]
+    if not one_by_one and has_bias and _CONV_PP:
+        cands += _conv_pp_candidates(M, K_out, Kg, C)
     return cands
 
 
@@ -1278,7 +1321,7 @@ def conv2d_nhwc(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] =
             return
         sp = splits_of(c)
         if sp > 1 and ws is None:
-            ws = _private_splitk_ws(x.device, int(_ops().conv_splitk_bytes(M, K, c & 255, sp)))
+            ws = _private_splitk_ws(x.device, int(_ops().conv_splitk_bytes(M, K, c & ~0xF00, sp)))
         fn(*args, _stream(), int(c), _ptr(ws), 0 if ws is None else ws.numel())
 
     if tile_cfg < 0:
@@ -1294,7 +1337,7 @@ def conv2d_nhwc(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] =
                 if ws is None:
                     ws = _tune_ws[sid] = splitk_workspace(x.device)
             launch(c, ws)
-        tile_cfg = _tuned_cfg(key, tune_launch, _conv_candidates(M, K, Kg, one_by_one))
+        tile_cfg = _tuned_cfg(key, tune_launch, _conv_candidates(M, K, Kg, one_by_one, C, bias is not None))
     launch(int(tile_cfg), workspace)
     return out
 
@@ -1407,3 +1450,49 @@ def se_scale(x: torch.Tensor, s: torch.Tensor, out: Optional[torch.Tensor] = Non
 
 def se_scale_ref(x, s):
     return (x.float() * s.float()[:, None, None, :]).to(torch.float16)
+
+
+# ---------------------------------------------------------------------------
+# Per-block stamps of the diagnostic kernel build (ops/csrc/common.h
+# RDB_STAMP_*; ``python -m ray_dynamic_batching_amd._build --variant stamps
+# -D RDB_BLOCK_STAMPS``, loaded with RDB_OPS_SO).  bench/stamp_timeline.py turns
+# the records into co-residency / CU-time of the UN-profiled serving bench.
+# ---------------------------------------------------------------------------
+def stamps_built() -> bool:
+    """Whether the loaded kernel library is the RDB_BLOCK_STAMPS diagnostic build."""
+    f = getattr(_ops(), "stamps_built", None)
+    return bool(f and f())
+
+
+class BlockStamps:
+    """Device buffer the instrumented kernels write one record per block to:
+    [t_begin, t_end, meta, where] u64 (common.h).  ``cap`` records at most; the
+    counter keeps counting past it (``dropped``)."""
+
+    def __init__(self, cap: int = 1 << 22, device="cuda"):
+        _check(stamps_built(), "BlockStamps needs the RDB_BLOCK_STAMPS kernel build (RDB_OPS_SO=<variant .so>)")
+        self.cap = int(cap)
+        self.buf = torch.zeros(self.cap * 4, dtype=torch.int64, device=device)
+        self.count = torch.zeros(1, dtype=torch.int32, device=device)
+        _ops().stamps_set(self.buf.data_ptr(), self.count.data_ptr(), self.cap)
+
+    def reset(self) -> None:
+        torch.cuda.synchronize()
+        self.count.zero_()
+        torch.cuda.synchronize()
+
+    def read(self):
+        """The records written since the last reset, as an [n, 4] uint64 array."""
+        import numpy as np
+
+        torch.cuda.synchronize()
+        n = min(int(self.count.item()), self.cap)
+        return self.buf[: n * 4].view(n, 4).cpu().numpy().view(np.uint64)
+
+    @property
+    def dropped(self) -> int:
+        return max(0, int(self.count.item()) - self.cap)
+
+    def close(self) -> None:
+        torch.cuda.synchronize()
+        _ops().stamps_set(0, 0, 0)

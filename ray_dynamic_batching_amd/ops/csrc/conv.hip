@@ -11,8 +11,73 @@
 
 namespace rdb {
 
+// ---- ping-pong implicit-GEMM convolutions (force_cfg = kConvPPFlag | v | splits << 8) ----
+// The 8-wave two-group ping-pong kernel (gemm_pp.h) with the im2col A operand:
+// the per-wave tiles (64 x 64 / 64 x 32) read half the LDS bytes per MFMA of the
+// 4-wave 64 x 128 / 128 x 64 im2col tiles, and split-K keeps the small-M layers
+// (ResNet stages 3 / 4: M = 6272 / 1568 at batch 32) on >= ~200 blocks.
+constexpr int kConvPPFlag = 1 << 17;
+constexpr int kNumConvPP = 5;
+//                                  0    1    2    3    4
+constexpr int kConvPPBM[kNumConvPP] = {256, 128, 256, 256, 128};
+constexpr int kConvPPBN[kNumConvPP] = {128, 256, 128, 64, 128};
+constexpr int kConvPPBK[kNumConvPP] = {64, 64, 32, 64, 32};
+
+static size_t conv_pp_splitk_bytes(int M, int N, int v, int splits) {
+  const size_t tiles = (size_t)((M + kConvPPBM[v] - 1) / kConvPPBM[v]) * ((N + kConvPPBN[v] - 1) / kConvPPBN[v]);
+  return kSplitKHeader + tiles * splits * kConvPPBM[v] * kConvPPBN[v] * sizeof(float);
+}
+
+template <int BM, int BN, int GM, int GN, int STAGES, int BK, int OCC>
+static void launch_conv_pp(const ConvParams& p, const f16* w, f16* y, const f16* bias, const f16* res, int N, int act,
+                           hipStream_t s, int splits, void* ws, size_t ws_bytes) {
+  const int M = p.M, K = p.K;
+  if (p.C % BK != 0) throw std::invalid_argument("conv2d_nhwc: ping-pong conv tiles need C % BK == 0");
+  if (bias == nullptr || act == ACT_SWIGLU || !gemm_pp_ok(N, N, N, y, bias, res, act))
+    throw std::invalid_argument("conv2d_nhwc: ping-pong conv tiles need a bias, N % 8 == 0, 16-B aligned y / residual");
+  const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  LnEpi ln{};
+  int eff = 1;
+  if (splits > 1 && ws != nullptr) {
+    const int nk = K / BK;
+    const int kper = (nk + splits - 1) / splits;
+    eff = (nk + kper - 1) / kper;
+    const size_t need = kSplitKHeader + (size_t)tiles * eff * BM * BN * sizeof(float);
+    if (eff >= 2 && tiles <= kSplitKMaxTiles && need <= ws_bytes && need - kSplitKHeader <= (size_t(1) << 31)) {
+      ln.sk_cnt = static_cast<int*>(ws);
+      ln.sk_part = reinterpret_cast<float*>(static_cast<char*>(ws) + kSplitKHeader);
+      ln.sk_kper = kper;
+    } else {
+      eff = 1;
+    }
+  }
+  const ConvGeom cv{p.H, p.W, p.C, p.S, p.stride, p.pad, p.P, p.Q, (uint32_t)((size_t)p.N * p.H * p.W * p.C * sizeof(f16))};
+  const f16* x = static_cast<const f16*>(p.x);
+  const dim3 grid(tiles, eff), block(512);
+  if (res)
+    hipLaunchKernelGGL((gemm_pp_kernel<f16, f16, 8, BM, BN, GM, GN, STAGES, true, true, BK, OCC, 0, true>), grid, block, 0,
+                       s, x, 0, w, K, y, N, bias, res, N, M, N, K, 1.f, act, ln, cv);
+  else
+    hipLaunchKernelGGL((gemm_pp_kernel<f16, f16, 8, BM, BN, GM, GN, STAGES, true, false, BK, OCC, 0, true>), grid, block, 0,
+                       s, x, 0, w, K, y, N, bias, res, N, M, N, K, 1.f, act, ln, cv);
+}
+
+static void conv_pp(int v, const ConvParams& p, const f16* w, f16* y, const f16* bias, const f16* res, int N, int act,
+                    hipStream_t s, int splits, void* ws, size_t ws_bytes) {
+  switch (v) {
+    case 0: launch_conv_pp<256, 128, 2, 2, 3, 64, 2>(p, w, y, bias, res, N, act, s, splits, ws, ws_bytes); return;
+    case 1: launch_conv_pp<128, 256, 1, 4, 3, 64, 2>(p, w, y, bias, res, N, act, s, splits, ws, ws_bytes); return;
+    case 2: launch_conv_pp<256, 128, 2, 2, 3, 32, 4>(p, w, y, bias, res, N, act, s, splits, ws, ws_bytes); return;
+    case 3: launch_conv_pp<256, 64, 2, 2, 3, 64, 2>(p, w, y, bias, res, N, act, s, splits, ws, ws_bytes); return;
+    case 4: launch_conv_pp<128, 128, 1, 4, 4, 32, 4>(p, w, y, bias, res, N, act, s, splits, ws, ws_bytes); return;
+    default: throw std::invalid_argument("conv2d_nhwc: unknown ping-pong conv tile");
+  }
+}
+
 // force_cfg = tile | (splits << 8) [| kDeepFlag]: splits > 1 runs split-K on the workspace
 // `ws` (ws_bytes; zeroed counter header, see splitk_bytes) when it fits, else unsplit.
+// force_cfg = kConvPPFlag | v | (splits << 8): ping-pong conv tile v (R x S convs
+// and strided 1 x 1 -- the im2col operand; C % BK == 0, bias required).
 void conv2d_nhwc(uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t res, uintptr_t y, int N, int H,
                  int W, int C, int K, int R, int S, int stride, int pad, int P, int Q, int act,
                  uintptr_t stream, int force_cfg, uintptr_t ws, size_t ws_bytes) {
@@ -22,6 +87,13 @@ void conv2d_nhwc(uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t res, uintpt
     throw std::invalid_argument("conv2d_nhwc: P / Q larger than the padded output");
   const int M = N * P * Q, Kg = R * S * C;
   if (M <= 0 || K <= 0) return;
+  if (force_cfg >= 0 && (force_cfg & kConvPPFlag)) {
+    ConvParams p{reinterpret_cast<const void*>(x), N, H, W, C, R, S, stride, pad, P, Q, M, Kg};
+    conv_pp(force_cfg & 255, p, (const f16*)w, (f16*)y, (const f16*)bias, (const f16*)res, K, act,
+            reinterpret_cast<hipStream_t>(stream), (force_cfg >> 8) & 15, reinterpret_cast<void*>(ws), ws_bytes);
+    RDB_HIP_CHECK(hipGetLastError());
+    return;
+  }
   const int tile = force_cfg < 0 ? -1 : (force_cfg & 255);
   const int splits = force_cfg < 0 ? 1 : ((force_cfg >> 8) & 15);
   const int cfg = force_cfg < 0 ? -1 : (tile | (force_cfg & kDeepFlag));
@@ -40,7 +112,10 @@ void conv2d_nhwc(uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t res, uintpt
   RDB_HIP_CHECK(hipGetLastError());
 }
 
-size_t conv_splitk_bytes(int M, int N, int cfg, int splits) { return splitk_bytes(M, N, cfg, splits); }
+size_t conv_splitk_bytes(int M, int N, int cfg, int splits) {
+  if (cfg & kConvPPFlag) return conv_pp_splitk_bytes(M, N, cfg & 255, splits);
+  return splitk_bytes(M, N, cfg & 255, splits);
+}
 
 // Depthwise RxR conv, NHWC f16, weights [R][R][C] (channel-contiguous), bias [C].
 // One thread = 8 channels of one output pixel.

@@ -79,17 +79,31 @@ struct PPGeom {
   static __device__ __forceinline__ int off(int row, int chunk) { return row * ROWB + ((chunk ^ swz(row)) << 4); }
 };
 
+// Implicit-GEMM convolution operand (CONV instantiations): A is the im2col view
+// of an NHWC f16 image, A[m, k] = x[n, p*stride - pad + r, q*stride - pad + s, c]
+// with m = (n, p, q), k = (r, s, c).  C % BK == 0, so every K-tile lies inside one
+// filter tap: the tap (r, s) and channel offset are block-uniform per K-tile, and
+// each lane's 16-B DMA piece is one contiguous channel chunk of one input pixel
+// (padding -> kOOB -> zero fill).  The 9 taps of a 3x3 conv re-read the image
+// through L2 (the patch is L2-resident), never through an im2col buffer.
+struct ConvGeom {
+  int H, W, C, S, stride, pad, P, Q;
+  uint32_t img_bytes;   // N * H * W * C * 2: the A buffer resource's extent
+};
+
 // OCC = waves per SIMD the register budget must allow: 2 = one 8-wave block
 // per CU (<= 256 VGPRs), 4 = two co-resident blocks (<= 128 VGPRs; the tile's
 // LDS must then fit twice in 160 KiB)
 // EPI: 0, EPI_SWG (SwiGLU) or an EPI_STG LayerNorm mode (gemm_core.h): LN operands
 // are staged in LDS after the bias by the prologue and applied by the staged epilogue.
+// CONV: A is the im2col view described by `cv` (lda unused) and the launch may
+// split K over gridDim.y (ln.sk_* : the gemm_core.h split-K hand-off).
 template <typename T, typename OutT, int NW, int BM, int BN, int GM, int GN, int STAGES, bool HAS_BIAS, bool HAS_RES,
-          int BK_ = 64, int OCC = 2, int EPI = 0>
+          int BK_ = 64, int OCC = 2, int EPI = 0, bool CONV = false>
 __global__ void __launch_bounds__(64 * NW, OCC)
 gemm_pp_kernel(const T* __restrict__ A, int lda, const T* __restrict__ W, int ldw, OutT* __restrict__ C, int ldc,
                const T* __restrict__ bias, const T* __restrict__ R, int ldr, int M, int N, int K, float alpha,
-               int act, LnEpi ln) {
+               int act, LnEpi ln, ConvGeom cv) {
   typedef PPGeom<NW, BM, BN, BK_> G;
   constexpr int BK = G::BK;
   constexpr int KS = BK / 32;                // MFMA k-steps per tile
@@ -124,16 +138,32 @@ gemm_pp_kernel(const T* __restrict__ A, int lda, const T* __restrict__ W, int ld
   const int m0 = tile_m * BM, n0 = tile_n * BN;
 
   // ---- DMA addressing (wave wid_u owns A pieces [wid*A_PW, ...) and W pieces [wid*W_PW, ...)) ----
-  const __amdgpu_buffer_rsrc_t asrc = make_rsrc(A, (uint32_t)((size_t)(M - 1) * lda * sizeof(T) + (size_t)K * sizeof(T)));
+  const __amdgpu_buffer_rsrc_t asrc =
+      CONV ? make_rsrc(A, cv.img_bytes)
+           : make_rsrc(A, (uint32_t)((size_t)(M - 1) * lda * sizeof(T) + (size_t)K * sizeof(T)));
   const __amdgpu_buffer_rsrc_t wsrc = make_rsrc(W, (uint32_t)((size_t)(N - 1) * ldw * sizeof(T) + (size_t)K * sizeof(T)));
   uint32_t aoff[G::A_PW], woff[G::W_PW];
   int ach[G::A_PW], wch[G::W_PW];
+  // CONV: per piece the output pixel's top-left input corner (ah, aw) and its
+  // element offset (corner pixel + this lane's channel chunk; may be negative
+  // at the padding, never dereferenced there)
+  constexpr int CA = CONV ? G::A_PW : 1;
+  int ah[CA], aw[CA];
 #pragma unroll
   for (int i = 0; i < G::A_PW; ++i) {
     const int row = (wid * G::A_PW + i) * G::PR + lane / G::CPR;
     ach[i] = (lane % G::CPR) ^ G::swz(row);
     const int gm = m0 + row;
-    aoff[i] = gm < M ? (uint32_t)((size_t)gm * lda * sizeof(T)) : kOOB;
+    if constexpr (CONV) {
+      const int pq = cv.P * cv.Q;
+      const int n = gm / pq, rem = gm - n * pq;
+      const int pp = rem / cv.Q, qq = rem - pp * cv.Q;
+      ah[i] = gm < M ? pp * cv.stride - cv.pad : -(1 << 20);
+      aw[i] = qq * cv.stride - cv.pad;
+      aoff[i] = (uint32_t)(((n * cv.H + ah[i]) * cv.W + aw[i]) * cv.C + ach[i] * 8);
+    } else {
+      aoff[i] = gm < M ? (uint32_t)((size_t)gm * lda * sizeof(T)) : kOOB;
+    }
   }
 #pragma unroll
   for (int i = 0; i < G::W_PW; ++i) {
@@ -148,10 +178,25 @@ gemm_pp_kernel(const T* __restrict__ A, int lda, const T* __restrict__ W, int ld
   };
   auto stage = [&](int buf, int k0) {
     char* base = smem + buf * G::STAGE_BYTES;
+    if constexpr (CONV) {
+      // block-uniform tap of this K-tile
+      const int tap = k0 / cv.C, c0 = k0 - tap * cv.C;
+      const int ur = tap / cv.S, us = tap - ur * cv.S;
+      const int uoff = (ur * cv.W + us) * cv.C + c0;
 #pragma unroll
-    for (int i = 0; i < G::A_PW; ++i) {
-      const int gk = k0 + ach[i] * 8;
-      dma16(asrc, base + (wid_u * G::A_PW + i) * 1024, (gk < K && aoff[i] != kOOB) ? aoff[i] + (uint32_t)(gk * sizeof(T)) : kOOB);
+      for (int i = 0; i < G::A_PW; ++i) {
+        const int h = ah[i] + ur, w = aw[i] + us;
+        const bool ok = k0 < K && (unsigned)h < (unsigned)cv.H && (unsigned)w < (unsigned)cv.W;
+        dma16(asrc, base + (wid_u * G::A_PW + i) * 1024,
+              ok ? (uint32_t)(((int)aoff[i] + uoff) * (int)sizeof(T)) : kOOB);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < G::A_PW; ++i) {
+        const int gk = k0 + ach[i] * 8;
+        dma16(asrc, base + (wid_u * G::A_PW + i) * 1024,
+              (gk < K && aoff[i] != kOOB) ? aoff[i] + (uint32_t)(gk * sizeof(T)) : kOOB);
+      }
     }
 #pragma unroll
     for (int i = 0; i < G::W_PW; ++i) {
@@ -204,7 +249,14 @@ gemm_pp_kernel(const T* __restrict__ A, int lda, const T* __restrict__ W, int ld
   constexpr int kVm0 = 0x70 | 0xF00;
   constexpr int kLgkm0 = 0xC07F;            // lgkmcnt(0), vmcnt and expcnt at max
 
-  const int nk = (K + BK - 1) / BK;
+  // split-K (CONV launches with gridDim.y > 1): this block runs K-tiles [kb, kb + nk)
+  int kb = 0, nk = (K + BK - 1) / BK;
+  if constexpr (CONV) {
+    if (gridDim.y > 1) {
+      kb = blockIdx.y * ln.sk_kper;
+      nk = min(ln.sk_kper, nk - kb);
+    }
+  }
 #ifdef RDB_PP_STAMPS
   // diagnostic build only (bench/gemm_lab): per-block cycle stamps
   unsigned long long* stp = rdb_pp_stamps + (size_t)blockIdx.x * 8;
@@ -225,7 +277,7 @@ gemm_pp_kernel(const T* __restrict__ A, int lda, const T* __restrict__ W, int ld
   // prologue: tiles 0 .. STAGES-2 in flight, tile 0 retired and visible
 #pragma unroll
   for (int s = 0; s < STAGES - 1; ++s)
-    if (s < nk) stage(s, s * BK);
+    if (s < nk) stage(s, (kb + s) * BK);
   if (nk >= STAGES - 1) __builtin_amdgcn_s_waitcnt(kVmSteady);
   else __builtin_amdgcn_s_waitcnt(kVm0);
   barrier();
@@ -239,7 +291,7 @@ gemm_pp_kernel(const T* __restrict__ A, int lda, const T* __restrict__ W, int ld
     // ---- read interval: fragments of tile kt, DMA of tile kt+STAGES-1 ----
     read_tile(buf);
     const bool steady = kt + STAGES - 1 < nk;
-    if (steady) stage((kt + STAGES - 1) % STAGES, (kt + STAGES - 1) * BK);
+    if (steady) stage((kt + STAGES - 1) % STAGES, (kb + kt + STAGES - 1) * BK);
     __builtin_amdgcn_s_waitcnt(kLgkm0);           // my reads of this buffer are done (WAR)
     if (steady) __builtin_amdgcn_s_waitcnt(kVmSteady);  // my pieces of tile kt+1 landed (RAW)
     else __builtin_amdgcn_s_waitcnt(kVm0);
@@ -255,6 +307,50 @@ gemm_pp_kernel(const T* __restrict__ A, int lda, const T* __restrict__ W, int ld
 #ifdef RDB_PP_STAMPS
   const unsigned long long t_loop = __builtin_amdgcn_s_memtime();
 #endif
+  if constexpr (CONV) {
+    if (gridDim.y > 1) {
+      // ---- split-K hand-off (mfma_gemm_kernel's protocol): a non-last split
+      // stores its f32 partial (sc1), drains, meets at a barrier and one lane
+      // bumps the tile's counter; the last arriver resets the counter, folds the
+      // other partials in and runs the epilogue.  Nobody waits on anybody.
+      __shared__ int sk_flag;
+      const int splits = gridDim.y, z = blockIdx.y;
+      int* cnt = ln.sk_cnt + t;
+      const int nwg = tiles_m * tiles_n;
+      const __amdgpu_buffer_rsrc_t psrc =
+          make_rsrc(ln.sk_part, (uint32_t)((size_t)nwg * splits * BM * BN * sizeof(float)));
+      auto slot_off = [&](int zz, int i, int j) {
+        return (uint32_t)(((((size_t)t * splits + zz) * (TN * TM) + i * TM + j) * G::NT + tid) * 16);
+      };
+      if (tid == 0) sk_flag = __hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == splits - 1;
+      __syncthreads();
+      bool last = sk_flag != 0;
+      __syncthreads();
+      if (!last) {
+#pragma unroll
+        for (int i = 0; i < TN; ++i)
+#pragma unroll
+          for (int j = 0; j < TM; ++j)
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i][j]), psrc, slot_off(z, i, j), 0, 16);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0)
+          sk_flag = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == splits - 1;
+        __syncthreads();
+        last = sk_flag != 0;
+      }
+      if (!last) return;
+      if (tid == 0) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      for (int zz = 0; zz < splits; ++zz) {
+        if (zz == z) continue;
+#pragma unroll
+        for (int i = 0; i < TN; ++i)
+#pragma unroll
+          for (int j = 0; j < TM; ++j)
+            acc[i][j] += __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(psrc, slot_off(zz, i, j), 0, 16));
+      }
+    }
+  }
 
   // ---- epilogue: LDS-staged, row-coalesced (launch_gemm_pp's caller guarantees
   // its requirements: 16-bit output, N % 8 == 0 (SwiGLU: N % 16, no residual), 16-B alignment) ----
@@ -305,24 +401,24 @@ void launch_gemm_pp(const T* A, int lda, const T* W, int ldw, OutT* C, int ldc, 
   if (act == ACT_SWIGLU) {   // gemm_pp_ok: R == nullptr
     if (bias)
       hipLaunchKernelGGL((gemm_pp_kernel<T, OutT, NW, BM, BN, GM, GN, STAGES, true, false, BK, OCC, EPI_SWG>), grid, block,
-                         0, s, A, lda, W, ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act, ln);
+                         0, s, A, lda, W, ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act, ln, ConvGeom{});
     else
       hipLaunchKernelGGL((gemm_pp_kernel<T, OutT, NW, BM, BN, GM, GN, STAGES, false, false, BK, OCC, EPI_SWG>), grid, block,
-                         0, s, A, lda, W, ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act, ln);
+                         0, s, A, lda, W, ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act, ln, ConvGeom{});
     return;
   }
   if (bias && R)
     hipLaunchKernelGGL((gemm_pp_kernel<T, OutT, NW, BM, BN, GM, GN, STAGES, true, true, BK, OCC>), grid, block, 0, s, A, lda, W,
-                       ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act, ln);
+                       ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act, ln, ConvGeom{});
   else if (bias)
     hipLaunchKernelGGL((gemm_pp_kernel<T, OutT, NW, BM, BN, GM, GN, STAGES, true, false, BK, OCC>), grid, block, 0, s, A, lda, W,
-                       ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act, ln);
+                       ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act, ln, ConvGeom{});
   else if (R)
     hipLaunchKernelGGL((gemm_pp_kernel<T, OutT, NW, BM, BN, GM, GN, STAGES, false, true, BK, OCC>), grid, block, 0, s, A, lda, W,
-                       ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act, ln);
+                       ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act, ln, ConvGeom{});
   else
     hipLaunchKernelGGL((gemm_pp_kernel<T, OutT, NW, BM, BN, GM, GN, STAGES, false, false, BK, OCC>), grid, block, 0, s, A, lda,
-                       W, ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act, ln);
+                       W, ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act, ln, ConvGeom{});
 }
 
 // The staged-LayerNorm modes (EPI_STG | ...) on a ping-pong tile.  LNA: no bias
@@ -333,7 +429,7 @@ void launch_gemm_pp_ln(const T* A, int lda, const T* W, int ldw, OutT* C, int ld
   const int nwg = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
   constexpr bool RES = (EPI & (EPI_LNR | EPI_STATS)) != 0;
   hipLaunchKernelGGL((gemm_pp_kernel<T, OutT, NW, BM, BN, GM, GN, STAGES, RES, RES, BK, OCC, EPI>), dim3(nwg),
-                     dim3(64 * NW), 0, s, A, lda, W, ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act, ln);
+                     dim3(64 * NW), 0, s, A, lda, W, ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act, ln, ConvGeom{});
 }
 
 }  // namespace rdb

@@ -279,6 +279,73 @@ def test_conv2d_splitk(N, H, C, K, R, stride, pad):
             _close(ops.conv2d_nhwc(x, w, b, act="relu", residual=r, tile_cfg=ops.CONV_LINEAR | c), ref_r, 2e-2, 2e-2)
 
 
+@pytest.mark.parametrize("N,H,C,K,R,stride,pad", [
+    (2, 56, 64, 64, 3, 1, 1), (32, 7, 512, 512, 3, 1, 1), (4, 28, 128, 128, 3, 2, 1), (3, 14, 256, 256, 3, 2, 1),
+    (2, 56, 256, 128, 1, 2, 0), (2, 15, 96, 40, 3, 1, 1)])
+def test_conv2d_pingpong(N, H, C, K, R, stride, pad):
+    """The 8-wave ping-pong kernel with the im2col operand (CONV_PP | v [| splits
+    << 8]): every tile whose BK divides C, with and without residual, unsplit and
+    split-K on one shared workspace (counters back to zero), ragged M / N edges."""
+    ops = _ops()
+    torch.manual_seed(13 + H)
+    x = torch.randn(N, H, H, C, device="cuda", dtype=torch.float16)
+    w = torch.randn(K, R, R, C, device="cuda", dtype=torch.float16) * (R * R * C) ** -0.5
+    b = torch.randn(K, device="cuda", dtype=torch.float16) * 0.1
+    ref = ops.conv2d_nhwc_ref(x, w, b, stride=stride, pad=pad, act="relu")
+    r = torch.randn_like(ref)
+    ref_r = ops.conv2d_nhwc_ref(x, w, b, stride=stride, pad=pad, act="relu", residual=r)
+    ws = ops.splitk_workspace("cuda")
+    ran = 0
+    for v in range(len(ops._CONV_PP_BM)):
+        if C % ops._CONV_PP_BK[v]:
+            continue
+        nk = R * R * C // ops._CONV_PP_BK[v]
+        for sp in (0, 2, 5):
+            if sp and -(-nk // -(-nk // sp)) < 2:
+                continue
+            c = ops.CONV_PP | v | (sp << 8)
+            _close(ops.conv2d_nhwc(x, w, b, stride=stride, pad=pad, act="relu", tile_cfg=c, workspace=ws), ref, 2e-2, 2e-2)
+            _close(ops.conv2d_nhwc(x, w, b, stride=stride, pad=pad, act="relu", residual=r, tile_cfg=c, workspace=ws),
+                   ref_r, 2e-2, 2e-2)
+            ran += 1
+    assert ran >= 2
+    torch.cuda.synchronize()
+    assert int(ws[:ops.SPLITK_HEADER].view(torch.int32).abs().sum()) == 0
+
+
+def test_conv2d_pingpong_splitk_graph_replay():
+    """A split-K ping-pong conv chain captured in a graph (per-forward workspace,
+    as ResNet50._logits_hip), replayed with new inputs."""
+    ops = _ops()
+    torch.manual_seed(14)
+    x = torch.randn(32, 14, 14, 256, device="cuda", dtype=torch.float16)
+    w = torch.randn(256, 3, 3, 256, device="cuda", dtype=torch.float16) * (9 * 256) ** -0.5
+    b = torch.randn(256, device="cuda", dtype=torch.float16) * 0.1
+
+    def fwd():
+        ws = ops.splitk_workspace("cuda")
+        h = ops.conv2d_nhwc(x, w, b, pad=1, act="relu", tile_cfg=ops.CONV_PP | 0 | (4 << 8), workspace=ws)
+        return ops.conv2d_nhwc(h, w, b, pad=1, act="relu", tile_cfg=ops.CONV_PP | 2 | (6 << 8), workspace=ws)
+
+    def ref():
+        h = ops.conv2d_nhwc_ref(x, w, b, pad=1, act="relu")
+        return ops.conv2d_nhwc_ref(h, w, b, pad=1, act="relu")
+
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        fwd()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            y = fwd()
+    torch.cuda.synchronize()
+    for _ in range(2):
+        x.copy_(torch.randn_like(x))
+        g.replay()
+        torch.cuda.synchronize()
+        _close(y, ref(), 3e-2, 3e-2)
+
+
 @pytest.mark.parametrize("M,N,K", [(4096, 768, 768), (512, 768, 3072), (1000, 520, 1160)])
 def test_linear_deep_tiles(M, N, K):
     """The DEEP 4-wave tiles (kStages up to 8, one block per CU; K tails and

@@ -6,7 +6,7 @@ from ray_dynamic_batching_amd import ops
 
 
 def _decode(c):
-    return c & 255, (c >> 8) & 15, bool(c & ops.DEEP), c >= ops.CONV_LINEAR
+    return c & 255, (c >> 8) & 15, bool(c & ops.DEEP), bool(c & ops.CONV_LINEAR)
 
 
 def test_conv_candidates_encode_valid_choices():
@@ -79,3 +79,37 @@ def test_key_output_shape_for_cu_time():
     assert ops._key_mn(("qkv_attn", "torch.bfloat16", 32, 128, 12, 768, 768, False)) is None
     # a 1x1 conv on the dense ping-pong tile: its share follows the GEMM grid
     assert ops._cu_share(ops.CONV_LINEAR | 19, 1568, 2048) == ops._cu_share(19, 1568, 2048)
+
+
+def test_conv_pp_candidates():
+    """Ping-pong conv tiles (CONV_PP | v | splits << 8) for the im2col convs of
+    ResNet-50 at bs32: only where BK divides C and a bias is fused, split-K only
+    under ~one block per CU, every split non-empty, partials within the workspace."""
+    assert ops.splits_of(ops.CONV_PP | 2 | (4 << 8)) == 4
+    assert ops.splits_of(ops.CONV_PP | 3) == 0
+    assert ops.splits_of(ops.CONV_LINEAR | 19) == 0
+    for M, N, Kg, C in ((100352, 64, 576, 64), (25088, 128, 1152, 128), (6272, 256, 2304, 256), (1568, 512, 4608, 512)):
+        cands = ops._conv_candidates(M, N, Kg, False, C, True)
+        pp = [c for c in cands if c & ops.CONV_PP]
+        assert pp and len(cands) == len(set(cands))
+        assert not [c for c in ops._conv_candidates(M, N, Kg, False, C, False) if c & ops.CONV_PP]   # no bias: none
+        for c in pp:
+            v, sp = c & 255, ops.splits_of(c)
+            assert not c & ops.CONV_LINEAR and not c & ops.DEEP
+            bm, bn, bk = ops._CONV_PP_BM[v], ops._CONV_PP_BN[v], ops._CONV_PP_BK[v]
+            assert C % bk == 0
+            tiles = -(-M // bm) * -(-N // bn)
+            if sp:
+                assert tiles < 256
+                nk = Kg // bk
+                kper = -(-nk // sp)
+                eff = -(-nk // kper)
+                assert eff >= 2 and kper >= 3
+                assert ops.SPLITK_HEADER + tiles * eff * bm * bn * 4 <= ops.SPLITK_WS_BYTES
+            share = ops._cu_share(c, M, N)
+            assert 0 < share <= 1.0
+        if M == 1568:
+            assert any(ops.splits_of(c) for c in pp)                   # stage 4: split-K choices
+    # C = 96 (no BK divides it... 96 % 32 == 0): the BK 32 tiles only
+    pp = [c for c in ops._conv_candidates(6272, 96, 864, False, 96, True) if c & ops.CONV_PP]
+    assert pp and all(ops._CONV_PP_BK[c & 255] == 32 for c in pp)
