@@ -20,6 +20,7 @@
 #include <vector>
 
 #include "gemm_core.h"
+#include "gemm_8ph.h"   // lab-only 8-phase schedule (not in the library)
 
 using namespace rdb;
 

@@ -100,6 +100,12 @@ class BertForSequenceClassification:
         # run on the raw rows with the LayerNorm folded into their weights, residual
         # adds normalise on load (_forward_hip_pstats)
         self.ln_pstats = os.environ.get("RDB_BERT_LN_PSTATS", "0") == "1"
+        if backend == "hip" and (self.fuse_residual_ln or self.rowln_o or self.rowln_d or self.ln_pstats):
+            from .. import ops as _ops_mod
+
+            if not _ops_mod.experimental_kernels_built():
+                raise RuntimeError("RDB_BERT_LNOUT / RDB_BERT_ROWLN / RDB_BERT_LN_PSTATS run kernels that lost their "
+                                   "A/Bs and are only in the opt-in RDB_EXPERIMENTAL_KERNELS build (ops/csrc/common.h)")
         env = os.environ.get("RDB_BERT_FOLD_LN", "")
         self.fold_ln_auto = env == ""
         self.fold_ln = env == "1" or (env == "" and self.auto_fold_ln(1))

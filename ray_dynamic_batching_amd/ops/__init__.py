@@ -251,17 +251,18 @@ def _tuned_cfg(key: tuple, launch: Callable[[int], None], candidates=range(NUM_T
 def _gemm_candidates(M: int, N: int, K: int, splitk: bool = False):
     """Dense GEMM tile choices: every tile cfg, plus the DEEP variants of the
     4-wave tiles whose grid is about one block per CU (``DEEP`` flag), plus
-    (``splitk``) split-K variants of the 4-wave tiles where the tile grid leaves
-    CUs idle and each split keeps >= 8 K steps (long-K GEMMs of small M: the
-    Llama prefill's down projection at 128 tokens is 128 blocks x 224 K steps)."""
+    (``splitk``) split-K variants of the 4-wave tiles and the BK-64 ping-pong
+    tiles 19 / 21 where the tile grid leaves CUs idle and each split keeps >= 8 K
+    steps (long-K GEMMs of small M: the Llama prefill's down projection at 128
+    tokens is 128 blocks x 224 K steps; at 1024 tokens 128 ping-pong tiles)."""
     cands = list(range(NUM_TILE_CFGS))
     if _GEMM_DEEP and K >= 256:
         cands += [c | DEEP for c in _DEEP_TILES
                   if c in _DEEP_BIG or -(-M // _TILE_BM[c]) * -(-N // _TILE_BN[c]) <= _DEEP_MAX_BLOCKS]
     if splitk and _GEMM_SPLITK:
         nk = -(-K // 64)
-        for c in range(NUM_CONV_TILE_CFGS):
-            tiles = -(-M // _TILE_BM[c]) * -(-N // _TILE_BN[c])
+        for c in list(range(NUM_CONV_TILE_CFGS)) + list(_PP_SPLITK_TILES):
+            tiles = -(-M // _ALL_BM[c]) * -(-N // _ALL_BN[c])
             if tiles >= 256:
                 continue
             for sp in _SPLITS:
@@ -269,7 +270,7 @@ def _gemm_candidates(M: int, N: int, K: int, splitk: bool = False):
                 eff = -(-nk // kper)
                 if eff < 2 or kper < 8 or tiles * eff > 1024:
                     continue
-                if SPLITK_HEADER + tiles * eff * _TILE_BM[c] * _TILE_BN[c] * 4 > SPLITK_WS_BYTES:
+                if SPLITK_HEADER + tiles * eff * _ALL_BM[c] * _ALL_BN[c] * 4 > SPLITK_WS_BYTES:
                     continue
                 cands.append(c | (sp << 8))
     return cands
@@ -1180,6 +1181,7 @@ _DEEP_MAX_BLOCKS = 320                # DEEP candidates only where the grid is ~
 SPLITK_HEADER = 65536                 # gemm_core.h kSplitKHeader (tile arrival counters)
 SPLITK_WS_BYTES = 40 << 20            # one forward's split-K workspace (ops.splitk_workspace)
 _SPLITS = (2, 3, 4, 6, 8)
+_PP_SPLITK_TILES = (19, 21)           # ping-pong tiles with a split-K instantiation (BK 64, gemm_core.h splitk_epi)
 _TILE_BM = (128, 64, 128, 64, 128, 192, 256, 128, 128, 64, 128, 256, 128)   # gemm_core.h kTileBM/BN, 4-wave tiles
 _TILE_BN = (128, 128, 64, 64, 192, 128, 128, 256, 144, 96, 96, 144, 48)
 _tune_ws: Dict[int, torch.Tensor] = {}
@@ -1314,10 +1316,10 @@ def conv2d_nhwc(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] =
             stride, pad, P, Q, ACT_CODE[act])
 
     def launch(c: int, ws: Optional[torch.Tensor]) -> None:
-        if c >= CONV_LINEAR:
+        if c >= 0 and c & CONV_LINEAR:
             _ops().gemm_tn(DTYPE_CODE[torch.float16], DTYPE_CODE[torch.float16], x.data_ptr(), C, w.data_ptr(), C,
                            out.data_ptr(), K, _ptr(bias), _ptr(residual), K if residual is not None else 0, M, K, C,
-                           1.0, ACT_CODE[act], _stream(), c - CONV_LINEAR)
+                           1.0, ACT_CODE[act], _stream(), c & ~CONV_LINEAR)
             return
         sp = splits_of(c)
         if sp > 1 and ws is None:
@@ -1458,6 +1460,15 @@ def se_scale_ref(x, s):
 # -D RDB_BLOCK_STAMPS``, loaded with RDB_OPS_SO).  bench/stamp_timeline.py turns
 # the records into co-residency / CU-time of the UN-profiled serving bench.
 # ---------------------------------------------------------------------------
+def experimental_kernels_built() -> bool:
+    """Whether the loaded kernel library carries the opt-in variants that lost
+    their A/Bs (stream-K, row-LayerNorm, LNOUT / staged-LN epilogues): built only
+    with ``python -m ray_dynamic_batching_amd._build --variant experimental -D
+    RDB_EXPERIMENTAL_KERNELS`` and loaded with RDB_OPS_SO (ops/csrc/common.h)."""
+    f = getattr(_ops(), "experimental_kernels_built", None)
+    return bool(f and f())
+
+
 def stamps_built() -> bool:
     """Whether the loaded kernel library is the RDB_BLOCK_STAMPS diagnostic build."""
     f = getattr(_ops(), "stamps_built", None)

@@ -97,6 +97,13 @@ PYBIND11_MODULE(_rdb_ops, m) {
   m.def("gemm_stg_cfg", &rdb::gemm_stg_cfg, "tile the staged-LayerNorm modes run for a requested cfg");
   m.def("gemm_tile_bn", &rdb::gemm_tile_bn, "N extent of tile cfg (partial-statistics count = ceil(N / BN))");
   m.def("gemm_rowln", &rdb::gemm_rowln, py::call_guard<py::gil_scoped_release>());
+#ifdef RDB_EXPERIMENTAL_KERNELS
+  constexpr bool experimental = true;
+#else
+  constexpr bool experimental = false;
+#endif
+  m.def("experimental_kernels_built", [] { return experimental; },
+        "whether the opt-in RDB_EXPERIMENTAL_KERNELS variants (stream-K, row-LN, LNOUT / staged LN) are compiled in");
   m.def("gemm_sk_bf16", &rdb::gemm_sk_bf16, py::call_guard<py::gil_scoped_release>());
   m.def("gemm_sk_workspace_size", &rdb::gemm_sk_workspace_size);
   m.def("norm_fwd", &rdb::norm_fwd, py::call_guard<py::gil_scoped_release>());

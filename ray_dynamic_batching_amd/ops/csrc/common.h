@@ -3,6 +3,23 @@
 // Everything here is written for a 64-lane wavefront and the gfx950 MFMA
 // instruction set; there is no portability layer.
 #pragma once
+#include <stdexcept>
+#include <string>
+// RDB_EXPERIMENTAL_KERNELS: kernel variants that lost their A/Bs (stream-K,
+// the full-row GEMM+LayerNorm, the LNOUT / staged-partial-statistics LayerNorm
+// epilogues) are only compiled into an opt-in build:
+//   python -m ray_dynamic_batching_amd._build --variant experimental -D RDB_EXPERIMENTAL_KERNELS
+// (loaded with RDB_OPS_SO=<that .so>).  The default library's entry points
+// for them throw.
+#ifdef RDB_EXPERIMENTAL_KERNELS
+#define RDB_EXPERIMENTAL 1
+#else
+#define RDB_EXPERIMENTAL 0
+#endif
+#define RDB_EXPERIMENTAL_MISSING(WHAT)                                                                 \
+  throw std::runtime_error(std::string(WHAT) +                                                          \
+                           ": experimental kernel not in this build (python -m ray_dynamic_batching_amd._build " \
+                           "--variant experimental -D RDB_EXPERIMENTAL_KERNELS, then RDB_OPS_SO=<that .so>)")
 #include <hip/hip_runtime.h>
 #include <hip/hip_bf16.h>
 #include <stdint.h>

@@ -1230,7 +1230,6 @@ mfma_gemm_kernel(typename LoaderT<T, 1>::Params ap, const T* __restrict__ W, int
 
 }  // namespace rdb
 #include "gemm_pp.h"
-#include "gemm_8ph.h"
 namespace rdb {
 
 // Tile table (index = the `cfg` argument): BM x BN with WGM waves along M.
@@ -1366,7 +1365,14 @@ void launch_mfma_gemm_t(const P& ap, const T* W, int ldw, OutT* C, int ldc, cons
   } else {
     // the ping-pong tiles (19..) take plain staged epilogues only: deferred-LN modes,
     // SwiGLU and unaligned / N % 8 != 0 outputs run the 8-wave 256x192 tile instead
-    if (cfg >= 19 && (EPI != 0 || !gemm_pp_ok(N, ldc, ldr, C, bias, R, act))) cfg = 15;
+    if (cfg >= 19 && (EPI != 0 || !gemm_pp_ok(N, ldc, ldr, C, bias, R, act))) {
+      cfg = 15;
+      if (EPI == 0 && ln.sk_kper > 0) {   // split-K was requested for the pp tile: the 8-wave fallback runs unsplit
+        launch_mfma_gemm_t<T, OutT, LoaderT, HB, HR, EPI>(ap, W, ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act, s, 15,
+                                                          LnEpi{});
+        return;
+      }
+    }
     if constexpr (EPI == 0 && sizeof(OutT) == 2) {
       if (deep) {
 #define RDB_TILE_DEEP(IDX, BM_, BN_)                                                                             \
@@ -1418,14 +1424,24 @@ void launch_mfma_gemm_t(const P& ap, const T* W, int ldw, OutT* C, int ldc, cons
       }
       if constexpr (EPI == 0 && sizeof(OutT) == 2) {
         switch (cfg) {
-          case 19: launch_gemm_pp<T, OutT, 8, 256, 128, 2, 2, 3>(static_cast<const T*>(ap.A), ap.lda, W, ldw, C, ldc,
-                                                                  bias, R, ldr, M, N, K, alpha, act, s);
+          case 19:
+            if (ln.sk_kper > 0)
+              launch_gemm_pp_sk<T, OutT, 8, 256, 128, 2, 2, 3>(static_cast<const T*>(ap.A), ap.lda, W, ldw, C, ldc,
+                                                               bias, R, ldr, M, N, K, alpha, act, s, ln);
+            else
+              launch_gemm_pp<T, OutT, 8, 256, 128, 2, 2, 3>(static_cast<const T*>(ap.A), ap.lda, W, ldw, C, ldc,
+                                                            bias, R, ldr, M, N, K, alpha, act, s);
             return;
           case 20: launch_gemm_pp<T, OutT, 8, 256, 144, 4, 1, 3>(static_cast<const T*>(ap.A), ap.lda, W, ldw, C, ldc,
                                                                   bias, R, ldr, M, N, K, alpha, act, s);
             return;
-          case 21: launch_gemm_pp<T, OutT, 8, 128, 256, 1, 4, 3>(static_cast<const T*>(ap.A), ap.lda, W, ldw, C, ldc,
-                                                                  bias, R, ldr, M, N, K, alpha, act, s);
+          case 21:
+            if (ln.sk_kper > 0)
+              launch_gemm_pp_sk<T, OutT, 8, 128, 256, 1, 4, 3>(static_cast<const T*>(ap.A), ap.lda, W, ldw, C, ldc,
+                                                               bias, R, ldr, M, N, K, alpha, act, s, ln);
+            else
+              launch_gemm_pp<T, OutT, 8, 128, 256, 1, 4, 3>(static_cast<const T*>(ap.A), ap.lda, W, ldw, C, ldc,
+                                                            bias, R, ldr, M, N, K, alpha, act, s);
             return;
           case 22: launch_gemm_pp<T, OutT, 8, 256, 256, 2, 2, 4, 32>(static_cast<const T*>(ap.A), ap.lda, W, ldw, C,
                                                                       ldc, bias, R, ldr, M, N, K, alpha, act, s);
@@ -1462,7 +1478,8 @@ inline size_t splitk_bytes(int M, int N, int cfg, int splits) {
 // workspace, too many tiles, > 2^31 partial bytes): the launch then runs unsplit.
 inline LnEpi splitk_epi(int M, int N, int K, int cfg, int splits, void* ws, size_t ws_bytes) {
   LnEpi e{};
-  if (splits < 2 || ws == nullptr || cfg < 0 || cfg >= kNumTiles4) return e;
+  // the 4-wave tiles, and the BK 64 ping-pong tiles 19 / 21 (gemm_pp.h SK instantiations)
+  if (splits < 2 || ws == nullptr || cfg < 0 || (cfg >= kNumTiles4 && cfg != 19 && cfg != 21)) return e;
   const int nk = (K + 63) / 64;
   const int kper = (nk + splits - 1) / splits;
   const int eff = (nk + kper - 1) / kper;
@@ -1484,8 +1501,8 @@ void launch_mfma_gemm(const P& ap, const T* W, int ldw, OutT* C, int ldc, const 
   const int deep = (cfg >= 0 && (cfg & kDeepFlag) != 0) ? kDeepFlag : 0;
   if (cfg >= 0) cfg &= 0xFF;
   if (cfg < 0 || cfg >= (dense ? kNumTiles : kNumTiles4)) cfg = pick_tile_cfg(M, N, dense);
-  // split-K runs on the 4-wave tiles (0..12) only: their kernel carries the hand-off
-  const LnEpi e = (ln.sk_kper > 0 && cfg < kNumTiles4 && act != ACT_SWIGLU) ? ln : LnEpi{};
+  // split-K runs on the 4-wave tiles (0..12) and the ping-pong tiles 19 / 21: their kernels carry the hand-off
+  const LnEpi e = (ln.sk_kper > 0 && (cfg < kNumTiles4 || cfg == 19 || cfg == 21) && act != ACT_SWIGLU) ? ln : LnEpi{};
   cfg |= deep;
   if (bias && R)
     launch_mfma_gemm_t<T, OutT, LoaderT, true, true>(ap, W, ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act, s, cfg, e);

@@ -18,6 +18,7 @@
 // BertLayer LayerNorms of the served models.
 #include "gemm_core.h"
 #include <stdexcept>
+#include <string>
 
 namespace rdb {
 
@@ -88,6 +89,7 @@ void gemm_tn_ln(uintptr_t A, int lda, uintptr_t W, int ldw, uintptr_t C, int ldc
       launch_mfma_gemm_t<bf16, bf16, DenseLoader, true, true, EPI_LNR>(p, w, ldw, c, ldc, b, r, ldr, M, N, K, alpha,
                                                                        act, s, cfg, ln);
       break;
+#if RDB_EXPERIMENTAL
     case EPI_LNOUT: {
       need(bias && R && r_g && r_b && o_stats && panel && act == ACT_NONE,
            "gemm_tn_ln: LNOUT needs bias, R, r_g/r_b, o_stats, panel workspaces and no activation");
@@ -109,11 +111,13 @@ void gemm_tn_ln(uintptr_t A, int lda, uintptr_t W, int ldw, uintptr_t C, int ldc
                                                                          act, s, cfg, ln);
       break;
     }
+#endif
     case EPI_LNA | EPI_SELF:
       need(a_colsum && a_bias && !bias && !R, "gemm_tn_ln: LNA|SELF needs a_colsum/a_bias, no bias/R");
       launch_mfma_gemm_t<bf16, bf16, DenseLoader, false, false, EPI_LNA | EPI_SELF>(p, w, ldw, c, ldc, b, r, ldr, M, N,
                                                                                     K, alpha, act, s, cfg, ln);
       break;
+#if RDB_EXPERIMENTAL
     case EPI_STG | EPI_LNA:
       need(a_stats && a_colsum && a_bias && !bias && !R, "gemm_tn_ln: STG|LNA needs a_stats/a_colsum/a_bias, no bias/R");
       launch_mfma_gemm_t<bf16, bf16, DenseLoader, false, false, EPI_STG | EPI_LNA>(p, w, ldw, c, ldc, b, r, ldr, M, N,
@@ -134,6 +138,14 @@ void gemm_tn_ln(uintptr_t A, int lda, uintptr_t W, int ldw, uintptr_t C, int ldc
       launch_mfma_gemm_t<bf16, bf16, DenseLoader, true, true, EPI_STG | EPI_LNR>(p, w, ldw, c, ldc, b, r, ldr, M, N,
                                                                                  K, alpha, act, s, cfg, ln);
       break;
+#else
+    case EPI_LNOUT:
+    case EPI_STG | EPI_LNA:
+    case EPI_STG | EPI_STATS:
+    case EPI_STG | EPI_LNR | EPI_STATS:
+    case EPI_STG | EPI_LNR:
+      RDB_EXPERIMENTAL_MISSING("gemm_tn_ln (LNOUT / staged modes)");
+#endif
     default:
       throw std::invalid_argument(
           "gemm_tn_ln: mode must be LNA (1), STATS (4), LNR|STATS (6), LNR (2), LNA|SELF (9), LNOUT (16) or a "

@@ -96,10 +96,10 @@ struct ConvGeom {
 // LDS must then fit twice in 160 KiB)
 // EPI: 0, EPI_SWG (SwiGLU) or an EPI_STG LayerNorm mode (gemm_core.h): LN operands
 // are staged in LDS after the bias by the prologue and applied by the staged epilogue.
-// CONV: A is the im2col view described by `cv` (lda unused) and the launch may
+// CONV: A is the im2col view described by `cv` (lda unused).  SK: the launch may
 // split K over gridDim.y (ln.sk_* : the gemm_core.h split-K hand-off).
 template <typename T, typename OutT, int NW, int BM, int BN, int GM, int GN, int STAGES, bool HAS_BIAS, bool HAS_RES,
-          int BK_ = 64, int OCC = 2, int EPI = 0, bool CONV = false>
+          int BK_ = 64, int OCC = 2, int EPI = 0, bool CONV = false, bool SK = CONV>
 __global__ void __launch_bounds__(64 * NW, OCC)
 gemm_pp_kernel(const T* __restrict__ A, int lda, const T* __restrict__ W, int ldw, OutT* __restrict__ C, int ldc,
                const T* __restrict__ bias, const T* __restrict__ R, int ldr, int M, int N, int K, float alpha,
@@ -249,9 +249,9 @@ gemm_pp_kernel(const T* __restrict__ A, int lda, const T* __restrict__ W, int ld
   constexpr int kVm0 = 0x70 | 0xF00;
   constexpr int kLgkm0 = 0xC07F;            // lgkmcnt(0), vmcnt and expcnt at max
 
-  // split-K (CONV launches with gridDim.y > 1): this block runs K-tiles [kb, kb + nk)
+  // split-K (SK launches with gridDim.y > 1): this block runs K-tiles [kb, kb + nk)
   int kb = 0, nk = (K + BK - 1) / BK;
-  if constexpr (CONV) {
+  if constexpr (SK) {
     if (gridDim.y > 1) {
       kb = blockIdx.y * ln.sk_kper;
       nk = min(ln.sk_kper, nk - kb);
@@ -307,7 +307,7 @@ gemm_pp_kernel(const T* __restrict__ A, int lda, const T* __restrict__ W, int ld
 #ifdef RDB_PP_STAMPS
   const unsigned long long t_loop = __builtin_amdgcn_s_memtime();
 #endif
-  if constexpr (CONV) {
+  if constexpr (SK) {
     if (gridDim.y > 1) {
       // ---- split-K hand-off (mfma_gemm_kernel's protocol): a non-last split
       // stores its f32 partial (sc1), drains, meets at a barrier and one lane
@@ -419,6 +419,28 @@ void launch_gemm_pp(const T* A, int lda, const T* W, int ldw, OutT* C, int ldc, 
   else
     hipLaunchKernelGGL((gemm_pp_kernel<T, OutT, NW, BM, BN, GM, GN, STAGES, false, false, BK, OCC>), grid, block, 0, s, A, lda,
                        W, ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act, ln, ConvGeom{});
+}
+
+// Split-K on a ping-pong tile (sk from splitk_epi: K-steps of 64 per split =
+// BK 64 tiles only): gridDim.y = the number of non-empty splits.
+template <typename T, typename OutT, int NW, int BM, int BN, int GM, int GN, int STAGES>
+void launch_gemm_pp_sk(const T* A, int lda, const T* W, int ldw, OutT* C, int ldc, const T* bias, const T* R, int ldr,
+                       int M, int N, int K, float alpha, int act, hipStream_t s, const LnEpi& sk) {
+  const int nwg = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  const int nk = (K + 63) / 64;
+  const dim3 grid(nwg, (nk + sk.sk_kper - 1) / sk.sk_kper), block(64 * NW);
+  if (bias && R)
+    hipLaunchKernelGGL((gemm_pp_kernel<T, OutT, NW, BM, BN, GM, GN, STAGES, true, true, 64, 2, 0, false, true>), grid,
+                       block, 0, s, A, lda, W, ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act, sk, ConvGeom{});
+  else if (bias)
+    hipLaunchKernelGGL((gemm_pp_kernel<T, OutT, NW, BM, BN, GM, GN, STAGES, true, false, 64, 2, 0, false, true>), grid,
+                       block, 0, s, A, lda, W, ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act, sk, ConvGeom{});
+  else if (R)
+    hipLaunchKernelGGL((gemm_pp_kernel<T, OutT, NW, BM, BN, GM, GN, STAGES, false, true, 64, 2, 0, false, true>), grid,
+                       block, 0, s, A, lda, W, ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act, sk, ConvGeom{});
+  else
+    hipLaunchKernelGGL((gemm_pp_kernel<T, OutT, NW, BM, BN, GM, GN, STAGES, false, false, 64, 2, 0, false, true>), grid,
+                       block, 0, s, A, lda, W, ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act, sk, ConvGeom{});
 }
 
 // The staged-LayerNorm modes (EPI_STG | ...) on a ping-pong tile.  LNA: no bias

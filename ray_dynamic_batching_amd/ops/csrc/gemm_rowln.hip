@@ -46,6 +46,7 @@
 
 namespace rdb {
 
+#if RDB_EXPERIMENTAL
 template <int NFULL>
 __global__ void __launch_bounds__(512, 2)
 gemm_rowln_kernel(const bf16* __restrict__ A, int lda, const bf16* __restrict__ W,
@@ -259,5 +260,11 @@ void gemm_rowln(uintptr_t A, int lda, uintptr_t W, uintptr_t bias, uintptr_t R, 
                      reinterpret_cast<const bf16*>(beta), reinterpret_cast<bf16*>(C), ldc, M, K, eps);
   RDB_HIP_CHECK(hipGetLastError());
 }
+#else
+void gemm_rowln(uintptr_t, int, uintptr_t, uintptr_t, uintptr_t, int, uintptr_t, uintptr_t, uintptr_t, int, int, int,
+                int, float, uintptr_t) {
+  RDB_EXPERIMENTAL_MISSING("gemm_rowln");
+}
+#endif
 
 }  // namespace rdb

@@ -3,10 +3,15 @@
 // 128 x 128 tile at BK = 64 (4 stages).  Own translation unit: the header is
 // not pulled into gemm_core.h's users.
 #include "gemm_core.h"
+#if RDB_EXPERIMENTAL
 #include "gemm_sk.h"
+#endif
+#include <stdexcept>
+#include <string>
 
 namespace rdb {
 
+#if RDB_EXPERIMENTAL
 size_t gemm_sk_workspace_size(int tile, int grid) {
   return tile == 1 ? gemm_sk_workspace_bytes<128, 128>(grid) : gemm_sk_workspace_bytes<256, 128>(grid);
 }
@@ -31,5 +36,12 @@ void gemm_sk_bf16(uintptr_t A, int lda, uintptr_t W, int ldw, uintptr_t C, int l
                                                          grid, s);
   RDB_HIP_CHECK(hipGetLastError());
 }
+#else
+size_t gemm_sk_workspace_size(int, int) { RDB_EXPERIMENTAL_MISSING("gemm_sk"); }
+void gemm_sk_bf16(uintptr_t, int, uintptr_t, int, uintptr_t, int, uintptr_t, uintptr_t, int, int, int, int, float, int,
+                  uintptr_t, int, int, uintptr_t) {
+  RDB_EXPERIMENTAL_MISSING("gemm_sk");
+}
+#endif
 
 }  // namespace rdb

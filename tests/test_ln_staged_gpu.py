@@ -18,6 +18,13 @@ def _ops():
     return ops
 
 
+@pytest.fixture(autouse=True)
+def _experimental_build():
+    # the staged-LN modes are in the opt-in RDB_EXPERIMENTAL_KERNELS build (ops/csrc/common.h)
+    if not _ops().experimental_kernels_built():
+        pytest.skip("opt-in RDB_EXPERIMENTAL_KERNELS build not loaded")
+
+
 def _ln(x, g, b, eps):
     xf = x.float()
     mu = xf.mean(-1, keepdim=True)

@@ -30,7 +30,7 @@ def test_conv_candidates_encode_valid_choices():
                 assert ops.SPLITK_HEADER + tiles * -(-nk // kper) * ops._TILE_BM[tile] * ops._TILE_BN[tile] * 4 \
                     <= ops.SPLITK_WS_BYTES
         if one:
-            assert any(c >= ops.CONV_LINEAR for c in cands)
+            assert any(c & ops.CONV_LINEAR for c in cands)
         if M == 1568:
             assert any((c >> 8) & 15 for c in cands)                # the small-grid conv gets split-K choices
 
@@ -113,3 +113,19 @@ def test_conv_pp_candidates():
     # C = 96 (no BK divides it... 96 % 32 == 0): the BK 32 tiles only
     pp = [c for c in ops._conv_candidates(6272, 96, 864, False, 96, True) if c & ops.CONV_PP]
     assert pp and all(ops._CONV_PP_BK[c & 255] == 32 for c in pp)
+
+
+def test_gemm_candidates_pingpong_splitk():
+    """Llama-3-8B prefill down projection at 8 x 128 tokens (1024 x 4096 x 14336):
+    128 ping-pong 256x128 tiles leave half the CUs idle, so tiles 19 / 21 get
+    split-K choices (workspace-bounded); a full grid gets none."""
+    cands = ops._gemm_candidates(1024, 4096, 14336, splitk=True)
+    pp = [c for c in cands if (c & 255) in ops._PP_SPLITK_TILES and ops.splits_of(c) > 1]
+    assert pp
+    for c in pp:
+        t, sp = c & 255, ops.splits_of(c)
+        tiles = -(-1024 // ops._ALL_BM[t]) * -(-4096 // ops._ALL_BN[t])
+        nk = 14336 // 64
+        eff = -(-nk // -(-nk // sp))
+        assert ops.SPLITK_HEADER + tiles * eff * ops._ALL_BM[t] * ops._ALL_BN[t] * 4 <= ops.SPLITK_WS_BYTES
+    assert not [c for c in ops._gemm_candidates(4096, 3072, 768, splitk=True) if ops.splits_of(c) > 1 and (c & 255) >= 19]

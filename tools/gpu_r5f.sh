@@ -9,7 +9,7 @@ cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 T=$GRAFT_REPO_ROOT/$O/resnet_pp_table.json
 rm -f $T
 V=$GRAFT_REPO_ROOT/ray_dynamic_batching_amd/_variants/stamps/_rdb_ops.cpython-310-x86_64-linux-gnu.so
-timeout -k 10 400 python3 -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_ops_gpu.py -k "conv2d" > $O/pytest_conv.log 2>&1 && \
+timeout -k 10 400 python3 -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_ops_gpu.py tests/test_ln_staged_gpu.py -k "conv2d or splitk or streamk or rowln or residual_ln or staged or partial" > $O/pytest_conv.log 2>&1 && \
 RDB_TUNE_FILE=$T timeout -k 10 600 python3 -u bench/serve_bench.py --model resnet50 --closed 96 --seconds 8 --json-out $O/resnet_tune.json > $O/resnet_tune.out 2> $O/resnet_tune.err && \
 RDB_TUNE_FILE=$T timeout -k 10 300 python3 bench/serve_bench.py --model resnet50 --closed 96 --seconds 8 --json-out $O/resnet_new_r1.json > $O/resnet_new_r1.out 2>&1 && \
 timeout -k 10 300 python3 bench/serve_bench.py --model resnet50 --closed 96 --seconds 8 --json-out $O/resnet_old_r1.json > $O/resnet_old_r1.out 2>&1 && \
