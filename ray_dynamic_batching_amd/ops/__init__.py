@@ -1200,9 +1200,15 @@ def _private_splitk_ws(device, need: int) -> torch.Tensor:
     """The split-K workspace a launch without a caller workspace uses: one per
     (device, stream), grown on demand, so a forward that passes none pays no
     allocation or counter memset per call.  Split-K launches leave the counters
-    zero, so consecutive launches on one stream may share it (two streams never do)."""
-    key = (str(device), _stream())
+    zero, so consecutive launches on one stream may share it (two streams never do).
+    Inside a graph capture the workspace comes from the graph's own pool, zeroed
+    by a memset node, and is never cached: a cached one would be shared by graphs
+    that the engine replays concurrently on different streams, and would pin the
+    capture pool past the graph's lifetime."""
     need = max(SPLITK_HEADER, int(need))
+    if torch.cuda.is_current_stream_capturing():
+        return splitk_workspace(device, need)
+    key = (str(device), _stream())
     ws = _priv_ws.get(key)
     if ws is None or ws.numel() < need:
         ws = _priv_ws[key] = splitk_workspace(device, max(need, SPLITK_WS_BYTES))

@@ -406,6 +406,40 @@ def test_linear_splitk(M, N, K):
         _close(y, x.float() @ w.float().t() + b.float() + r.float(), 2e-2, 2e-2)
 
 
+def test_linear_splitk_private_workspace_per_graph():
+    """Split-K without a caller workspace inside graph capture: each graph gets
+    its own (graph-pool) workspace, so two graphs captured on ONE stream and
+    replayed concurrently on two streams do not share counters / partials, and
+    capturing again after the graphs are gone works (no cached pool tensor)."""
+    ops = _ops()
+    torch.manual_seed(21)
+    M, N, K = 1024, 4096, 4096
+    w = torch.randn(N, K, device="cuda", dtype=torch.bfloat16) * K ** -0.5
+    b = torch.randn(N, device="cuda", dtype=torch.bfloat16) * 0.1
+    xs = [torch.randn(M, K, device="cuda", dtype=torch.bfloat16) for _ in range(2)]
+    for rnd in range(2):
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        gs, ys = [], []
+        with torch.cuda.stream(side):
+            for i in range(2):
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, pool=torch.cuda.graph_pool_handle(), stream=side):
+                    ys.append(ops.linear(xs[i], w, b, tile_cfg=19 | (2 << 8)))
+                gs.append(g)
+        torch.cuda.synchronize()
+        sts = [torch.cuda.Stream() for _ in range(2)]
+        for _ in range(3):
+            for g, st in zip(gs, sts):
+                st.wait_stream(torch.cuda.current_stream())
+                with torch.cuda.stream(st):
+                    g.replay()
+            torch.cuda.synchronize()
+            for i in range(2):
+                _close(ys[i], xs[i].float() @ w.float().t() + b.float(), 2e-2, 2e-2)
+        del gs, ys
+
+
 def test_conv2d_splitk_graph_replay():
     """Split-K inside a captured graph with the per-forward workspace idiom of
     ResNet50._logits_hip, replayed with new inputs."""
