@@ -119,6 +119,9 @@ def build_ops(force: bool = False, jobs: int | None = None, verbose: bool = Fals
     cc = hipcc()
     common = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wno-unused-result",
               f"-I{OPS_SRC}", f"-I{RT_SRC}"] + _pybind_includes() + [f"-D{d}" for d in defines]
+    if variant:
+        # A/B builds may add compiler flags (e.g. "-mllvm -amdgpu-mfma-vgpr-form=1")
+        common += os.environ.get("RDB_VARIANT_HIPFLAGS", "").split()
     objs = []
     cmds = []
     for s in srcs:
