@@ -25,8 +25,12 @@ H2D on a side stream, replays the hipGraph of the batched forward, and returns
 per-request logits through the completion ring.
 
 One "step" = 32 x N completed requests (one full dynamic batch per replica).
-The timed region is bracketed by barrier + torch.cuda.synchronize() on every
-rank; the reported time is the max over ranks.  Latency percentiles are
+Untimed set-up: model load, tile table, graph capture, then the engine's device
+warm-up (EngineRunner.build: ~0.25 s of graph replays, so serving starts at
+steady clocks, as a production replica does before it reports ready), then the
+W warm-up steps.  The timed region is bracketed by barrier +
+torch.cuda.synchronize() on every rank and contains exactly K steps of the full
+request path; the reported time is the max over ranks.  Latency percentiles are
 client-side end-to-end (submit -> result received).
 """
 from __future__ import annotations
@@ -206,6 +210,32 @@ def main():
     job.configure_queue(rank, rank, 0, args.concurrency * 2, 0.0, True)
 
     cfg = BertConfig(seq_len=args.seq, layers=args.layers)
+    # The ingress: every rank runs G native generator threads (GIL released
+    # inside run()), each with its own client and completion ring, all routing
+    # through the power-of-two choice over EVERY replica's queue depth -- like
+    # Serve, where each proxy / handle owns a router over all replicas.  One
+    # ingress per rank keeps submission and completion draining spread over
+    # the node's processes instead of funnelling 8 GPUs' traffic through rank 0.
+    # `--ingress rank0` keeps the single node-wide ingress on rank 0.  Built
+    # BEFORE the engine: the engine's device warm-up (EngineRunner.build) is then
+    # followed only by the W warm-up steps, not by host-side set-up.
+    from concurrent.futures import ThreadPoolExecutor
+
+    drivers = range(n) if args.ingress == "per-rank" else [0]
+    n_drv = len(drivers)
+    is_driver = rank in drivers
+    G = args.ingress_threads or (1 if args.ingress == "per-rank" else min(4, max(1, n // 2)))
+    if is_driver:
+        g = torch.Generator().manual_seed(1234 + rank)
+        payloads = []
+        for _ in range(256):
+            ids = torch.randint(1, cfg.vocab_size, (args.seq,), generator=g, dtype=torch.int32)
+            ids[0] = 101
+            payloads.append(ids.numpy().tobytes())
+        clients = [rjob.Client(job, seed=1234 + 64 * rank + i) for i in range(G)]
+        gens = [rjob.LoadGen(c, 0, payloads) for c in clients]
+        pool = ThreadPoolExecutor(G)
+        slot = list(drivers).index(rank)
     os.environ.setdefault("RDB_TUNE_STREAMS", str(args.tune_streams or args.compute_streams))
     tile_table = _tile_table(args)
     if tile_table and "RDB_TUNE_FILE" not in os.environ:
@@ -228,31 +258,7 @@ def main():
 
     result = {}
     per_step = args.max_batch * n
-    # The ingress: every rank runs G native generator threads (GIL released
-    # inside run()), each with its own client and completion ring, all routing
-    # through the power-of-two choice over EVERY replica's queue depth -- like
-    # Serve, where each proxy / handle owns a router over all replicas.  One
-    # ingress per rank keeps submission and completion draining spread over
-    # the node's processes instead of funnelling 8 GPUs' traffic through rank 0.
-    # `--ingress rank0` keeps the single node-wide ingress on rank 0.
-    from concurrent.futures import ThreadPoolExecutor
-
-    drivers = range(n) if args.ingress == "per-rank" else [0]
-    n_drv = len(drivers)
-    is_driver = rank in drivers
-    G = args.ingress_threads or (1 if args.ingress == "per-rank" else min(4, max(1, n // 2)))
     if is_driver:
-        g = torch.Generator().manual_seed(1234 + rank)
-        payloads = []
-        for _ in range(256):
-            ids = torch.randint(1, cfg.vocab_size, (args.seq,), generator=g, dtype=torch.int32)
-            ids[0] = 101
-            payloads.append(ids.numpy().tobytes())
-        clients = [rjob.Client(job, seed=1234 + 64 * rank + i) for i in range(G)]
-        gens = [rjob.LoadGen(c, 0, payloads) for c in clients]
-        pool = ThreadPoolExecutor(G)
-        slot = list(drivers).index(rank)
-
         def share(total, k, i):
             return total // k + (1 if i < total % k else 0)
 

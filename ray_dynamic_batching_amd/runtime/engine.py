@@ -102,7 +102,14 @@ class EngineRunner:
             n *= s
         return n * torch.empty((), dtype=dtype).element_size()
 
-    def build(self) -> "EngineRunner":
+    def build(self, warm_s: Optional[float] = None) -> "EngineRunner":
+        """Capture every session's graphs, then warm the device: ``warm_s``
+        seconds (default RDB_ENGINE_WARM_S, 0.25) of back-to-back replays of the
+        largest bucket on every compute stream, so the first served batches do not
+        run at idle clocks / cold caches (what a production replica does before it
+        reports ready).  The replays write only the sessions' own output slots."""
+        import os
+
         t0 = time.perf_counter()
         self.pools = [torch.cuda.graph_pool_handle() for _ in range(self.compute_streams)]
         for s in self.sessions:
@@ -113,7 +120,32 @@ class EngineRunner:
 
             ops.save_tuning(self.tune_file)
         self.capture_s = time.perf_counter() - t0
+        self.warm_device(float(os.environ.get("RDB_ENGINE_WARM_S", "0.25")) if warm_s is None else warm_s)
         return self
+
+    def warm_device(self, seconds: float) -> int:
+        """Replay the largest bucket's graphs of every session on the compute
+        streams for ``seconds``; returns the number of replays (before start())."""
+        if seconds <= 0:
+            return 0
+        streams = [torch.cuda.Stream(device=self.device) for _ in range(self.compute_streams)]
+        cur = torch.cuda.current_stream()
+        n = 0
+        t_end = time.perf_counter() + seconds
+        while time.perf_counter() < t_end:
+            for st in streams:
+                st.wait_stream(cur)
+            for s in self.sessions:
+                if not s.graphs:
+                    continue
+                for slot, g in enumerate(s.graphs[-1]):
+                    with torch.cuda.stream(streams[slot % self.compute_streams]):
+                        g.replay()
+                    n += 1
+            for st in streams:
+                cur.wait_stream(st)
+            torch.cuda.synchronize(self.device)
+        return n
 
     def _capture(self, s: SessionSpec, live: bool) -> None:
         """Warm up, (tune,) capture and register one session's graphs.  ``live``:
