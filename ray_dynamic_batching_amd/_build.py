@@ -99,6 +99,12 @@ def hipcc() -> str:
     return p
 
 
+# per-source compiler flags: gemm_v4.hip's one-block-per-CU kernels keep their
+# MFMA accumulators in VGPR form (the default heuristic picks AGPRs and copies
+# them after every MFMA: profiles/gemm_lab_r5_v4.txt)
+SRC_FLAGS = {"gemm_v4.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"]}
+
+
 def variant_target(name: str) -> Path:
     """Where ``build_ops(variant=name)`` puts an A/B build of the kernels
     (loaded instead of the default one when ``RDB_OPS_SO`` points at it)."""
@@ -131,7 +137,7 @@ def build_ops(force: bool = False, jobs: int | None = None, verbose: bool = Fals
         if not force and o.exists() and o.stat().st_mtime >= newest:
             continue  # object up to date
         lang = ["-x", "hip"] if s.suffix == ".hip" else []
-        cmds.append([cc] + common + lang + ["-c", str(s), "-o", str(o)])
+        cmds.append([cc] + common + SRC_FLAGS.get(s.name, []) + lang + ["-c", str(s), "-o", str(o)])
     jobs = jobs or min(8, os.cpu_count() or 4, 16)
     with cf.ThreadPoolExecutor(jobs) as ex:
         for c in cmds:

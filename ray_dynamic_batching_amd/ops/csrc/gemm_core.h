@@ -1249,15 +1249,22 @@ namespace rdb {
 // 24 / 25 = ping-pong 256x192 at BK = 32 with 3 / 4 stages (89 / 119 KiB): a
 // 4096 x 3072 GEMM (BERT FFN-up) is exactly 256 tiles = one per CU, where 23
 // leaves 1.5 blocks per CU, at 1/110 operand bytes per FLOP vs 1/85 for 256x128.
-constexpr int kNumTiles = 26;
+// 26 / 27 / 28 = the 4-wave VGPR-staged tiles of gemm_v4.h (128x96, 128x128,
+// 256x192; one block per CU; own translation unit gemm_v4.hip, K % 64 == 0).
+constexpr int kNumTiles = 29;
 //                                 0    1    2    3    4    5    6    7    8    9   10   11   12 | 8-wave: 13   14   15   16   17   18 | pp: 19   20   21   22   23   24   25
-constexpr int kTileBM[kNumTiles] = {128, 64, 128, 64, 128, 192, 256, 128, 128, 64, 128, 256, 128, 256, 128, 256, 256, 128, 256, 256, 256, 128, 256, 256, 256, 256};
-constexpr int kTileBN[kNumTiles] = {128, 128, 64, 64, 192, 128, 128, 256, 144, 96, 96, 144, 48, 128, 256, 192, 144, 96, 96, 128, 144, 256, 256, 128, 192, 192};
+constexpr int kTileBM[kNumTiles] = {128, 64, 128, 64, 128, 192, 256, 128, 128, 64, 128, 256, 128, 256, 128, 256, 256, 128, 256, 256, 256, 128, 256, 256, 256, 256, 128, 128, 256};
+constexpr int kTileBN[kNumTiles] = {128, 128, 64, 64, 192, 128, 128, 256, 144, 96, 96, 144, 48, 128, 256, 192, 144, 96, 96, 128, 144, 256, 256, 128, 192, 192, 96, 128, 192};
 // tile cfg flag: the DEEP (one block per CU, up to 8 LDS stages) variant of
 // 4-wave tiles 0, 1, 2, 3, 6, 7, 9, 10 (plain epilogues); other tiles ignore it
 constexpr int kDeepFlag = 1 << 12;
-constexpr int kTileWGM[kNumTiles] = {2, 2, 2, 2, 2, 2, 2, 2, 4, 2, 2, 4, 4, 4, 2, 4, 8, 4, 8, 4, 8, 2, 4, 4, 4, 4};
-constexpr int kTileNW[kNumTiles] = {4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 8, 8, 8, 8, 8, 8, 8, 8, 8, 8, 8, 8, 8};
+constexpr int kTileWGM[kNumTiles] = {2, 2, 2, 2, 2, 2, 2, 2, 4, 2, 2, 4, 4, 4, 2, 4, 8, 4, 8, 4, 8, 2, 4, 4, 4, 4, 2, 2, 2};
+constexpr int kTileNW[kNumTiles] = {4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 8, 8, 8, 8, 8, 8, 8, 8, 8, 8, 8, 8, 8, 4, 4, 4};
+
+// gemm_v4.hip (tile cfgs 26..28): dtype 0 = bf16, 1 = f16; 16-bit output, plain epilogues
+void launch_gemm_v4_cfg(int cfg, int dtype, const void* A, int lda, const void* W, int ldw, void* C, int ldc,
+                        const void* bias, const void* R, int ldr, int M, int N, int K, float alpha, int act,
+                        hipStream_t s);
 
 inline int tile_blocks_per_cu(int cfg) {
   if (cfg == 23) return 2;
@@ -1365,7 +1372,7 @@ void launch_mfma_gemm_t(const P& ap, const T* W, int ldw, OutT* C, int ldc, cons
   } else {
     // the ping-pong tiles (19..) take plain staged epilogues only: deferred-LN modes,
     // SwiGLU and unaligned / N % 8 != 0 outputs run the 8-wave 256x192 tile instead
-    if (cfg >= 19 && (EPI != 0 || !gemm_pp_ok(N, ldc, ldr, C, bias, R, act))) {
+    if (cfg >= 19 && (EPI != 0 || !gemm_pp_ok(N, ldc, ldr, C, bias, R, act) || (cfg >= 26 && K % 64 != 0))) {
       cfg = 15;
       if (EPI == 0 && ln.sk_kper > 0) {   // split-K was requested for the pp tile: the 8-wave fallback runs unsplit
         launch_mfma_gemm_t<T, OutT, LoaderT, HB, HR, EPI>(ap, W, ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act, s, 15,
@@ -1454,6 +1461,12 @@ void launch_mfma_gemm_t(const P& ap, const T* W, int ldw, OutT* C, int ldc, cons
             return;
           case 25: launch_gemm_pp<T, OutT, 8, 256, 192, 2, 2, 4, 32>(static_cast<const T*>(ap.A), ap.lda, W, ldw, C,
                                                                       ldc, bias, R, ldr, M, N, K, alpha, act, s);
+            return;
+          case 26:
+          case 27:
+          case 28:
+            launch_gemm_v4_cfg(cfg, std::is_same<T, bf16>::value ? 0 : 1, ap.A, ap.lda, W, ldw, C, ldc, bias, R, ldr,
+                               M, N, K, alpha, act, s);
             return;
           default: break;
         }

@@ -38,7 +38,7 @@ def test_linear_plain(M, N, K, dtype):
     _close(y, ops.linear_ref(x, w), 2e-2, 2e-2)
 
 
-@pytest.mark.parametrize("cfg", list(range(26)))
+@pytest.mark.parametrize("cfg", list(range(29)))
 def test_linear_tile_configs_asymmetric(cfg):
     """A = I with an asymmetric W catches a transposed C-write (guide §3)."""
     ops = _ops()
@@ -557,7 +557,7 @@ def test_image_to_nhwc_and_gather():
 
 
 @pytest.mark.parametrize("N", [392, 388])   # 388 % 8 != 0: the direct (unstaged) epilogue
-@pytest.mark.parametrize("cfg", list(range(26)))
+@pytest.mark.parametrize("cfg", list(range(29)))
 def test_linear_all_tiles_random(cfg, N):
     ops = _ops()
     torch.manual_seed(11)
@@ -567,6 +567,29 @@ def test_linear_all_tiles_random(cfg, N):
     r = torch.randn(300, N, device="cuda", dtype=torch.bfloat16)
     _close(ops.linear(x, w, b, act="gelu", residual=r, tile_cfg=cfg),
            ops.linear_ref(x, w, b, act="gelu", residual=r), 3e-2, 2e-2)
+
+
+@pytest.mark.parametrize("cfg", [26, 27, 28])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_linear_v4_tiles(cfg, dtype):
+    """The 4-wave VGPR-staged tiles (gemm_v4.h, K % 64 == 0): ragged M / N edges,
+    every epilogue combination, both 16-bit dtypes, against the fp32 reference;
+    K % 64 != 0 falls back to an 8-wave tile (still correct)."""
+    ops = _ops()
+    torch.manual_seed(cfg)
+    for M, N, K in ((300, 392, 512), (4096, 768, 768), (129, 200, 3072), (256, 96, 128)):
+        x = torch.randn(M, K, device="cuda", dtype=dtype)
+        w = torch.randn(N, K, device="cuda", dtype=dtype) * K ** -0.5
+        b = torch.randn(N, device="cuda", dtype=dtype) * 0.1
+        r = torch.randn(M, N, device="cuda", dtype=dtype)
+        _close(ops.linear(x, w, tile_cfg=cfg), ops.linear_ref(x, w), 2e-2, 2e-2)
+        _close(ops.linear(x, w, b, act="gelu", tile_cfg=cfg), ops.linear_ref(x, w, b, act="gelu"), 2e-2, 2e-2)
+        _close(ops.linear(x, w, b, residual=r, tile_cfg=cfg), ops.linear_ref(x, w, b, residual=r), 2e-2, 2e-2)
+        _close(ops.linear(x, w, residual=r, act="relu", tile_cfg=cfg), ops.linear_ref(x, w, residual=r, act="relu"),
+               2e-2, 2e-2)
+    x = torch.randn(200, 520, device="cuda", dtype=dtype)
+    w = torch.randn(264, 520, device="cuda", dtype=dtype) * 0.05
+    _close(ops.linear(x, w, tile_cfg=cfg), ops.linear_ref(x, w), 2e-2, 2e-2)
 
 
 @pytest.mark.parametrize("cfg", [0, 8, 15, 19, 20, 21, 22, 24])
