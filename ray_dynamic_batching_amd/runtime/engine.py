@@ -125,7 +125,9 @@ class EngineRunner:
 
     def warm_device(self, seconds: float) -> int:
         """Replay the largest bucket's graphs of every session on the compute
-        streams for ``seconds``; returns the number of replays (before start())."""
+        streams for ``seconds``; returns the number of replays (before start()).
+        A model whose captured forward has side effects (state it updates per
+        call) opts out with ``warm_replay = False``."""
         if seconds <= 0:
             return 0
         streams = [torch.cuda.Stream(device=self.device) for _ in range(self.compute_streams)]
@@ -136,7 +138,7 @@ class EngineRunner:
             for st in streams:
                 st.wait_stream(cur)
             for s in self.sessions:
-                if not s.graphs:
+                if not s.graphs or not getattr(s.model, "warm_replay", True):
                     continue
                 for slot, g in enumerate(s.graphs[-1]):
                     with torch.cuda.stream(streams[slot % self.compute_streams]):
