@@ -147,6 +147,8 @@ class EngineRunner:
             for st in streams:
                 cur.wait_stream(st)
             torch.cuda.synchronize(self.device)
+            if n == 0:          # nothing to replay (no graphs, or every model opted out)
+                break
         return n
 
     def _capture(self, s: SessionSpec, live: bool) -> None:
