@@ -35,6 +35,8 @@ def main(argv=None):
     ap.add_argument("--pipeline-depth", type=int, default=4)
     ap.add_argument("--compute-streams", type=int, default=2, help="batches executing concurrently on the GPU")
     ap.add_argument("--json-out", default="")
+    ap.add_argument("--stamps-out", default="", help="diagnostic: block-stamp records of the closed-loop run (.npy; needs "
+                    "the RDB_BLOCK_STAMPS kernel build via RDB_OPS_SO, bench/stamp_timeline.py reads them)")
     a = ap.parse_args(argv)
 
     import numpy as np
@@ -78,7 +80,20 @@ def main(argv=None):
             j.reset_stats()
             if kind == "closed":
                 total = int(max(2000, 20000 * a.seconds / 5))
+                stamps = None
+                if a.stamps_out:
+                    from ray_dynamic_batching_amd import ops as _ops_mod
+
+                    stamps = _ops_mod.BlockStamps()
+                    total = min(total, 4096)          # ~30k records per batch: stay inside the stamp buffer
+                    torch.cuda.synchronize()
+                    stamps.reset()
                 res = lg.run(total, int(v), 0.0, 0.0, True, 600.0)
+                if stamps is not None:
+                    torch.cuda.synchronize()
+                    np.save(a.stamps_out, stamps.read())
+                    print(json.dumps({"stamps": a.stamps_out, "dropped": stamps.dropped}), flush=True)
+                    stamps.close()
             else:
                 total = int(v * a.seconds)
                 res = lg.run(total, 0, v, 0.0, True, 600.0)
