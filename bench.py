@@ -158,7 +158,10 @@ def main():
     from ray_dynamic_batching_amd.runtime import numa
 
     rank_gpus = [0] * world if (args.rehearse_one_gpu or world == 1) else list(range(world))
-    placement = dict(rank=rank, gpu=rank_gpus[rank], **numa.place_rank(rank, rank_gpus))
+    try:
+        placement = dict(rank=rank, gpu=rank_gpus[rank], **numa.place_rank(rank, rank_gpus))
+    except Exception as e:  # noqa: BLE001 -- placement is an optimisation: never fail the bench on it
+        placement = dict(rank=rank, gpu=rank_gpus[rank], numa_node=-1, cpus="", pinned=False, error=str(e)[:200])
     import torch
     import torch.distributed as dist
 
