@@ -134,7 +134,23 @@ gemm_pp_kernel(const T* __restrict__ A, int lda, const T* __restrict__ W, int ld
 
   const int tiles_n = (N + BN - 1) / BN, tiles_m = (M + BM - 1) / BM;
   const int t = xcd_remap(blockIdx.x, tiles_m * tiles_n);
-  const int tile_m = t / tiles_n, tile_n = t - tile_m * tiles_n;
+  // Wide grids (>= 12 tile columns) walk their tiles in groups of 4 tile rows,
+  // column-major inside a group: an XCD's contiguous chunk of tiles is then a
+  // 4 x (chunk / 4) block, so its L2 holds fewer distinct A and W panels
+  // (profiles/gemm_lab_r5_group.txt: FFN-up -2..3 %, 4096^3 -3 %; narrow grids
+  // such as N = 768 keep the row-major walk)
+  int tile_m, tile_n;
+  if (tiles_n >= 12 && tiles_m >= 8) {
+    const int gsize = 4 * tiles_n;
+    const int g = t / gsize, first = 4 * g;
+    const int gm = tiles_m - first < 4 ? tiles_m - first : 4;
+    const int r = t - g * gsize;
+    tile_m = first + r % gm;
+    tile_n = r / gm;
+  } else {
+    tile_m = t / tiles_n;
+    tile_n = t - tile_m * tiles_n;
+  }
   const int m0 = tile_m * BM, n0 = tile_n * BN;
 
   // ---- DMA addressing (wave wid_u owns A pieces [wid*A_PW, ...) and W pieces [wid*W_PW, ...)) ----
