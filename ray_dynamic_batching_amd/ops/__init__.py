@@ -51,8 +51,9 @@ def _aligned(t: torch.Tensor, n: int = 16) -> bool:
 # while a hipGraph is being captured (those calls use the cached choice, or the
 # on-device heuristic if the shape was never seen eagerly).
 # ---------------------------------------------------------------------------
-NUM_TILE_CFGS = 29   # gemm_core.h kTileBM/BN: 0..12 4-wave (GEMM and conv), 13..18 8-wave, 19..25 ping-pong,
-                     # 26..28 4-wave VGPR-staged one-block-per-CU tiles (gemm_v4.h; GEMM only, K % 64 == 0)
+NUM_TILE_CFGS = 30   # gemm_core.h kTileBM/BN: 0..12 4-wave (GEMM and conv), 13..18 8-wave, 19..25 ping-pong,
+                     # 26..28 4-wave VGPR-staged one-block-per-CU tiles (gemm_v4.h; GEMM only, K % 64 == 0),
+                     # 29 ping-pong 256x224 (the Llama gate-up N = 28672 = 128 x 224)
 NUM_LN_TILE_CFGS = 19  # the deferred-LayerNorm epilogues run on tiles 0..18
 NUM_CONV_TILE_CFGS = 13
 FORCE_TILED = 99      # tile_cfg value that bypasses the skinny-M GEMM (M <= 64)
@@ -132,10 +133,10 @@ def tune_in_context(time_forward: Callable[[], float], keys: Optional[list] = No
 
 # gemm_core.h kTileBM / kTileBN / kTileNW and tile_blocks_per_cu (CU-time estimates of the tuner)
 _ALL_BM = (128, 64, 128, 64, 128, 192, 256, 128, 128, 64, 128, 256, 128, 256, 128, 256, 256, 128, 256, 256, 256, 128,
-           256, 256, 256, 256, 128, 128, 256)
+           256, 256, 256, 256, 128, 128, 256, 256)
 _ALL_BN = (128, 128, 64, 64, 192, 128, 128, 256, 144, 96, 96, 144, 48, 128, 256, 192, 144, 96, 96, 128, 144, 256, 256,
-           128, 192, 192, 96, 128, 192)
-_ALL_NW = (4,) * 13 + (8,) * 13 + (4,) * 3
+           128, 192, 192, 96, 128, 192, 224)
+_ALL_NW = (4,) * 13 + (8,) * 13 + (4,) * 3 + (8,)
 
 
 def _blocks_per_cu(t: int) -> int:
@@ -249,7 +250,7 @@ def _tuned_cfg(key: tuple, launch: Callable[[int], None], candidates=range(NUM_T
 # ---------------------------------------------------------------------------
 # GEMM (+ fused bias / activation / residual epilogue)
 # ---------------------------------------------------------------------------
-_NUM_SWIGLU_TILE_CFGS = 26   # the VGPR-staged tiles (26..28) have no SwiGLU epilogue
+_SWIGLU_TILE_CFGS = tuple(range(26)) + (29,)   # the VGPR-staged tiles (26..28) have no SwiGLU epilogue
 
 
 def _gemm_candidates(M: int, N: int, K: int, splitk: bool = False):
@@ -259,7 +260,7 @@ def _gemm_candidates(M: int, N: int, K: int, splitk: bool = False):
     tiles 19 / 21 where the tile grid leaves CUs idle and each split keeps >= 8 K
     steps (long-K GEMMs of small M: the Llama prefill's down projection at 128
     tokens is 128 blocks x 224 K steps; at 1024 tokens 128 ping-pong tiles)."""
-    cands = [c for c in range(NUM_TILE_CFGS) if c < 26 or K % 64 == 0]   # VGPR-staged tiles: K % 64 == 0
+    cands = [c for c in range(NUM_TILE_CFGS) if not 26 <= c <= 28 or K % 64 == 0]   # VGPR-staged tiles: K % 64 == 0
     if _GEMM_DEEP and K >= 256:
         cands += [c | DEEP for c in _DEEP_TILES
                   if c in _DEEP_BIG or -(-M // _TILE_BM[c]) * -(-N // _TILE_BN[c]) <= _DEEP_MAX_BLOCKS]
@@ -343,7 +344,7 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
                     ws = _tune_ws[sid] = splitk_workspace(x.device)
             launch(c, ws)
         tile_cfg = _tuned_cfg(key, tune_launch,
-                              _gemm_candidates(M, N, K, splitk=True) if act != "swiglu" else range(_NUM_SWIGLU_TILE_CFGS))
+                              _gemm_candidates(M, N, K, splitk=True) if act != "swiglu" else _SWIGLU_TILE_CFGS)
     launch(int(tile_cfg), workspace)
     return out
 

@@ -1251,15 +1251,18 @@ namespace rdb {
 // leaves 1.5 blocks per CU, at 1/110 operand bytes per FLOP vs 1/85 for 256x128.
 // 26 / 27 / 28 = the 4-wave VGPR-staged tiles of gemm_v4.h (128x96, 128x128,
 // 256x192; one block per CU; own translation unit gemm_v4.hip, K % 64 == 0).
-constexpr int kNumTiles = 29;
+// 29 = ping-pong 256x224 at BK = 32, 4 stages (123 KiB): the Llama-3-8B SwiGLU
+// gate-up projection (N = 28672 = 128 x 224) at 1024 / 512 tokens is exactly
+// 2 / 1 rounds of 256 blocks, where 256x256 leaves the last round 3/4 / 7/8 full.
+constexpr int kNumTiles = 30;
 //                                 0    1    2    3    4    5    6    7    8    9   10   11   12 | 8-wave: 13   14   15   16   17   18 | pp: 19   20   21   22   23   24   25
-constexpr int kTileBM[kNumTiles] = {128, 64, 128, 64, 128, 192, 256, 128, 128, 64, 128, 256, 128, 256, 128, 256, 256, 128, 256, 256, 256, 128, 256, 256, 256, 256, 128, 128, 256};
-constexpr int kTileBN[kNumTiles] = {128, 128, 64, 64, 192, 128, 128, 256, 144, 96, 96, 144, 48, 128, 256, 192, 144, 96, 96, 128, 144, 256, 256, 128, 192, 192, 96, 128, 192};
+constexpr int kTileBM[kNumTiles] = {128, 64, 128, 64, 128, 192, 256, 128, 128, 64, 128, 256, 128, 256, 128, 256, 256, 128, 256, 256, 256, 128, 256, 256, 256, 256, 128, 128, 256, 256};
+constexpr int kTileBN[kNumTiles] = {128, 128, 64, 64, 192, 128, 128, 256, 144, 96, 96, 144, 48, 128, 256, 192, 144, 96, 96, 128, 144, 256, 256, 128, 192, 192, 96, 128, 192, 224};
 // tile cfg flag: the DEEP (one block per CU, up to 8 LDS stages) variant of
 // 4-wave tiles 0, 1, 2, 3, 6, 7, 9, 10 (plain epilogues); other tiles ignore it
 constexpr int kDeepFlag = 1 << 12;
-constexpr int kTileWGM[kNumTiles] = {2, 2, 2, 2, 2, 2, 2, 2, 4, 2, 2, 4, 4, 4, 2, 4, 8, 4, 8, 4, 8, 2, 4, 4, 4, 4, 2, 2, 2};
-constexpr int kTileNW[kNumTiles] = {4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 8, 8, 8, 8, 8, 8, 8, 8, 8, 8, 8, 8, 8, 4, 4, 4};
+constexpr int kTileWGM[kNumTiles] = {2, 2, 2, 2, 2, 2, 2, 2, 4, 2, 2, 4, 4, 4, 2, 4, 8, 4, 8, 4, 8, 2, 4, 4, 4, 4, 2, 2, 2, 4};
+constexpr int kTileNW[kNumTiles] = {4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 8, 8, 8, 8, 8, 8, 8, 8, 8, 8, 8, 8, 8, 4, 4, 4, 8};
 
 // gemm_v4.hip (tile cfgs 26..28): dtype 0 = bf16, 1 = f16; 16-bit output, plain epilogues
 void launch_gemm_v4_cfg(int cfg, int dtype, const void* A, int lda, const void* W, int ldw, void* C, int ldc,
@@ -1372,7 +1375,8 @@ void launch_mfma_gemm_t(const P& ap, const T* W, int ldw, OutT* C, int ldc, cons
   } else {
     // the ping-pong tiles (19..) take plain staged epilogues only: deferred-LN modes,
     // SwiGLU and unaligned / N % 8 != 0 outputs run the 8-wave 256x192 tile instead
-    if (cfg >= 19 && (EPI != 0 || !gemm_pp_ok(N, ldc, ldr, C, bias, R, act) || (cfg >= 26 && K % 64 != 0))) {
+    if (cfg >= 19 && (EPI != 0 || !gemm_pp_ok(N, ldc, ldr, C, bias, R, act) ||
+                      (cfg >= 26 && cfg <= 28 && (K % 64 != 0 || act == ACT_SWIGLU)))) {
       cfg = 15;
       if (EPI == 0 && ln.sk_kper > 0) {   // split-K was requested for the pp tile: the 8-wave fallback runs unsplit
         launch_mfma_gemm_t<T, OutT, LoaderT, HB, HR, EPI>(ap, W, ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act, s, 15,
@@ -1460,6 +1464,9 @@ void launch_mfma_gemm_t(const P& ap, const T* W, int ldw, OutT* C, int ldc, cons
                                                                       ldc, bias, R, ldr, M, N, K, alpha, act, s);
             return;
           case 25: launch_gemm_pp<T, OutT, 8, 256, 192, 2, 2, 4, 32>(static_cast<const T*>(ap.A), ap.lda, W, ldw, C,
+                                                                      ldc, bias, R, ldr, M, N, K, alpha, act, s);
+            return;
+          case 29: launch_gemm_pp<T, OutT, 8, 256, 224, 2, 2, 4, 32>(static_cast<const T*>(ap.A), ap.lda, W, ldw, C,
                                                                       ldc, bias, R, ldr, M, N, K, alpha, act, s);
             return;
           case 26:

@@ -38,7 +38,7 @@ def test_linear_plain(M, N, K, dtype):
     _close(y, ops.linear_ref(x, w), 2e-2, 2e-2)
 
 
-@pytest.mark.parametrize("cfg", list(range(29)))
+@pytest.mark.parametrize("cfg", list(range(30)))
 def test_linear_tile_configs_asymmetric(cfg):
     """A = I with an asymmetric W catches a transposed C-write (guide §3)."""
     ops = _ops()
@@ -557,7 +557,7 @@ def test_image_to_nhwc_and_gather():
 
 
 @pytest.mark.parametrize("N", [392, 388])   # 388 % 8 != 0: the direct (unstaged) epilogue
-@pytest.mark.parametrize("cfg", list(range(29)))
+@pytest.mark.parametrize("cfg", list(range(30)))
 def test_linear_all_tiles_random(cfg, N):
     ops = _ops()
     torch.manual_seed(11)
@@ -592,7 +592,7 @@ def test_linear_v4_tiles(cfg, dtype):
     _close(ops.linear(x, w, tile_cfg=cfg), ops.linear_ref(x, w), 2e-2, 2e-2)
 
 
-@pytest.mark.parametrize("cfg", [0, 8, 15, 19, 20, 21, 22, 24])
+@pytest.mark.parametrize("cfg", [0, 8, 15, 19, 20, 21, 22, 24, 29])
 def test_linear_swiglu_and_f16_tiles(cfg):
     """SwiGLU pairing epilogue and f16 on the 8-wave and ping-pong tiles."""
     ops = _ops()
