@@ -179,6 +179,14 @@ class Engine {
     fault_delay_batch_us_ = knob("RDB_FAULT_DELAY_BATCH_US");
     fault_kill_after_ = knob("RDB_FAULT_KILL_AFTER_BATCHES");
     idle_dispatch_.store(knob("RDB_IDLE_DISPATCH") != 0);
+    // RDB_ENGINE_STAGGER_US (opt-in, A/B knob): when a batch is about to start on an
+    // idle compute stream less than this long after another stream started from idle,
+    // hold it back to that offset -- two streams that start together stay in lockstep
+    // (same kernel types at the same time: profiles/stamp_timeline_r5.json), staggered
+    // ones pair different kernels
+    stagger_ns_ = knob("RDB_ENGINE_STAGGER_US") * 1000;
+    stream_running_.reset(new std::atomic<int>[compute_streams_.size()]);
+    for (size_t i = 0; i < compute_streams_.size(); ++i) stream_running_[i].store(0);
     for (int s = 0; s < depth_; ++s) {
       hipEvent_t a, b, c;
       ENG_CHECK(hipEventCreateWithFlags(&a, hipEventDisableTiming));
@@ -704,7 +712,17 @@ class Engine {
               ENG_CHECK(hipMemsetAsync(reinterpret_cast<char*>(in) + (size_t)n * s.in_row_bytes, 0,
                                        (size_t)(rows - n) * s.in_row_bytes, copy_stream_));
           }
-          hipStream_t cs = compute_streams_[slot % compute_streams_.size()];
+          const int si = slot % (int)compute_streams_.size();
+          hipStream_t cs = compute_streams_[si];
+          if (stagger_ns_ > 0 && compute_streams_.size() > 1 && stream_running_[si].load(std::memory_order_acquire) == 0) {
+            // this stream starts from idle: keep it stagger_ns_ behind the last idle-start of another stream
+            const int64_t t_other = last_idle_start_ns_.load(std::memory_order_acquire);
+            const int64_t wait = t_other + stagger_ns_ - now_ns();
+            if (last_idle_stream_.load(std::memory_order_acquire) != si && wait > 0)
+              std::this_thread::sleep_for(std::chrono::nanoseconds(std::min<int64_t>(wait, stagger_ns_)));
+            last_idle_start_ns_.store(now_ns(), std::memory_order_release);
+            last_idle_stream_.store(si, std::memory_order_release);
+          }
           ENG_CHECK(hipEventRecord(ev_copy_[slot], copy_stream_));
           ENG_CHECK(hipStreamWaitEvent(cs, ev_copy_[slot], 0));
           ENG_CHECK(hipEventRecord(ev_start_[slot], cs));
@@ -726,6 +744,7 @@ class Engine {
             f.seq = launch_seq_.fetch_add(1, std::memory_order_acq_rel) + 1;
             ++gpu_inflight_;
             gpu_running_.fetch_add(1, std::memory_order_acq_rel);
+            stream_running_[slot % compute_streams_.size()].fetch_add(1, std::memory_order_acq_rel);
           }
           inflight_.push_back(std::move(f));
         }
@@ -764,6 +783,7 @@ class Engine {
             std::this_thread::yield();
           }
           gpu_running_.fetch_sub(1, std::memory_order_acq_rel);
+          stream_running_[f.slot % compute_streams_.size()].fetch_sub(1, std::memory_order_acq_rel);
           const int64_t t_obs = now_ns();
           roctxRangePushA("rdb:complete");
           float ms = 0.f;
@@ -858,6 +878,10 @@ class Engine {
   std::deque<InFlight> inflight_;
   int gpu_inflight_ = 0;                   // GPU batches launched and not yet completed (under mu_)
   std::atomic<int> gpu_running_{0};        // GPU batches whose done-event has not fired yet
+  std::unique_ptr<std::atomic<int>[]> stream_running_;   // ... per compute stream
+  int64_t stagger_ns_ = 0;
+  std::atomic<int64_t> last_idle_start_ns_{0};
+  std::atomic<int> last_idle_stream_{-1};
   std::atomic<bool> idle_dispatch_{false}; // batch policy: dispatch partial batches onto an idle stream
   std::atomic<uint64_t> launch_seq_{0};    // GPU launches so far (solo detection)
   std::mutex mu_;
