@@ -49,6 +49,8 @@ def main(argv=None):
     ap.add_argument("--reps", type=int, default=5, help="timed graph replays per arm (median reported)")
     ap.add_argument("--cfg", type=int, default=-1, help="our tile config (default: shipped per shape)")
     ap.add_argument("--sweep", action="store_true", help="also time every tile config")
+    ap.add_argument("--splits", default="", help="with --sweep: also time these split-K counts (e.g. 2,3,4) on "
+                    "the split-capable tiles, with a caller workspace")
     a = ap.parse_args(argv)
     import torch
     import torch.nn.functional as F
@@ -111,6 +113,14 @@ def main(argv=None):
                         sw[c] = round(timed(lambda: ops.linear(x, w, b, act=act, residual=r, tile_cfg=c)), 2)
                     except Exception as ex:  # tile not valid for this epilogue
                         sw[c] = str(ex)[:40]
+                if a.splits:
+                    # the split-K choices the tuner would consider (workspace-bounded)
+                    ws = ops.splitk_workspace(x.device)
+                    want = {int(v) for v in a.splits.split(",") if v}
+                    for c in ops._gemm_candidates(m, n, k, splitk=True):
+                        if ops.splits_of(c) in want and not c & ops.DEEP:
+                            sw[f"{c & 255}|{ops.splits_of(c)}"] = round(timed(
+                                lambda: ops.linear(x, w, b, act=act, residual=r, tile_cfg=c, workspace=ws)), 2)
                 row["ours_sweep_us"] = sw
         out[name] = row
         print(json.dumps({name: row}), flush=True)
