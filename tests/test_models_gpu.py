@@ -199,7 +199,12 @@ def _serve_all(c, rjob, q, payloads):
     return got
 
 
-def test_engine_concurrent_streams_match_single_stream():
+@pytest.mark.parametrize("stagger_us", [0, 300])
+def test_engine_concurrent_streams_match_single_stream(stagger_us, monkeypatch):
+    """Two compute streams serve the same outputs as the model; with the opt-in
+    stream stagger (RDB_ENGINE_STAGGER_US, read when the engine is built) too."""
+    if stagger_us:
+        monkeypatch.setenv("RDB_ENGINE_STAGGER_US", str(stagger_us))
     from ray_dynamic_batching_amd.models.bert import BertConfig, BertForSequenceClassification
     from ray_dynamic_batching_amd.runtime import job as rjob
     from ray_dynamic_batching_amd.runtime.engine import EngineRunner, SessionSpec
