@@ -74,7 +74,7 @@ Variant core1(const char* nm) {
                                                                                1.f, ACT_NONE, s);
           }};
 }
-#if !defined(LAB_SET_GELU) && !defined(LAB_SET_FFN2)   // the whole tile table: minutes of compile time
+#if !defined(LAB_SET_GELU) && !defined(LAB_SET_FFN2) && !defined(LAB_FAST)   // the whole tile table: minutes of compile time
 Variant core(int cfg) {
   char nm[64];
   snprintf(nm, sizeof nm, "core cfg%d %dx%d/%dw", cfg, kTileBM[cfg], kTileBN[cfg], 4 * kTileNW[cfg] / 4);
