@@ -35,6 +35,16 @@
 // Included by gemm_core.h (after the shared helpers, before the tile table);
 // not meant to be included on its own.
 
+// RDB_PP_LATE_PCT (A/B builds): share of a wave's DMA pieces per K-tile issued in
+// the matrix interval; -1: half on the BK 64 tiles, none on the BK 32 ones.
+// Default 0: the lab gain on the BK 64 tiles (-4..6 % alone, -2.5..4 % on two
+// streams) did not carry into the engines -- BERT 34.77k +- 0.40 vs 34.93k +- 0.20,
+// ResNet-50 tie, Llama-3-8B prefill +3 % (profiles/gemm_lab_r5_late_dma.txt,
+// profiles/ab_r5_late_dma.json)
+#ifndef RDB_PP_LATE_PCT
+#define RDB_PP_LATE_PCT 0
+#endif
+
 namespace rdb {
 
 #ifdef RDB_PP_STAMPS
@@ -192,6 +202,38 @@ gemm_pp_kernel(const T* __restrict__ A, int lda, const T* __restrict__ W, int ld
     const int piece = wid_u * G::W_PW + i;
     return base + (piece < G::W_PIECES ? G::W_OFF + piece * 1024 : G::DUMMY_OFF);
   };
+  // one DMA piece p of a K-tile (p < A_PW: A pieces, then W pieces); stage_rng
+  // issues pieces [p0, p1) (compile-time bounds after inlining)
+  auto stage_rng = [&](int buf, int k0, int p0, int p1) {
+    char* base = smem + buf * G::STAGE_BYTES;
+    if constexpr (CONV) {
+      const int tap = k0 / cv.C, c0 = k0 - tap * cv.C;
+      const int ur = tap / cv.S, us = tap - ur * cv.S;
+      const int uoff = (ur * cv.W + us) * cv.C + c0;
+#pragma unroll
+      for (int i = 0; i < G::A_PW; ++i) {
+        if (i < p0 || i >= p1) continue;
+        const int h = ah[i] + ur, w = aw[i] + us;
+        const bool ok = k0 < K && (unsigned)h < (unsigned)cv.H && (unsigned)w < (unsigned)cv.W;
+        dma16(asrc, base + (wid_u * G::A_PW + i) * 1024,
+              ok ? (uint32_t)(((int)aoff[i] + uoff) * (int)sizeof(T)) : kOOB);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < G::A_PW; ++i) {
+        if (i < p0 || i >= p1) continue;
+        const int gk = k0 + ach[i] * 8;
+        dma16(asrc, base + (wid_u * G::A_PW + i) * 1024,
+              (gk < K && aoff[i] != kOOB) ? aoff[i] + (uint32_t)(gk * sizeof(T)) : kOOB);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < G::W_PW; ++i) {
+      if (G::A_PW + i < p0 || G::A_PW + i >= p1) continue;
+      const int gk = k0 + wch[i] * 8;
+      dma16(wsrc, wdst(base, i), (gk < K && woff[i] != kOOB) ? woff[i] + (uint32_t)(gk * sizeof(T)) : kOOB);
+    }
+  };
   auto stage = [&](int buf, int k0) {
     char* base = smem + buf * G::STAGE_BYTES;
     if constexpr (CONV) {
@@ -243,13 +285,33 @@ gemm_pp_kernel(const T* __restrict__ A, int lda, const T* __restrict__ W, int ld
       for (int j = 0; j < TM; ++j) af[ks][j] = *reinterpret_cast<const frag*>(sa + G::off(arow0 + j * 16, chunk));
     }
   };
-  auto mfma_tile = [&]() {
+  // Late DMA pieces (RDB_PP_LATE_PCT % of a wave's L pieces per K-tile): issued
+  // by the MATRIX interval, spread between its MFMAs, instead of the read
+  // interval.  An LDS-DMA issue holds its wave for ~60 cycles among bare MFMAs
+  // but 100-185 inside a read burst (MI355X_MICROARCH.md, LDS-DMA piece issue
+  // cost), so a read interval carrying all L pieces outlasts the partner's
+  // MFMAs.  Hazards: the late pieces of tile kt+STAGES-1 go to the buffer of
+  // tile kt-1, whose last reader (group 1's read interval of kt-1) ended before
+  // this group's matrix interval of kt began (both groups); they are retired
+  // by the read interval of tile kt+STAGES-2 like the early ones (vmcnt counts
+  // them in issue order), one or more barriers before any read of that tile.
+  constexpr int NMF = KS * TN * TM;
+  constexpr int LPCT = RDB_PP_LATE_PCT >= 0 ? RDB_PP_LATE_PCT : (BK == 64 ? 50 : 0);
+  constexpr int LB = L * LPCT / 100 < L ? L * LPCT / 100 : L - 1;
+  constexpr int LGAP = NMF / (LB + 1);
+  auto mfma_tile = [&](bool late, int lbuf, int lk0) {
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
       for (int i = 0; i < TN; ++i)
 #pragma unroll
-        for (int j = 0; j < TM; ++j) acc[i][j] = MfmaOp<T>::mma(wf[ks][i], af[ks][j], acc[i][j]);
+        for (int j = 0; j < TM; ++j) {
+          acc[i][j] = MfmaOp<T>::mma(wf[ks][i], af[ks][j], acc[i][j]);
+          if constexpr (LB > 0) {
+            const int q = (ks * TN + i) * TM + j + 1;       // MFMAs issued so far
+            if (q % LGAP == 0 && q / LGAP <= LB && late) stage_rng(lbuf, lk0, L - LB + q / LGAP - 1, L - LB + q / LGAP);
+          }
+        }
   };
   // sched_barrier(0) pins the intervals: no MFMA may be hoisted into a read
   // interval (or LDS read sunk into a matrix interval) across a block barrier
@@ -261,7 +323,9 @@ gemm_pp_kernel(const T* __restrict__ A, int lda, const T* __restrict__ W, int ld
     __builtin_amdgcn_sched_barrier(0);
   };
   // s_waitcnt immediates (gfx9 encoding: vmcnt lo[3:0] hi[15:14], expcnt[6:4], lgkmcnt[11:8])
-  constexpr int kVmSteady = (((STAGES - 2) * L) & 15) | ((((STAGES - 2) * L) >> 4) << 14) | 0x70 | 0xF00;
+  constexpr int kVmPro = (((STAGES - 2) * L) & 15) | ((((STAGES - 2) * L) >> 4) << 14) | 0x70 | 0xF00;
+  // in the loop the late pieces of the newest tile are not issued yet when the read interval waits
+  constexpr int kVmSteady = (((STAGES - 2) * L - LB) & 15) | ((((STAGES - 2) * L - LB) >> 4) << 14) | 0x70 | 0xF00;
   constexpr int kVm0 = 0x70 | 0xF00;
   constexpr int kLgkm0 = 0xC07F;            // lgkmcnt(0), vmcnt and expcnt at max
 
@@ -294,7 +358,7 @@ gemm_pp_kernel(const T* __restrict__ A, int lda, const T* __restrict__ W, int ld
 #pragma unroll
   for (int s = 0; s < STAGES - 1; ++s)
     if (s < nk) stage(s, (kb + s) * BK);
-  if (nk >= STAGES - 1) __builtin_amdgcn_s_waitcnt(kVmSteady);
+  if (nk >= STAGES - 1) __builtin_amdgcn_s_waitcnt(kVmPro);
   else __builtin_amdgcn_s_waitcnt(kVm0);
   barrier();
 #ifdef RDB_PP_STAMPS
@@ -307,14 +371,15 @@ gemm_pp_kernel(const T* __restrict__ A, int lda, const T* __restrict__ W, int ld
     // ---- read interval: fragments of tile kt, DMA of tile kt+STAGES-1 ----
     read_tile(buf);
     const bool steady = kt + STAGES - 1 < nk;
-    if (steady) stage((kt + STAGES - 1) % STAGES, (kb + kt + STAGES - 1) * BK);
+    const int nbuf = (kt + STAGES - 1) % STAGES, nk0 = (kb + kt + STAGES - 1) * BK;
+    if (steady) stage_rng(nbuf, nk0, 0, L - LB);
     __builtin_amdgcn_s_waitcnt(kLgkm0);           // my reads of this buffer are done (WAR)
     if (steady) __builtin_amdgcn_s_waitcnt(kVmSteady);  // my pieces of tile kt+1 landed (RAW)
     else __builtin_amdgcn_s_waitcnt(kVm0);
     barrier();
-    // ---- matrix interval ----
+    // ---- matrix interval (+ the late DMA pieces of tile kt+STAGES-1) ----
     __builtin_amdgcn_s_setprio(1);
-    mfma_tile();
+    mfma_tile(steady, nbuf, nk0);
     __builtin_amdgcn_s_setprio(0);
     barrier();
     buf = buf == STAGES - 1 ? 0 : buf + 1;
