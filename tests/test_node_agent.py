@@ -157,8 +157,10 @@ def test_supervisor_heartbeat_loss_fails_pending_and_bumps_generation(tmp_path):
         got = []
         assert _wait(lambda: bool(got.extend(c.poll(8, 0.05)) or got), 20)
         assert got[0][0] == rid and got[0][1] == int(rjob.Status.REPLICA_DIED)
-        assert j.replica_generation(0) == 1
-        assert a.info(pid)["state"] == "BACKOFF"
+        # the agent fails the pending requests first, then bumps the generation and
+        # enters back-off (node_agent.cpp on_death_locked): the completion can win the race
+        assert _wait(lambda: j.replica_generation(0) == 1, 10)
+        assert _wait(lambda: a.info(pid)["state"] == "BACKOFF", 10)
         assert "missed heartbeats" in a.info(pid)["last_exit"]
     finally:
         a.shutdown(1.0)
