@@ -87,17 +87,6 @@ def parse():
     return ap.parse_args()
 
 
-def _tile_table(args) -> str:
-    if args.tile_table == "none" or args.backend != "hip":
-        return ""
-    if args.tile_table != "auto":
-        return args.tile_table
-    name = (f"mi355x_bert_L{args.layers}_S{args.seq}_B{args.max_batch}_"
-            f"cs{args.compute_streams}_d{args.pipeline_depth}.json")
-    p = os.path.join(os.path.dirname(os.path.abspath(__file__)), "ray_dynamic_batching_amd", "ops", "tuned", name)
-    return p if os.path.exists(p) else ""
-
-
 class _EchoRunner:
     """CPU stand-in for EngineRunner (native EchoServer fake replica)."""
 
@@ -240,19 +229,25 @@ def main():
         pool = ThreadPoolExecutor(G)
         slot = list(drivers).index(rank)
     os.environ.setdefault("RDB_TUNE_STREAMS", str(args.tune_streams or args.compute_streams))
-    tile_table = _tile_table(args)
-    if tile_table and "RDB_TUNE_FILE" not in os.environ:
-        # replay a tile table selected on MI355X (ops/tuned/README.md) instead of
-        # tuning at start-up: start-up tuning is timed on a few replays, so its
-        # picks -- and the served throughput -- vary run to run by up to ~10 %
-        os.environ["RDB_TUNE_FILE"] = tile_table
     if echo:
         runner = _EchoRunner(rjob.EchoServer(job, rank, [rank], args.max_batch, args.echo_service_us, 0.0, 8))
     else:
+        from ray_dynamic_batching_amd.runtime.engine import resolve_tile_table
+
         model = BertForSequenceClassification(cfg, device="cuda", backend=args.backend)
+        # replay the tile table selected on MI355X for this configuration
+        # (ops/tuned/README.md) instead of tuning at start-up: start-up tuning is
+        # timed on a few replays, so its picks -- and the served throughput --
+        # vary run to run by up to ~10 %.  The same resolution as a Serve-deployed
+        # replica's EngineConfig.tile_table="auto"; RDB_TUNE_FILE set by the caller wins.
+        tile_table = os.environ.get("RDB_TUNE_FILE") or resolve_tile_table(
+            args.tile_table, model, args.max_batch, args.compute_streams, args.pipeline_depth)
+        if tile_table:
+            os.environ["RDB_TUNE_FILE"] = tile_table
         spec = SessionSpec(model=model, queue=rank, max_batch=args.max_batch, max_wait_s=args.max_wait_ms / 1e3)
         runner = EngineRunner(name, rank, [spec], pipeline_depth=args.pipeline_depth,
-                              compute_streams=args.compute_streams, batch_policy=args.batch_policy).build()
+                              compute_streams=args.compute_streams, batch_policy=args.batch_policy,
+                              tile_table=tile_table).build()
     runner.start()
     if not echo and getattr(runner, "tuning_changes", None):
         print(json.dumps({"rank": rank, "in_context_tile_changes": {str(k[2:5]): v for k, v in runner.tuning_changes.items()}}),

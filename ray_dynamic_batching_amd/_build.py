@@ -8,7 +8,9 @@
                       CPU-only hosts.
 
 Both land next to this file so they travel with the repository snapshot.
-Usage: ``python -m ray_dynamic_batching_amd._build [--force] [--only ops|runtime]``.
+Usage: ``python -m ray_dynamic_batching_amd._build [--force] [--only ops|runtime]``;
+``--sanitize thread`` builds an instrumented runtime + Python launcher under
+``_variants/san-thread/`` (tests/test_sanitizers.py).
 """
 from __future__ import annotations
 
@@ -151,20 +153,61 @@ def build_ops(force: bool = False, jobs: int | None = None, verbose: bool = Fals
     return target
 
 
-def build_runtime(force: bool = False) -> Path:
-    target = runtime_target()
+def sanitizer_dir(san: str) -> Path:
+    """Where the sanitizer build of the host runtime and its launcher live:
+    ``_variants/san-<preset>/`` -- never the production extension's path."""
+    return PKG / "_variants" / ("san-" + san.replace(",", "-"))
+
+
+def build_runtime(force: bool = False, sanitize: str = "") -> Path:
+    """Build _rdb_runtime.  ``sanitize`` ("thread", "address,undefined", ...;
+    default from RDB_SANITIZE) builds an instrumented copy under
+    ``sanitizer_dir(preset)`` instead (load it with RDB_RUNTIME_SO; the
+    production ``_rdb_runtime`` is never replaced by a sanitizer build)."""
+    san = sanitize or os.environ.get("RDB_SANITIZE", "")
+    target = (sanitizer_dir(san) / f"_rdb_runtime{EXT}") if san else runtime_target()
     srcs = [RT_SRC / "runtime.cpp", RT_SRC / "node_agent.cpp"]
     if not force and not _stale(target, _deps(srcs, [RT_SRC])):
         return target
-    cxx = os.environ.get("CXX", "g++")
+    target.parent.mkdir(parents=True, exist_ok=True)
+    cxx = _san_cxx() if san else os.environ.get("CXX", "g++")
     tmp = target.with_suffix(".tmp.so")
-    san = os.environ.get("RDB_SANITIZE", "")  # "address" / "thread" / "undefined" (host-code presets)
     flags = ["-O1", "-g", "-fno-omit-frame-pointer", f"-fsanitize={san}"] if san else ["-O2"]
     _run([cxx] + flags + ["-std=c++17", "-fPIC", "-shared", "-Wall", "-Wno-unused-function",
           "-fvisibility=hidden", f"-I{RT_SRC}"] + _pybind_includes() + [str(s) for s in srcs]
          + ["-o", str(tmp), "-lrt", "-pthread"])
     os.replace(tmp, target)
     return target
+
+
+def _san_cxx() -> str:
+    """Compiler of the sanitizer builds: ROCm's clang++ (its compiler-rt links the
+    sanitizer runtime into the launcher only; the instrumented extension resolves
+    it from there -- with GCC 11's shared libtsan, any fork after dlopen-ing the
+    instrumented extension hung), else $CXX / g++."""
+    if os.environ.get("RDB_SAN_CXX"):
+        return os.environ["RDB_SAN_CXX"]
+    clang = Path(ROCM) / "lib" / "llvm" / "bin" / "clang++"
+    return str(clang) if clang.exists() else os.environ.get("CXX", "g++")
+
+
+def build_sanitized_python(san: str, force: bool = False) -> Path:
+    """A CPython launcher (Py_BytesMain) linked with -fsanitize=<san>, so the
+    sanitizer runtime is initialised before the interpreter and every
+    extension it loads -- how the Python test suites run against the
+    instrumented runtime (reference: the Bazel tsan / asan configs, .bazelrc)."""
+    out = sanitizer_dir(san) / "python"
+    src = RT_SRC / "tests" / "sanitized_python.cpp"
+    if not force and out.exists() and out.stat().st_mtime >= src.stat().st_mtime:
+        return out
+    out.parent.mkdir(parents=True, exist_ok=True)
+    inc = sysconfig.get_paths()["include"]
+    libdir = sysconfig.get_config_var("LIBDIR") or "/usr/lib/x86_64-linux-gnu"
+    ver = sysconfig.get_config_var("LDVERSION") or sysconfig.get_python_version()
+    _run([_san_cxx(), "-O1", "-g", "-fno-omit-frame-pointer", f"-fsanitize={san}", "-fPIE", "-pie",
+          f"-I{inc}", str(src), "-o", str(out), f"-L{libdir}", f"-lpython{ver}", f"-Wl,-rpath,{libdir}",
+          "-ldl", "-lm", "-pthread"])
+    return out
 
 
 def build_all(force: bool = False, verbose: bool = False) -> None:
@@ -179,7 +222,12 @@ def main(argv=None) -> int:
     ap.add_argument("-v", "--verbose", action="store_true")
     ap.add_argument("--variant", default="", help="A/B build name (kernels only), with -D defines")
     ap.add_argument("-D", dest="defines", action="append", default=[])
+    ap.add_argument("--sanitize", default="", help="host runtime only: build an instrumented copy + launcher under "
+                    "_variants/san-<preset>/ (e.g. thread, address,undefined)")
     a = ap.parse_args(argv)
+    if a.sanitize:
+        print("built", build_runtime(a.force, sanitize=a.sanitize), build_sanitized_python(a.sanitize, a.force))
+        return 0
     if a.variant:
         print("built", build_ops(a.force, verbose=a.verbose, variant=a.variant, defines=tuple(a.defines)))
         return 0

@@ -36,6 +36,8 @@ class ResNet50:
         self.device = torch.device(device)
         self.dtype = dtype
         self.backend = backend
+        # shipped MI355X tile table key (runtime.engine.shipped_tile_table): 224x224 fp16 only
+        self.tile_signature = "resnet50" if backend == "hip" and image_size == 224 and dtype == torch.float16 else None
         self.num_classes = num_classes
         self.image_size = image_size
         self.topk = topk

@@ -260,7 +260,10 @@ def _gemm_candidates(M: int, N: int, K: int, splitk: bool = False):
     tiles 19 / 21 where the tile grid leaves CUs idle and each split keeps >= 8 K
     steps (long-K GEMMs of small M: the Llama prefill's down projection at 128
     tokens is 128 blocks x 224 K steps; at 1024 tokens 128 ping-pong tiles)."""
-    cands = [c for c in range(NUM_TILE_CFGS) if not 26 <= c <= 28 or K % 64 == 0]   # VGPR-staged tiles: K % 64 == 0
+    # VGPR-staged tiles 26..28: K % 64 == 0, and only in the experimental build (they tied
+    # or lost every engine A/B, profiles/ab_r5_v4_bert.json)
+    v4 = K % 64 == 0 and _v4_tiles_built()
+    cands = [c for c in range(NUM_TILE_CFGS) if not 26 <= c <= 28 or v4]
     if _GEMM_DEEP and K >= 256:
         cands += [c | DEEP for c in _DEEP_TILES
                   if c in _DEEP_BIG or -(-M // _TILE_BM[c]) * -(-N // _TILE_BN[c]) <= _DEEP_MAX_BLOCKS]
@@ -1471,6 +1474,21 @@ def se_scale_ref(x, s):
 # -D RDB_BLOCK_STAMPS``, loaded with RDB_OPS_SO).  bench/stamp_timeline.py turns
 # the records into co-residency / CU-time of the UN-profiled serving bench.
 # ---------------------------------------------------------------------------
+_V4_BUILT = None
+
+
+def _v4_tiles_built() -> bool:
+    """The 4-wave VGPR-staged tiles (cfg 26..28) are part of the opt-in
+    RDB_EXPERIMENTAL_KERNELS build only."""
+    global _V4_BUILT
+    if _V4_BUILT is None:
+        try:
+            _V4_BUILT = experimental_kernels_built()
+        except Exception:  # noqa: BLE001 -- no kernel library (CPU host): not built
+            _V4_BUILT = False
+    return _V4_BUILT
+
+
 def experimental_kernels_built() -> bool:
     """Whether the loaded kernel library carries the opt-in variants that lost
     their A/Bs (stream-K, row-LayerNorm, LNOUT / staged-LN epilogues): built only

@@ -23,6 +23,20 @@
 //                     results into the clients' completion rings, releases the
 //                     request-ring slots and updates shm metrics.
 // No Python runs in steady state.
+//
+// Tensor-parallel replicas (one Engine per rank process, compute_streams = 1):
+//   leader (rank 0) : the loop above; after forming a batch it publishes
+//                     (session, bucket, slot, n) + the n request rows to the
+//                     group's broadcast ring (runtime/csrc/tp_bcast.h) before
+//                     launching, then completes the requests as usual;
+//   follower        : its launcher takes the records in order, copies the rows
+//                     into a pinned staging slot, H2D on the copy stream, replays
+//                     the SAME (session, bucket, slot) graph -- its RCCL / xGMI
+//                     all-reduces pair up with the other ranks' because every
+//                     rank launches the same graphs in the same order -- and its
+//                     completer only retires the slot (no requests, no replica
+//                     state: the group's replica slot belongs to rank 0).
+//   Batch k+1 is formed, broadcast and copied while batch k computes on every rank.
 #include <hip/hip_runtime.h>
 #include <rocprofiler-sdk-roctx/roctx.h>
 #include <pybind11/pybind11.h>
@@ -41,6 +55,7 @@
 #include <vector>
 
 #include "../../runtime/csrc/shm.h"
+#include "../../runtime/csrc/tp_bcast.h"
 
 namespace py = pybind11;
 using namespace rdb::rt;
@@ -134,6 +149,7 @@ struct InFlight {
   bool gpu = false;
   bool solo = false;     // no other GPU batch in flight when this one launched
   uint64_t seq = 0;      // launch sequence number (launch_seq_ after this launch)
+  int tp_n = 0;          // TP follower: requests in the leader's batch (stats only)
 };
 
 class Engine {
@@ -199,6 +215,7 @@ class Engine {
   }
   ~Engine() {
     stop();
+    for (auto p : tp_stage_) hipHostFree(p);
     for (auto e : ev_copy_) hipEventDestroy(e);
     for (auto e : ev_start_) hipEventDestroy(e);
     for (auto e : ev_done_) hipEventDestroy(e);
@@ -384,6 +401,9 @@ class Engine {
   }
   int compute_streams() const { return (int)compute_streams_.size(); }
   void set_idle_dispatch(bool on) { idle_dispatch_.store(on, std::memory_order_relaxed); }
+  // EngineConfig.stagger_us (the RDB_ENGINE_STAGGER_US knob, set before start())
+  void set_stagger_us(int64_t us) { stagger_ns_ = std::max<int64_t>(0, us) * 1000; }
+  int64_t stagger_us() const { return stagger_ns_ / 1000; }
   bool idle_dispatch() const { return idle_dispatch_.load(std::memory_order_relaxed); }
   void set_max_batch(int sid, int b) {
     Session& s = sess(sid);
@@ -403,28 +423,80 @@ class Engine {
             throw std::runtime_error("engine: missing graph/input for a (session, bucket, slot)");
     }
     running_ = true;
-    ReplicaState* rs = job_.replica(replica_);
-    rs->gpu.store(device_);
-    rs->pid.store((uint32_t)getpid());
-    rs->heartbeat_ns.store(now_ns());
-    rs->status.store(RS_READY, std::memory_order_release);
+    if (tp_role_ != TP_FOLLOWER) {   // a follower never touches the group's replica slot (rank 0 owns it)
+      ReplicaState* rs = job_.replica(replica_);
+      rs->gpu.store(device_);
+      rs->pid.store((uint32_t)getpid());
+      rs->heartbeat_ns.store(now_ns());
+      rs->status.store(RS_READY, std::memory_order_release);
+    }
     completer_ = std::thread([this] { completer_loop(); });
-    launcher_ = std::thread([this] { launcher_loop(); });
+    if (tp_role_ == TP_FOLLOWER) launcher_ = std::thread([this] { follower_loop(); });
+    else launcher_ = std::thread([this] { launcher_loop(); });
   }
   void stop() {
     if (!running_) return;
     running_ = false;
     for (int i = 0; i < n_sess_.load(); ++i) sess_ptr_[i].load()->ring.ring_bell();
     cv_.notify_all();
-    if (launcher_.joinable()) launcher_.join();
+    if (launcher_.joinable()) launcher_.join();   // a TP launcher re-checks running_ every 50 ms on the ring
+    if (bcast_) {
+      // leader (the ring's only writer, its launcher has exited): a STOP record
+      // for the followers (bounded wait), then close -- which also wakes anyone
+      // still blocked on the ring; a follower closing tells the leader the group broke
+      if (tp_role_ == TP_LEADER) bcast_->publish(BCAST_STOP, 0, 0, 0, 0, nullptr, 0, 200000000LL);
+      bcast_->close();
+    }
     {
       std::lock_guard<std::mutex> lk(mu_);
       stopping_completer_ = true;
     }
     cv_.notify_all();
     if (completer_.joinable()) completer_.join();
-    job_.replica(replica_)->status.store(RS_DRAINING);
+    if (tp_role_ != TP_FOLLOWER) job_.replica(replica_)->status.store(RS_DRAINING);
   }
+
+  // ---- tensor-parallel roles (see the header comment); set after the sessions
+  // and graphs are registered, before start() ----
+  // Leader: create the group's broadcast ring for `n_followers` readers; a slot
+  // holds one batch of the largest session's rows.
+  void set_tp_leader(const std::string& name, int n_followers, int n_slots) {
+    if (running_) throw std::runtime_error("set_tp_leader: engine already running");
+    if (compute_streams_.size() != 1) throw std::invalid_argument("a TP engine runs ONE compute stream (graph order)");
+    size_t cap = 0;
+    for (int i = 0; i < n_sess_.load(); ++i) {
+      Session& ss = *sess_ptr_[i].load();
+      cap = std::max(cap, (size_t)ss.max_batch * (size_t)ss.in_row_bytes);
+    }
+    bcast_.reset(new TPBcast());
+    bcast_->create(name, (uint32_t)n_followers, (uint32_t)std::max(2, n_slots), cap);
+    tp_role_ = TP_LEADER;
+  }
+  // Follower `reader` (rank - 1): attach to the leader's ring, allocate the
+  // pinned staging slots the records are copied into.
+  void set_tp_follower(const std::string& name, int reader, double attach_timeout_s) {
+    if (running_) throw std::runtime_error("set_tp_follower: engine already running");
+    if (compute_streams_.size() != 1) throw std::invalid_argument("a TP engine runs ONE compute stream (graph order)");
+    bcast_.reset(new TPBcast());
+    {
+      py::gil_scoped_release nogil;
+      bcast_->attach(name, (int64_t)(attach_timeout_s * 1e9));
+    }
+    if (reader < 0 || (uint32_t)reader >= bcast_->n_readers()) throw std::out_of_range("tp follower reader index");
+    tp_reader_ = (uint32_t)reader;
+    const size_t cap = bcast_->payload_capacity();
+    for (int sl = 0; sl < depth_; ++sl) {
+      void* p = nullptr;
+      ENG_CHECK(hipHostMalloc(&p, std::max<size_t>(cap, 64), hipHostMallocDefault));
+      tp_stage_.push_back(p);
+    }
+    tp_role_ = TP_FOLLOWER;
+  }
+  void unlink_tp() { if (bcast_) bcast_->unlink(); }
+  int tp_role() const { return tp_role_; }
+  // false once stopped, failed, or (TP follower) after the leader's STOP
+  bool running() const { return running_.load(); }
+  uint64_t tp_published() const { return bcast_ ? bcast_->head() : 0; }
   void heartbeat() { job_.replica(replica_)->heartbeat_ns.store(now_ns()); }
   std::string error() {
     std::lock_guard<std::mutex> lk(mu_);
@@ -643,6 +715,7 @@ class Engine {
         const int64_t flush_at = f.t_form_start + s.max_wait_ns;
         uint64_t* tbl = reinterpret_cast<uint64_t*>(s.host_tbl[slot]);
         int n = 0;
+        if (tp_role_ == TP_LEADER) tp_rows_.clear();
         while (n < s.max_batch) {
           SlotHeader* h = s.ring.peek(s.peek_pos);
           if (!h) {
@@ -682,8 +755,14 @@ class Engine {
             ++s.peek_pos;
             continue;
           }
+          if (h->kind != 0) {   // KIND_TENSOR only: a pickled call cannot be a model row
+            write_completion(h, s.queue, ST_ERROR, nullptr, 0, now_ns());
+            ++s.peek_pos;
+            continue;
+          }
           f.req_pos.push_back(s.peek_pos);
           char* payload = reinterpret_cast<char*>(h) + sizeof(SlotHeader);
+          if (tp_role_ == TP_LEADER) tp_rows_.push_back(payload);
           tbl[n++] = zero_copy_ ? reinterpret_cast<uint64_t>(dev_base_ + (payload - host_base_))
                                 : reinterpret_cast<uint64_t>(payload);
           ++s.peek_pos;
@@ -699,6 +778,26 @@ class Engine {
           const int rows = s.buckets[bi];
           f.bucket_idx = bi;
           f.gpu = true;
+          if (tp_role_ == TP_LEADER) {
+            // every follower replays the same (session, bucket, slot) graph on these rows
+            BcastRecord* r = nullptr;
+            while (running_ && !(r = bcast_->reserve(50000000LL)))
+              if (bcast_->closed()) throw std::runtime_error("tp broadcast ring closed (a follower rank is gone)");
+            if (!r) {   // stopping while the followers lag: the batch is abandoned with the engine
+              s.inflight.fetch_sub(1, std::memory_order_seq_cst);
+              roctxRangePop();
+              break;
+            }
+            r->kind = BCAST_BATCH;
+            r->a = sid;
+            r->b = bi;
+            r->c = slot;
+            r->n = (uint32_t)n;
+            r->len = (uint32_t)((size_t)n * s.in_row_bytes);
+            char* dst = bcast_->payload(r);
+            for (int i = 0; i < n; ++i) memcpy(dst + (size_t)i * s.in_row_bytes, tp_rows_[i], s.in_row_bytes);
+            bcast_->commit(r);
+          }
           const uintptr_t in = s.in_dev[slot];
           if (zero_copy_) {
             gather_rows(reinterpret_cast<uintptr_t>(tbl), n, rows, s.in_row_bytes, in,
@@ -759,6 +858,73 @@ class Engine {
     }
   }
 
+  // TP follower launcher: the leader's records, in order (see the header comment).
+  void follower_loop() {
+    try {
+      ENG_CHECK(hipSetDevice(device_));
+      while (running_) {
+        const BcastRecord* r = bcast_->take(tp_reader_, 20000000LL);
+        if (!r) {
+          if (bcast_->closed()) break;      // the leader stopped (or the group is going down)
+          continue;
+        }
+        if (r->kind == BCAST_STOP) {
+          bcast_->release(tp_reader_);
+          break;
+        }
+        const int sid = r->a, bi = r->b, slot = r->c, n = (int)r->n;
+        if (sid < 0 || sid >= n_sess_.load(std::memory_order_acquire) || slot < 0 || slot >= depth_)
+          throw std::runtime_error("tp follower: record names an unknown session / slot");
+        Session& s = *sess_ptr_[sid].load(std::memory_order_acquire);
+        if (bi < 0 || bi >= (int)s.buckets.size() || n < 1 || n > s.buckets[bi] ||
+            r->len != (uint32_t)((size_t)n * s.in_row_bytes))
+          throw std::runtime_error("tp follower: record does not match the session's buckets / row size");
+        {  // the slot's previous batch must be done before its input / staging are rewritten
+          std::unique_lock<std::mutex> lk(mu_);
+          cv_.wait(lk, [&] { return !slot_busy_[slot] || !running_; });
+          if (!running_) break;
+        }
+        s.inflight.fetch_add(1, std::memory_order_seq_cst);
+        InFlight f;
+        f.session = sid;
+        f.slot = slot;
+        f.bucket_idx = bi;
+        f.gpu = true;
+        f.tp_n = n;
+        f.t_form_start = now_ns();
+        memcpy(tp_stage_[slot], reinterpret_cast<const char*>(r) + sizeof(BcastRecord), r->len);
+        bcast_->release(tp_reader_);
+        const int rows = s.buckets[bi];
+        const uintptr_t in = s.in_dev[slot];
+        ENG_CHECK(hipMemcpyAsync(reinterpret_cast<void*>(in), tp_stage_[slot], (size_t)n * s.in_row_bytes,
+                                 hipMemcpyHostToDevice, copy_stream_));
+        if (rows > n)
+          ENG_CHECK(hipMemsetAsync(reinterpret_cast<char*>(in) + (size_t)n * s.in_row_bytes, 0,
+                                   (size_t)(rows - n) * s.in_row_bytes, copy_stream_));
+        hipStream_t cs = compute_streams_[0];
+        ENG_CHECK(hipEventRecord(ev_copy_[slot], copy_stream_));
+        ENG_CHECK(hipStreamWaitEvent(cs, ev_copy_[slot], 0));
+        ENG_CHECK(hipEventRecord(ev_start_[slot], cs));
+        ENG_CHECK(hipGraphLaunch(s.graphs[bi][slot], cs));
+        ENG_CHECK(hipEventRecord(ev_done_[slot], cs));
+        f.t_launch = now_ns();
+        {
+          std::lock_guard<std::mutex> lk(mu_);
+          slot_busy_[slot] = true;
+          ++gpu_inflight_;
+          gpu_running_.fetch_add(1, std::memory_order_acq_rel);
+          stream_running_[0].fetch_add(1, std::memory_order_acq_rel);
+          inflight_.push_back(std::move(f));
+        }
+        cv_.notify_all();
+      }
+    } catch (const std::exception& e) {
+      set_error(std::string("tp follower: ") + e.what());
+    }
+    running_ = false;
+    cv_.notify_all();
+  }
+
   void completer_loop() {
     try {
       ENG_CHECK(hipSetDevice(device_));
@@ -774,6 +940,27 @@ class Engine {
         }
         Session& s = *sess_ptr_[f.session].load(std::memory_order_acquire);
         const int n = (int)f.req_pos.size();
+        if (f.gpu && tp_role_ == TP_FOLLOWER) {
+          // a follower's batch: its requests belong to rank 0; only the slot is retired
+          for (;;) {
+            hipError_t q = hipEventQuery(ev_done_[f.slot]);
+            if (q == hipSuccess) break;
+            if (q != hipErrorNotReady) ENG_CHECK(q);
+            std::this_thread::yield();
+          }
+          gpu_running_.fetch_sub(1, std::memory_order_acq_rel);
+          stream_running_[0].fetch_sub(1, std::memory_order_acq_rel);
+          batches_.fetch_add(1, std::memory_order_relaxed);
+          requests_.fetch_add(f.tp_n, std::memory_order_relaxed);
+          {
+            std::lock_guard<std::mutex> lk(mu_);
+            slot_busy_[f.slot] = false;
+            --gpu_inflight_;
+          }
+          s.inflight.fetch_sub(1, std::memory_order_seq_cst);
+          cv_.notify_all();
+          continue;
+        }
         if (f.gpu) {
           // low-latency wait: spin on the event, yielding
           for (;;) {
@@ -892,6 +1079,13 @@ class Engine {
   std::string error_;
   std::atomic<uint64_t> batches_{0}, requests_{0}, dropped_{0}, padded_{0}, cmp_dropped_{0};
   std::atomic<double> gpu_busy_ms_{0.0};
+  // tensor-parallel role (set_tp_leader / set_tp_follower)
+  enum { TP_NONE = 0, TP_LEADER = 1, TP_FOLLOWER = 2 };
+  int tp_role_ = TP_NONE;
+  std::unique_ptr<TPBcast> bcast_;
+  uint32_t tp_reader_ = 0;
+  std::vector<void*> tp_stage_;            // follower: pinned staging per pipeline slot
+  std::vector<const char*> tp_rows_;       // leader: host rows of the batch being formed
 };
 
 }  // namespace
@@ -925,6 +1119,15 @@ void register_engine(py::module_& m) {
       .def("num_sessions", &Engine::num_sessions)
       .def("compute_streams", &Engine::compute_streams)
       .def("set_idle_dispatch", &Engine::set_idle_dispatch)
+      .def("set_stagger_us", &Engine::set_stagger_us)
+      .def("set_tp_leader", &Engine::set_tp_leader, py::arg("name"), py::arg("n_followers"), py::arg("n_slots") = 8)
+      .def("set_tp_follower", &Engine::set_tp_follower, py::arg("name"), py::arg("reader"),
+           py::arg("attach_timeout_s") = 120.0)
+      .def("unlink_tp", &Engine::unlink_tp)
+      .def("tp_role", &Engine::tp_role)
+      .def("running", &Engine::running)
+      .def("tp_published", &Engine::tp_published)
+      .def("stagger_us", &Engine::stagger_us)
       .def("idle_dispatch", &Engine::idle_dispatch)
       .def("set_max_batch", &Engine::set_max_batch)
       .def("set_max_wait", &Engine::set_max_wait)

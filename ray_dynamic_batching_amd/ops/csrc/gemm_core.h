@@ -1375,8 +1375,9 @@ void launch_mfma_gemm_t(const P& ap, const T* W, int ldw, OutT* C, int ldc, cons
   } else {
     // the ping-pong tiles (19..) take plain staged epilogues only: deferred-LN modes,
     // SwiGLU and unaligned / N % 8 != 0 outputs run the 8-wave 256x192 tile instead
+    // (so do the VGPR-staged tiles 26..28 outside the experimental build)
     if (cfg >= 19 && (EPI != 0 || !gemm_pp_ok(N, ldc, ldr, C, bias, R, act) ||
-                      (cfg >= 26 && cfg <= 28 && (K % 64 != 0 || act == ACT_SWIGLU)))) {
+                      (cfg >= 26 && cfg <= 28 && (!RDB_EXPERIMENTAL || K % 64 != 0 || act == ACT_SWIGLU)))) {
       cfg = 15;
       if (EPI == 0 && ln.sk_kper > 0) {   // split-K was requested for the pp tile: the 8-wave fallback runs unsplit
         launch_mfma_gemm_t<T, OutT, LoaderT, HB, HR, EPI>(ap, W, ldw, C, ldc, bias, R, ldr, M, N, K, alpha, act, s, 15,

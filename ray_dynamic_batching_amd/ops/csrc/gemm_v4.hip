@@ -2,11 +2,18 @@
 // gemm_core.h (26 = 128 x 96, 27 = 128 x 128, 28 = 256 x 192), bf16 / f16 in and
 // out, bias / residual / activation epilogues.  Own translation unit: it is
 // compiled with VGPR-form MFMA accumulators (_build.py SRC_FLAGS).
+// Experimental build only (RDB_EXPERIMENTAL_KERNELS, common.h): the tiles tied the
+// shipped ping-pong choice in the two-stream BERT engine (profiles/ab_r5_v4_bert.json)
+// and no shipped table uses them, so the default library does not carry them.
 #include "gemm_core.h"
+#if RDB_EXPERIMENTAL
 #include "gemm_v4.h"
+#endif
 #include <stdexcept>
 
 namespace rdb {
+
+#if RDB_EXPERIMENTAL
 
 template <typename T>
 static void v4_dispatch(int cfg, const T* A, int lda, const T* W, int ldw, T* C, int ldc, const T* bias, const T* R,
@@ -32,5 +39,11 @@ void launch_gemm_v4_cfg(int cfg, int dtype, const void* A, int lda, const void* 
     v4_dispatch<f16>(cfg, static_cast<const f16*>(A), lda, static_cast<const f16*>(W), ldw, static_cast<f16*>(C), ldc,
                      static_cast<const f16*>(bias), static_cast<const f16*>(R), ldr, M, N, K, alpha, act, s);
 }
+#else
+void launch_gemm_v4_cfg(int, int, const void*, int, const void*, int, void*, int, const void*, const void*, int, int,
+                        int, int, float, int, hipStream_t) {
+  RDB_EXPERIMENTAL_MISSING("gemm_v4 tiles 26..28");
+}
+#endif
 
 }  // namespace rdb

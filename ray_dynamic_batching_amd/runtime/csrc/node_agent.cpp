@@ -23,6 +23,8 @@
 //                    (replaces the gRPC control plane, rpc/grpc_server.h:85).
 #include <fcntl.h>
 #include <poll.h>
+#include <pthread.h>
+#include <sched.h>
 #include <signal.h>
 #include <spawn.h>
 #include <sys/socket.h>
@@ -504,6 +506,13 @@ struct Proc {
   std::vector<uint32_t> queues;
   int group = 0;   // > 0: member of a gang-spawned process group (never restarts alone)
   int rank = -1;
+  // CPU set the process starts pinned to (NUMA placement: the CPUs local to its
+  // GPU, runtime/numa.py gpu_placement); every thread it starts inherits it
+  std::vector<int> cpus;
+  // SIGKILLed but not yet reaped: the monitor keeps calling waitpid on it and
+  // the process (or its gang) restarts only once it is gone, so a new replica
+  // never starts while the old one still holds its GPU memory
+  pid_t zombie = -1;
 };
 
 // A gang of processes that live and die together: one tensor-parallel replica
@@ -548,7 +557,7 @@ class NodeAgent {
   int spawn(const std::string& owner, std::vector<std::string> argv, py::dict env_over,
             const std::string& log_path, const std::string& job_name, int replica,
             std::vector<uint32_t> queues, double hb_timeout_s, int max_restarts,
-            double backoff_initial_s, double backoff_max_s) {
+            double backoff_initial_s, double backoff_max_s, std::vector<int> cpus) {
     if (argv.empty()) throw std::invalid_argument("spawn: empty argv");
     auto p = std::make_unique<Proc>();
     p->owner = owner;
@@ -572,6 +581,7 @@ class NodeAgent {
     p->max_restarts = max_restarts;
     p->backoff_initial_s = backoff_initial_s;
     p->backoff_max_s = backoff_max_s;
+    p->cpus = std::move(cpus);
     {
       std::lock_guard<std::mutex> lk(mu_);
       if (!job_name.empty()) p->job = attach_job(job_name);
@@ -588,10 +598,11 @@ class NodeAgent {
   int spawn_group(const std::string& owner, std::vector<std::vector<std::string>> argvs,
                   std::vector<py::dict> envs, std::vector<std::string> logs, const std::string& job_name,
                   int replica, std::vector<uint32_t> queues, double hb_timeout_s, int max_restarts,
-                  double backoff_initial_s, double backoff_max_s) {
+                  double backoff_initial_s, double backoff_max_s, std::vector<std::vector<int>> cpus) {
     const size_t n = argvs.size();
     if (n == 0) throw std::invalid_argument("spawn_group: no ranks");
     if (envs.size() != n || logs.size() != n) throw std::invalid_argument("spawn_group: argvs/envs/logs sizes differ");
+    if (!cpus.empty() && cpus.size() != n) throw std::invalid_argument("spawn_group: cpus must list one set per rank");
     std::vector<std::unique_ptr<Proc>> ps;
     for (size_t r = 0; r < n; ++r) {
       if (argvs[r].empty()) throw std::invalid_argument("spawn_group: empty argv");
@@ -620,6 +631,7 @@ class NodeAgent {
       p->hb_timeout_s = r == 0 ? hb_timeout_s : 0.0;
       p->max_restarts = max_restarts;
       p->rank = (int)r;
+      if (!cpus.empty()) p->cpus = cpus[r];
       ps.push_back(std::move(p));
     }
     std::lock_guard<std::mutex> lk(mu_);
@@ -747,7 +759,33 @@ class NodeAgent {
   void forget(int id) {
     std::lock_guard<std::mutex> lk(mu_);
     auto it = procs_.find(id);
-    if (it != procs_.end() && it->second->pid <= 0) procs_.erase(it);
+    if (it != procs_.end() && it->second->pid <= 0) {
+      if (it->second->zombie > 0) orphans_.push_back(it->second->zombie);   // still reaped by the monitor
+      procs_.erase(it);
+    }
+  }
+  // Drop a stopped gang and its members (a TP replica stopped or drained for
+  // good); false while any member still runs.
+  bool forget_group(int gid) {
+    std::lock_guard<std::mutex> lk(mu_);
+    auto it = groups_.find(gid);
+    if (it == groups_.end()) return false;
+    for (int id : it->second->members) {
+      auto pit = procs_.find(id);
+      if (pit != procs_.end() && pit->second->pid > 0) return false;
+    }
+    for (int id : it->second->members) {
+      auto pit = procs_.find(id);
+      if (pit == procs_.end()) continue;
+      if (pit->second->zombie > 0) orphans_.push_back(pit->second->zombie);
+      procs_.erase(pit);
+    }
+    groups_.erase(it);
+    return true;
+  }
+  size_t num_groups() {
+    std::lock_guard<std::mutex> lk(mu_);
+    return groups_.size();
   }
 
   // -- control server
@@ -891,8 +929,24 @@ class NodeAgent {
       rs->heartbeat_ns.store(now_ns());
       rs->status.store(RS_STARTING);
     }
+    // NUMA placement: the child inherits the CPU mask of the thread that spawns
+    // it, so pin THIS thread to the child's set around the spawn (race-free: the
+    // mask is in place before the child runs a single instruction)
+    cpu_set_t saved, want;
+    bool pinned = false;
+    if (!p.cpus.empty()) {
+      CPU_ZERO(&want);
+      for (int c : p.cpus)
+        if (c >= 0 && c < CPU_SETSIZE) CPU_SET(c, &want);
+      if (pthread_getaffinity_np(pthread_self(), sizeof(saved), &saved) == 0 &&
+          pthread_setaffinity_np(pthread_self(), sizeof(want), &want) == 0)
+        pinned = true;
+      else
+        events_.emplace_back(p.id, "pin_failed", "cannot apply the CPU set; starting unpinned");
+    }
     pid_t pid = -1;
     const int rc = posix_spawnp(&pid, av[0], &fa, &at, av.data(), ev.data());
+    if (pinned) pthread_setaffinity_np(pthread_self(), sizeof(saved), &saved);
     posix_spawn_file_actions_destroy(&fa);
     posix_spawnattr_destroy(&at);
     if (rc != 0) {
@@ -945,13 +999,16 @@ class NodeAgent {
     Group& g = *it->second;
     dead.pid = -1;
     dead.last_exit = why;
+    // SIGKILL every member, never wait here (mu_ is held: every agent call,
+    // KV rendezvous polls included, would stall for the members' exit); the
+    // monitor reaps them (Proc::zombie) and the gang restarts only after that
     for (int id : g.members) {
       auto pit = procs_.find(id);
       if (pit == procs_.end() || pit->second->pid <= 0) continue;
       Proc& m = *pit->second;
       kill(-m.pid, SIGKILL);
       int st = 0;
-      for (int i = 0; i < 500 && waitpid(m.pid, &st, WNOHANG) == 0; ++i) usleep(1000);
+      if (waitpid(m.pid, &st, WNOHANG) != m.pid) m.zombie = m.pid;
       m.pid = -1;
       m.last_exit = "killed with its group (rank " + std::to_string(dead.rank) + ": " + why + ")";
     }
@@ -994,8 +1051,15 @@ class NodeAgent {
       {
         std::lock_guard<std::mutex> lk(mu_);
         const int64_t now = now_ns();
+        auto gone = [](pid_t z) {
+          int st = 0;
+          const pid_t w = waitpid(z, &st, WNOHANG);
+          return w == z || (w < 0 && errno == ECHILD);
+        };
+        orphans_.erase(std::remove_if(orphans_.begin(), orphans_.end(), gone), orphans_.end());
         for (auto& kv : procs_) {
           Proc& p = *kv.second;
+          if (p.zombie > 0 && gone(p.zombie)) p.zombie = -1;
           if (p.pid > 0) {
             int st = 0;
             const pid_t r = waitpid(p.pid, &st, WNOHANG);
@@ -1015,7 +1079,7 @@ class NodeAgent {
               if (p.state == P_RUNNING && p.hb_timeout_s > 0 && age > p.hb_timeout_s) {
                 kill(-p.pid, SIGKILL);
                 int st2 = 0;
-                for (int i = 0; i < 200 && waitpid(p.pid, &st2, WNOHANG) == 0; ++i) usleep(1000);
+                if (waitpid(p.pid, &st2, WNOHANG) != p.pid) p.zombie = p.pid;   // reaped below, not waited for here
                 const std::string why = "missed heartbeats for " + std::to_string(age) + " s";
                 if (p.group > 0) group_death_locked(p.group, p, why);
                 else on_death_locked(p, why);
@@ -1023,7 +1087,7 @@ class NodeAgent {
             } else if (p.state == P_STARTING) {
               p.state = P_RUNNING;
             }
-          } else if (p.group == 0 && p.state == P_BACKOFF && now >= p.next_start_ns) {
+          } else if (p.group == 0 && p.state == P_BACKOFF && now >= p.next_start_ns && p.zombie <= 0) {
             start_locked(p);
           }
         }
@@ -1038,6 +1102,12 @@ class NodeAgent {
             if (all) g.state = P_RUNNING;
           }
           if (g.state != P_BACKOFF || now < g.next_start_ns) continue;
+          bool reaped = true;   // every old member gone (its VRAM released) before the gang restarts
+          for (int id : g.members) {
+            auto pit = procs_.find(id);
+            reaped = reaped && (pit == procs_.end() || pit->second->zombie <= 0);
+          }
+          if (!reaped) continue;
           for (int id : g.members) {
             auto pit = procs_.find(id);
             if (pit != procs_.end()) start_locked(*pit->second);
@@ -1110,6 +1180,7 @@ class NodeAgent {
   std::thread monitor_, server_;
   int listen_fd_ = -1;
   std::string sock_path_;
+  std::vector<pid_t> orphans_;   // killed processes of forgotten entries, still to be reaped
 };
 
 // Client side of the control protocol (CLI / other processes).
@@ -1202,13 +1273,17 @@ void register_node_agent(py::module_& m) {
       .def("spawn", &NodeAgent::spawn, py::arg("owner"), py::arg("argv"), py::arg("env") = py::dict(),
            py::arg("log_path") = "", py::arg("job") = "", py::arg("replica") = -1,
            py::arg("queues") = std::vector<uint32_t>{}, py::arg("health_timeout_s") = 30.0,
-           py::arg("max_restarts") = -1, py::arg("backoff_initial_s") = 0.5, py::arg("backoff_max_s") = 30.0)
+           py::arg("max_restarts") = -1, py::arg("backoff_initial_s") = 0.5, py::arg("backoff_max_s") = 30.0,
+           py::arg("cpus") = std::vector<int>{})
       .def("terminate", &NodeAgent::terminate, py::arg("id"), py::arg("grace_s") = 5.0,
            py::call_guard<py::gil_scoped_release>())
       .def("spawn_group", &NodeAgent::spawn_group, py::arg("owner"), py::arg("argvs"), py::arg("envs"),
            py::arg("logs"), py::arg("job") = "", py::arg("replica") = -1,
            py::arg("queues") = std::vector<uint32_t>{}, py::arg("health_timeout_s") = 30.0,
-           py::arg("max_restarts") = -1, py::arg("backoff_initial_s") = 0.5, py::arg("backoff_max_s") = 30.0)
+           py::arg("max_restarts") = -1, py::arg("backoff_initial_s") = 0.5, py::arg("backoff_max_s") = 30.0,
+           py::arg("cpus") = std::vector<std::vector<int>>{})
+      .def("forget_group", &NodeAgent::forget_group, py::arg("group"))
+      .def("num_groups", &NodeAgent::num_groups)
       .def("terminate_group", &NodeAgent::terminate_group, py::arg("group"), py::arg("grace_s") = 5.0,
            py::call_guard<py::gil_scoped_release>())
       .def("group_info", &NodeAgent::group_info)

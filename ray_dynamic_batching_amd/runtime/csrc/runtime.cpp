@@ -13,6 +13,7 @@
 //     patterns, milind-code request_simulator -> LoadGen (closed loop, Poisson,
 //     plus rate schedules driven from Python)
 #include "shm.h"
+#include "tp_bcast.h"
 
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
@@ -976,6 +977,53 @@ PYBIND11_MODULE(_rdb_runtime, m) {
       .def("merge_state", &LoadGen::merge_state, py::arg("buckets"), py::arg("count"), py::arg("sum_ns"),
            py::arg("max_ns"))
       .def("latency", &LoadGen::latency);
+
+  // TP batch broadcast (tp_bcast.h): the Python TP serving loop's rank-0 ->
+  // follower hand-off (the GPU path uses the same ring from the native engine)
+  py::class_<TPBcast>(m, "TPBcast")
+      .def(py::init([](const std::string& name, bool create, uint32_t n_readers, uint32_t n_slots,
+                       uint64_t payload_bytes, double attach_timeout_s) {
+             auto b = std::make_unique<TPBcast>();
+             if (create) {
+               b->create(name, n_readers, n_slots, payload_bytes);
+             } else {
+               py::gil_scoped_release nogil;
+               b->attach(name, (int64_t)(attach_timeout_s * 1e9));
+             }
+             return b;
+           }),
+           py::arg("name"), py::arg("create"), py::arg("n_readers") = 0, py::arg("n_slots") = 8,
+           py::arg("payload_bytes") = 65536, py::arg("attach_timeout_s") = 60.0)
+      .def("publish",
+           [](TPBcast& b, int kind, int a, int bb, int c, uint32_t n, py::bytes payload, double timeout_s) {
+             std::string d = payload;
+             py::gil_scoped_release nogil;
+             return b.publish(kind, a, bb, c, n, d.data(), (uint32_t)d.size(),
+                              timeout_s < 0 ? -1 : (int64_t)(timeout_s * 1e9));
+           },
+           py::arg("kind"), py::arg("a"), py::arg("b"), py::arg("c"), py::arg("n"), py::arg("payload"),
+           py::arg("timeout_s") = -1.0)
+      .def("take",
+           [](TPBcast& b, uint32_t reader, double timeout_s) -> py::object {
+             if (reader >= b.n_readers()) throw std::out_of_range("tp_bcast: reader index");
+             const BcastRecord* r;
+             {
+               py::gil_scoped_release nogil;
+               r = b.take(reader, timeout_s < 0 ? -1 : (int64_t)(timeout_s * 1e9));
+             }
+             if (!r) return py::none();
+             py::tuple t = py::make_tuple(r->kind, r->a, r->b, r->c, r->n,
+                                          py::bytes(reinterpret_cast<const char*>(r) + sizeof(BcastRecord), r->len));
+             b.release(reader);
+             return t;
+           },
+           py::arg("reader"), py::arg("timeout_s") = -1.0)
+      .def("close", &TPBcast::close)
+      .def("closed", &TPBcast::closed)
+      .def("unlink", &TPBcast::unlink)
+      .def("head", &TPBcast::head)
+      .def_property_readonly("payload_capacity", &TPBcast::payload_capacity)
+      .def_property_readonly("n_readers", &TPBcast::n_readers);
 
   py::class_<Consumer>(m, "Consumer")
       .def(py::init<JobHandle&, std::vector<uint32_t>>(), py::keep_alive<1, 2>())

@@ -7,6 +7,7 @@ A *servable model* exposes ``input_shape``, ``input_dtype``, ``output_shape``,
 """
 from __future__ import annotations
 
+import os
 import time
 from dataclasses import dataclass, field
 from typing import List, Optional, Sequence
@@ -14,6 +15,40 @@ from typing import List, Optional, Sequence
 import torch
 
 from ..utils.native import require_gpu_ops
+
+
+TUNED_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "ops", "tuned")
+
+
+def shipped_tile_table(model, max_batch: int, compute_streams: int, pipeline_depth: int) -> str:
+    """Path of the MI355X tile table shipped for this replica configuration
+    (``ops/tuned/mi355x_<signature>_B<max_batch>_cs<streams>_d<depth>.json``,
+    signature = ``model.tile_signature``, e.g. ``bert_L12_S128`` / ``resnet50``),
+    or "" when none was tuned for it.  ``bench.py``, ``bench/serve_bench.py`` and
+    Serve-deployed replicas (``EngineConfig.tile_table="auto"``) all resolve their
+    table here, so the deployed replica replays what the benchmark replays."""
+    sig = getattr(model, "tile_signature", None)
+    if not sig:
+        return ""
+    names = [f"mi355x_{sig}_B{max_batch}_cs{compute_streams}_d{pipeline_depth}.json"]
+    if compute_streams == 1:
+        names.append(f"mi355x_{sig}_B{max_batch}_d{pipeline_depth}.json")    # round-3 single-stream name
+    for n in names:
+        p = os.path.join(TUNED_DIR, n)
+        if os.path.exists(p):
+            return p
+    return ""
+
+
+def resolve_tile_table(choice: str, model, max_batch: int, compute_streams: int, pipeline_depth: int) -> str:
+    """EngineConfig.tile_table / bench ``--tile-table`` -> a path to replay or ""
+    (= tune at start-up): "auto" = the shipped table when there is one, "none" =
+    tune, anything else = that file."""
+    if not choice or choice == "none":
+        return ""
+    if choice == "auto":
+        return shipped_tile_table(model, max_batch, compute_streams, pipeline_depth)
+    return choice
 
 
 def default_buckets(max_batch: int) -> List[int]:
@@ -53,7 +88,8 @@ class EngineRunner:
 
     def __init__(self, job_name: str, replica: int, sessions: Sequence[SessionSpec], pipeline_depth: int = 2,
                  zero_copy: bool = True, device: Optional[int] = None, warmup_iters: int = 2, policy: int = 0,
-                 compute_streams: int = 1, batch_policy: str = "timeout"):
+                 compute_streams: int = 1, batch_policy: str = "timeout", stagger_us: Optional[int] = None,
+                 tile_table: Optional[str] = None):
         """``policy``: 0 = priority then earliest-deadline-first across sessions
         (co-located models, config 5); 1 = Nexus duty cycle (``set_duty_cycle`` +
         per-session ``set_duty_share``).  ``compute_streams`` > 1 runs that many
@@ -62,7 +98,11 @@ class EngineRunner:
         ``batch_policy``: "timeout" (default, ``@serve.batch`` semantics: a batch
         closes when full or ``max_wait`` after its first request) or "idle" (a
         partial batch is also dispatched as soon as a compute stream has no batch
-        running -- lower latency at low load, same batches under saturation)."""
+        running -- lower latency at low load, same batches under saturation).
+        ``stagger_us``: hold a batch starting on an idle stream that long behind
+        the other stream's idle start (None: RDB_ENGINE_STAGGER_US).
+        ``tile_table``: a tile-table file to replay instead of tuning at start-up
+        (None: RDB_TUNE_FILE; resolve "auto" with ``resolve_tile_table``)."""
         if batch_policy not in ("timeout", "idle"):
             raise ValueError(f"batch_policy must be 'timeout' or 'idle', got {batch_policy!r}")
         self.ops = require_gpu_ops()
@@ -77,18 +117,22 @@ class EngineRunner:
         self.batch_policy = batch_policy
         if batch_policy == "idle":
             self.engine.set_idle_dispatch(True)
+        if stagger_us is not None:
+            self.engine.set_stagger_us(int(stagger_us))
+        self.stagger_us = self.engine.stagger_us()
+        # per-shape tile tuning ranks candidates by throughput with this many
+        # concurrent launches (ops._tuned_cfg), i.e. the replica's own regime
+        os.environ.setdefault("RDB_TUNE_STREAMS", str(self.compute_streams))
         self.pools = []
         self.capture_s = 0.0
         self.warmup_iters = warmup_iters
         # whole-forward selection among near-tied GEMM tiles for the largest bucket
         # (ops.tune_in_context); RDB_TUNE_IN_CONTEXT=0 turns it off
-        import os
-
         self.tune_in_context = os.environ.get("RDB_TUNE_IN_CONTEXT", "1") == "1"
         self.tuning_changes = {}
         # RDB_TUNE_FILE: replay a saved tile table (A/B runs, profiling passes) instead
         # of tuning; written after tuning when the file does not exist yet
-        self.tune_file = os.environ.get("RDB_TUNE_FILE", "")
+        self.tune_file = tile_table if tile_table is not None else os.environ.get("RDB_TUNE_FILE", "")
         self._tune_loaded = False
         if self.tune_file and os.path.exists(self.tune_file):
             from .. import ops

@@ -97,11 +97,12 @@ def gpu_pci_addresses() -> List[str]:
         return []
 
 
-def kfd_gpu_pci_addresses(sysfs: str = "/sys") -> List[str]:
+def kfd_gpu_pci_addresses(sysfs: str = "/sys", respect_visible: bool = True) -> List[str]:
     """PCI addresses of the GPUs in HIP device order WITHOUT initialising HIP
     (so a rank can pin itself before the runtime starts any thread): the KFD
     topology nodes that have SIMDs, in node order (the order ROCr enumerates
-    agents), filtered by ROCR_VISIBLE_DEVICES then HIP_VISIBLE_DEVICES."""
+    agents), filtered by ROCR_VISIBLE_DEVICES then HIP_VISIBLE_DEVICES (unless
+    ``respect_visible`` is False: the node agent plans over every GPU)."""
     root = os.path.join(sysfs, "class", "kfd", "kfd", "topology", "nodes")
     try:
         nodes = sorted(int(n) for n in os.listdir(root) if n.isdigit())
@@ -116,7 +117,7 @@ def kfd_gpu_pci_addresses(sysfs: str = "/sys") -> List[str]:
         loc = int(kv.get("location_id", "0"))
         dom = int(kv.get("domain", "0"))
         gpus.append(f"{dom:04x}:{(loc >> 8) & 0xff:02x}:{(loc >> 3) & 0x1f:02x}.{loc & 0x7}")
-    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES"):
+    for var in (("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES") if respect_visible else ()):
         v = os.environ.get(var)
         if v:
             try:
@@ -195,3 +196,24 @@ def place_rank(rank: int, rank_gpus: Sequence[int], sysfs: str = "/sys",
     node = loc.get(rank_gpus[rank], (-1, []))[0] if rank < len(rank_gpus) else -1
     pinned = pin_process(mine)
     return dict(numa_node=node, cpus=format_cpulist(mine), pinned=pinned)
+
+
+def gpu_placement(gpu: int, sysfs: str = "/sys", pci: Optional[List[str]] = None) -> dict:
+    """Placement of a Serve replica on physical GPU ``gpu``, planned by the
+    controller / node agent (which see every GPU of the node, not a replica's
+    HIP_VISIBLE_DEVICES view): {numa_node, cpus (list), cpulist}.  The CPU sets
+    are :func:`plan_cpu_sets` with one rank per GPU, so replicas of GPUs on one
+    NUMA node get disjoint cores -- the same split ``bench.py``'s ranks use.  The
+    agent applies the set to the replica process at spawn (inherited by every
+    thread it starts) and the controller binds the replica's request ring to
+    ``numa_node``.  RDB_NUMA_PIN=0 disables it (numa_node -1, no CPUs)."""
+    if os.environ.get("RDB_NUMA_PIN", "1") == "0" or gpu < 0:
+        return dict(numa_node=-1, cpus=[], cpulist="")
+    if pci is None:
+        pci = kfd_gpu_pci_addresses(sysfs, respect_visible=False)
+    if gpu >= len(pci):
+        return dict(numa_node=-1, cpus=[], cpulist="")
+    loc = gpu_locality_map(sysfs, pci)
+    allowed = os.sched_getaffinity(0) if hasattr(os, "sched_getaffinity") else None
+    sets = plan_cpu_sets(list(range(len(pci))), loc, allowed)
+    return dict(numa_node=loc.get(gpu, (-1, []))[0], cpus=list(sets[gpu]), cpulist=format_cpulist(sets[gpu]))

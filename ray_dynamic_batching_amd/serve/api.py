@@ -61,6 +61,10 @@ class Deployment:
                 raise TypeError(f"unknown deployment option {k!r}")
             if isinstance(v, (AutoscalingConfig, EngineConfig)):
                 v = v.model_dump()
+            elif k == "engine" and isinstance(v, dict):
+                # partial engine overrides (YAML `engine: {compute_streams: 1}`) keep
+                # the other engine fields (model_deployment's slot size, buckets, ...)
+                v = {**(data.get("engine") or {}), **v}
             data[k] = v
         if "num_replicas" in kw and kw["num_replicas"] != "auto" and "autoscaling_config" not in kw:
             data["autoscaling_config"] = None
@@ -124,6 +128,7 @@ def deployment(_func_or_class: Optional[Union[Callable, type]] = None, *, name: 
                health_check_period_s: Optional[float] = None, health_check_timeout_s: Optional[float] = None,
                logging_config=None, slo_ms: Optional[float] = None, profile_csv: Optional[str] = None,
                priority: Optional[int] = None, drop_stale: Optional[bool] = None,
+               max_request_retries: Optional[int] = None, request_retry_timeout_s: Optional[float] = None,
                engine: Union[Dict, EngineConfig, None] = None, tensor_parallel_size: Optional[int] = None,
                tp_backend: Optional[str] = None):
     """Decorator turning a class or function into a Deployment
@@ -137,6 +142,7 @@ def deployment(_func_or_class: Optional[Union[Callable, type]] = None, *, name: 
         graceful_shutdown_timeout_s=graceful_shutdown_timeout_s, health_check_period_s=health_check_period_s,
         health_check_timeout_s=health_check_timeout_s, logging_config=logging_config, slo_ms=slo_ms,
         profile_csv=profile_csv, priority=priority, drop_stale=drop_stale, engine=engine,
+        max_request_retries=max_request_retries, request_retry_timeout_s=request_retry_timeout_s,
         tensor_parallel_size=tensor_parallel_size, tp_backend=tp_backend).items() if v is not None}
     if isinstance(given.get("autoscaling_config"), AutoscalingConfig):
         given["autoscaling_config"] = given["autoscaling_config"].model_dump()

@@ -54,11 +54,41 @@ class AutoscalingConfig(BaseModel):
 
 
 class EngineConfig(BaseModel):
-    """MI355X replica-engine knobs for servable (natively executed) models."""
+    """MI355X replica-engine knobs for servable (natively executed) models.
+
+    Every knob the headline replica (``bench.py``) runs with travels here, from
+    the deployment (decorator options / YAML ``engine:``) to the replica process
+    that builds the engine (``serve/replica_main._run_engine``), the way Serve's
+    DeploymentConfig carries every replica knob (reference:
+    python/ray/serve/_private/config.py:81-170).  Defaults = the benchmarked
+    BERT / ResNet-50 replica: two compute streams x pipeline depth 4, the shipped
+    MI355X tile table for the model's signature, NUMA-pinned process and ring."""
     buckets: Optional[List[int]] = None          # padded batch sizes captured as hipGraphs
-    pipeline_depth: int = 2                      # batches in flight (H2D of k+1 under compute of k)
+    pipeline_depth: int = 4                      # batches in flight (H2D of k+1 under compute of k)
+    compute_streams: int = 2                     # batches executing concurrently on the GPU
+    batch_policy: str = "timeout"                # "timeout" (@serve.batch semantics) or "idle"
+    stagger_us: int = 0                          # hold an idle-starting stream behind the other (latency knob)
+    tile_table: str = "auto"                     # "auto" (shipped table for the model signature), "none", or a path
+    numa_pin: bool = True                        # node agent pins the replica to its GPU's CPUs, ring mbind-ed there
+    warm_s: Optional[float] = None               # device warm-up replays before READY (default 0.25 s)
     zero_copy: bool = True                       # GPU gathers payloads straight from pinned shm
     request_slot_bytes: Optional[int] = None     # per-request payload bytes (default: model input size)
+
+    @model_validator(mode="after")
+    def _check(self):
+        if self.pipeline_depth < 1:
+            raise ValueError("engine.pipeline_depth must be >= 1")
+        if self.compute_streams < 1:
+            raise ValueError("engine.compute_streams must be >= 1")
+        if self.compute_streams > self.pipeline_depth:
+            raise ValueError("engine.compute_streams must be <= engine.pipeline_depth (one slot per running batch)")
+        if self.batch_policy not in ("timeout", "idle"):
+            raise ValueError("engine.batch_policy must be 'timeout' or 'idle'")
+        if self.stagger_us < 0:
+            raise ValueError("engine.stagger_us must be >= 0")
+        if self.buckets is not None and (not self.buckets or any(int(b) < 1 for b in self.buckets)):
+            raise ValueError("engine.buckets must be a non-empty list of positive batch sizes")
+        return self
 
 
 class DeploymentConfig(BaseModel):
@@ -83,6 +113,9 @@ class DeploymentConfig(BaseModel):
     profile_csv: Optional[str] = None
     priority: int = 0
     drop_stale: bool = False
+    # router: re-dispatch of a request whose replica died (serve/router.py ShmRouter)
+    max_request_retries: int = 3
+    request_retry_timeout_s: float = 60.0
     engine: EngineConfig = Field(default_factory=EngineConfig)
     # Tensor-parallel replica: the node agent gang-spawns `tensor_parallel_size`
     # rank processes (one per placement bundle; default: that many bundles of
@@ -161,6 +194,8 @@ class DeploymentConfig(BaseModel):
             raise ValueError("a tensor-parallel deployment needs one placement bundle per rank")
         if self.tp_backend is not None and self.tp_backend not in ("nccl", "rccl", "gloo"):
             raise ValueError("tp_backend must be nccl / rccl / gloo")
+        if self.max_request_retries < 0 or self.request_retry_timeout_s < 0:
+            raise ValueError("max_request_retries / request_retry_timeout_s must be >= 0")
         if self.max_replicas_per_node is not None and not (1 <= self.max_replicas_per_node <= 100):
             raise ValueError("max_replicas_per_node must be in [1, 100]")
         return self

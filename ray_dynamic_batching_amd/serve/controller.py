@@ -93,7 +93,8 @@ def lookup_router(app_name: str, deployment: str):
             c = r["codec"]
             codec = TensorCodec(c["input_shape"], getattr(torch, c["input_dtype"]), c["output_shape"],
                                 getattr(torch, c["output_dtype"]))
-        return ShmRouter(r["job"], r["model_id"], deployment, r.get("max_queued", -1), codec)
+        return ShmRouter(r["job"], r["model_id"], deployment, r.get("max_queued", -1), codec,
+                         retry_timeout_s=r.get("retry_timeout_s", 60.0), max_retries=r.get("max_retries", 3))
     ctrl = get_controller(create=False)
     if ctrl is None:
         raise RayServeException("serve is not running; call serve.run() first")
@@ -148,6 +149,7 @@ class ServeController:
         self.proxy = None
         self.grpc_proxy = None
         self.jobs: Dict[str, Any] = {}            # app -> job segment handle (process mode)
+        self._rings_ready: Dict[str, set] = {}    # job name -> request rings initialised (NUMA-bound)
         self.lock = threading.RLock()
         self._clock = time.monotonic          # autoscaling look-back windows (tests may fake it)
         self.workdir = tempfile.mkdtemp(prefix="rdb_serve_")
@@ -273,9 +275,12 @@ class ServeController:
             if a.deployment.config.engine.request_slot_bytes:
                 req_bytes = max(req_bytes, a.deployment.config.engine.request_slot_bytes)
         jname = f"serve_{os.getpid()}_{app_name}_{int(time.time() * 1000) % 10**8}"
+        # request rings are initialised per replica slot at its first spawn, bound
+        # to the NUMA node of the GPU it lands on (_init_ring)
         job = rjob.Job(jname, create=True, n_replicas=n, n_queues=n, n_clients=16 + n, req_capacity=1024,
-                       req_slot_bytes=req_bytes, cmp_capacity=4096, cmp_slot_bytes=cmp_bytes)
+                       req_slot_bytes=req_bytes, cmp_capacity=4096, cmp_slot_bytes=cmp_bytes, defer_req_rings=True)
         self.jobs[app_name] = job
+        self._rings_ready[jname] = set()
 
     def _prepare_process_deployment(self, st: DeploymentState) -> None:
         import cloudpickle
@@ -292,13 +297,16 @@ class ServeController:
             cloudpickle.dump(spec, f)
         if sv is not None:
             st.codec = _codec_for_servable(sv)
-        st.router = ShmRouter(job.info()["name"], st.model_id, st.name, st.config.max_queued_requests, st.codec)
+        st.router = ShmRouter(job.info()["name"], st.model_id, st.name, st.config.max_queued_requests, st.codec,
+                              retry_timeout_s=st.config.request_retry_timeout_s,
+                              max_retries=st.config.max_request_retries)
 
     def _write_routing_table(self, app_name: str) -> None:
         routes = {}
         for st in self.apps[app_name].values():
             r = dict(job=self.jobs[app_name].info()["name"], model_id=st.model_id,
-                     max_queued=st.config.max_queued_requests)
+                     max_queued=st.config.max_queued_requests, max_retries=st.config.max_request_retries,
+                     retry_timeout_s=st.config.request_retry_timeout_s)
             if st.codec is not None:
                 c = st.codec
                 r["codec"] = dict(input_shape=list(c.input_shape), output_shape=list(c.output_shape),
@@ -320,6 +328,34 @@ class ServeController:
         env["PYTHONPATH"] = pkg_root + os.pathsep + os.environ.get("PYTHONPATH", "")
         return env
 
+    def _placement(self, st: DeploymentState, gpu: int) -> Dict[str, Any]:
+        """NUMA placement of a replica (rank) on physical GPU ``gpu``: the node
+        agent starts the process pinned to the GPU's share of its NUMA node's CPUs
+        (the same split bench.py's ranks use, runtime/numa.py gpu_placement)."""
+        if not st.config.engine.numa_pin or gpu < 0:
+            return dict(numa_node=-1, cpus=[], cpulist="")
+        from ..runtime import numa
+
+        try:
+            return numa.gpu_placement(gpu)
+        except Exception as e:  # noqa: BLE001 -- placement is an optimisation, never a failure
+            logger.warning("NUMA placement of GPU %d failed: %s", gpu, e)
+            return dict(numa_node=-1, cpus=[], cpulist="")
+
+    def _init_ring(self, job, slot: int, numa_node: int) -> None:
+        """First use of a replica slot: bind its request ring's pages to the NUMA
+        node of the replica's GPU (a shared-memory policy: it holds for every
+        process that touches the pages) and write the slot sequence numbers.
+        Runs before the slot's queue is configured, so no producer can pick it
+        earlier; a restarted replica keeps its live ring."""
+        ready = self._rings_ready.setdefault(job.info()["name"], set())
+        if slot in ready:
+            return
+        rc = job.init_req_ring(slot, numa_node)
+        if rc != 0:
+            logger.info("request ring %d: mbind to node %d returned %d (left to first touch)", slot, numa_node, rc)
+        ready.add(slot)
+
     def _spawn_tp(self, st: DeploymentState, rep: ProcReplica, owner: str) -> bool:
         """A tensor-parallel replica: one placement bundle per rank, gang-reserved;
         the agent spawns the ranks as one group (each pinned to its bundle's
@@ -337,23 +373,34 @@ class ServeController:
             logger.warning("no GPU capacity for TP replica %s (%d ranks)", owner, n)
             return False
         rep.alloc = alloc
-        job = self.jobs[st.app_name]
-        gpus = list(alloc["gpus"])
-        job.configure_queue(rep.slot, rep.slot, st.model_id, st.config.max_ongoing_requests,
-                            float(st.config.slo_ms or 0.0), True)
-        job.set_replica_status(rep.slot, 1, gpus[0] if gpus else -1, 0)
-        base = self._replica_env(st, rep, job)
-        argvs, envs, logs = [], [], []
-        for i, g in enumerate(alloc["bundle_gpus"]):
-            env = dict(base)
-            env.update(visible_devices_env(list(g)))
-            envs.append(env)
-            argvs.append([sys.executable, "-m", "ray_dynamic_batching_amd.serve.replica_main", "--spec",
-                          st.spec_path, "--replica", str(rep.slot), "--gpu", ",".join(map(str, g))])
-            logs.append(os.path.join(self.workdir, f"{owner.replace('#', '.')}.rank{i}.log"))
-        rep.group_id = self.agent.spawn_group(owner, argvs, envs, logs, job.info()["name"], rep.slot, [rep.slot],
-                                              float(st.config.health_check_timeout_s), -1, 0.5, 30.0)
-        rep.proc_id = self.agent.group_info(rep.group_id)["members"][0]
+        try:
+            job = self.jobs[st.app_name]
+            gpus = list(alloc["gpus"])
+            places = [self._placement(st, int(g[0]) if len(g) else -1) for g in alloc["bundle_gpus"]]
+            self._init_ring(job, rep.slot, places[0]["numa_node"] if places else -1)
+            job.configure_queue(rep.slot, rep.slot, st.model_id, st.config.max_ongoing_requests,
+                                float(st.config.slo_ms or 0.0), True)
+            job.set_replica_status(rep.slot, 1, gpus[0] if gpus else -1, 0)
+            base = self._replica_env(st, rep, job)
+            argvs, envs, logs = [], [], []
+            for i, g in enumerate(alloc["bundle_gpus"]):
+                env = dict(base)
+                env.update(visible_devices_env(list(g)))
+                env["RDB_NUMA_NODE"] = str(places[i]["numa_node"])
+                envs.append(env)
+                argvs.append([sys.executable, "-m", "ray_dynamic_batching_amd.serve.replica_main", "--spec",
+                              st.spec_path, "--replica", str(rep.slot), "--gpu", ",".join(map(str, g))])
+                logs.append(os.path.join(self.workdir, f"{owner.replace('#', '.')}.rank{i}.log"))
+            cpus = [list(p["cpus"]) for p in places] if any(p["cpus"] for p in places) else []
+            rep.group_id = self.agent.spawn_group(owner, argvs, envs, logs, job.info()["name"], rep.slot,
+                                                  [rep.slot], float(st.config.health_check_timeout_s), -1, 0.5,
+                                                  30.0, cpus)
+            rep.proc_id = self.agent.group_info(rep.group_id)["members"][0]
+        except Exception:
+            # never leak the gang reservation of a replica that did not start
+            self.agent.release(owner)
+            rep.alloc = None
+            raise
         rep.started_at = time.time()
         rep.ready = False
         rep.health_failures = 0
@@ -363,8 +410,10 @@ class ServeController:
         if rep.group_id >= 0:
             members = self.agent.group_info(rep.group_id)["members"]
             self.agent.terminate_group(rep.group_id, grace_s)
-            for m in members:
-                self.agent.forget(m)
+            if not self.agent.forget_group(rep.group_id):   # the Group entry and its members
+                for m in members:
+                    self.agent.forget(m)
+            rep.group_id = -1
         elif rep.proc_id >= 0:
             self.agent.terminate(rep.proc_id, grace_s)
             self.agent.forget(rep.proc_id)
@@ -389,16 +438,20 @@ class ServeController:
         rep.alloc = alloc
         gpus = list(alloc["gpus"])
         job = self.jobs[st.app_name]
+        place = self._placement(st, int(gpus[0]) if gpus and float(st.config.num_gpus) > 0 else -1)
+        self._init_ring(job, rep.slot, place["numa_node"])
         job.configure_queue(rep.slot, rep.slot, st.model_id, st.config.max_ongoing_requests,
                             float(st.config.slo_ms or 0.0), True)
         job.set_replica_status(rep.slot, 1, gpus[0] if gpus else -1, 0)
         env = dict(visible_devices_env(gpus))
         env.update(self._replica_env(st, rep, job))
+        env["RDB_NUMA_NODE"] = str(place["numa_node"])
         cmd = [sys.executable, "-m", "ray_dynamic_batching_amd.serve.replica_main", "--spec", st.spec_path,
                "--replica", str(rep.slot), "--gpu", ",".join(map(str, gpus))]
         log = os.path.join(self.workdir, f"{owner.replace('#', '.')}.log")
         rep.proc_id = self.agent.spawn(owner, cmd, env, log, job.info()["name"], rep.slot, [rep.slot],
-                                       float(st.config.health_check_timeout_s), -1, 0.5, 30.0)
+                                       float(st.config.health_check_timeout_s), -1, 0.5, 30.0,
+                                       list(place["cpus"]))
         rep.started_at = time.time()
         rep.ready = False
         rep.health_failures = 0

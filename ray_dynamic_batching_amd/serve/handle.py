@@ -106,9 +106,10 @@ class StreamSink:
     ``DeploymentResponseGenerator`` wraps (python/ray/serve/handle.py:620-743)
     is awaited natively on the caller's loop."""
 
-    __slots__ = ("_items", "_cv", "_waiters")
+    __slots__ = ("_items", "_cv", "_waiters", "cancelled")
 
     def __init__(self):
+        self.cancelled = False            # set by the router's cancel(): a queued request is never sent
         self._items: collections.deque = collections.deque()
         self._cv = threading.Condition(threading.Lock())
         self._waiters: list = []          # [(loop, future)] of async consumers

@@ -118,7 +118,7 @@ def _run_tp(spec, cfg, r, stop, tp, gpu) -> int:
 
     from ..parallel import collective as col
     from ..parallel.rendezvous import init_tp_group
-    from ..runtime.tp_replica import TPReplica
+    from ..runtime.tp_replica import TPReplica, bcast_name
 
     sv = spec.get("servable")
     if not sv:
@@ -147,9 +147,12 @@ def _run_tp(spec, cfg, r, stop, tp, gpu) -> int:
     eng = cfg.engine
     buckets = eng.buckets or [1, 2, 4, 8, 16, 32][: max(1, sv["max_batch_size"].bit_length())]
     buckets = sorted({min(b, sv["max_batch_size"]) for b in buckets} | {sv["max_batch_size"]})
+    ring = bcast_name(tp.group, tp.epoch)
+    use_graphs = use_gpu and os.environ.get("RDB_TP_GRAPHS", "1") == "1"
+    if use_graphs and os.environ.get("RDB_TP_NATIVE", "1") == "1":
+        return _run_tp_native(spec, cfg, r, stop, tp, model, buckets, ring)
     rep = TPReplica(model, spec["job"] if tp.rank == 0 else None, r, r, buckets, group="tp",
-                    max_wait_s=sv["batch_wait_timeout_s"],
-                    use_graphs=use_gpu and os.environ.get("RDB_TP_GRAPHS", "1") == "1", gpu_index=gpu)
+                    max_wait_s=sv["batch_wait_timeout_s"], use_graphs=use_graphs, gpu_index=gpu, ring=ring)
     rep.capture()                      # rank 0 marks the replica READY
     while True:
         if tp.rank == 0 and stop.is_set():
@@ -161,10 +164,37 @@ def _run_tp(spec, cfg, r, stop, tp, gpu) -> int:
     return 0
 
 
+def _run_tp_native(spec, cfg, r, stop, tp, model, buckets, ring) -> int:
+    """GPU ranks of a TP replica on the native engine (runtime/tp_replica.py
+    NativeTP): rank 0 a leader engine on the replica's queue, the others
+    followers of its broadcast ring; no Python per batch on any rank."""
+    from ..runtime.tp_replica import NativeTP
+
+    sv = spec["servable"]
+    eng = cfg.engine
+    ntp = NativeTP(model, spec["job"], r, buckets, tp.rank, tp.world, "tp", ring, sv["max_batch_size"],
+                   sv["batch_wait_timeout_s"], pipeline_depth=min(eng.pipeline_depth, 2),
+                   batch_policy=eng.batch_policy)
+    ntp.start()
+    logger.info("TP rank %d/%d: native engine (%s), ring %s", tp.rank, tp.world,
+                "leader" if tp.rank == 0 else "follower", ring)
+    code = 0
+    while not (tp.rank == 0 and stop.is_set()):
+        why = ntp.check()
+        if why:
+            if why != "stopped":
+                logger.error("TP rank %d: %s", tp.rank, why)
+                code = 2
+            break
+        stop.wait(0.2)
+    ntp.stop()
+    st = ntp.stats()
+    logger.info("TP rank %d leaves after %d batches / %d requests", tp.rank, st["batches"], st["requests"])
+    return code
+
+
 def _run_engine(spec, cfg, job, r, stop) -> int:
     import torch
-
-    from ..runtime.engine import EngineRunner, SessionSpec
 
     sv = spec["servable"]
     torch.cuda.set_device(0)
@@ -173,11 +203,10 @@ def _run_engine(spec, cfg, job, r, stop) -> int:
         model = factory(device="cuda")
     except TypeError:
         model = factory()
-    eng = cfg.engine
-    s = SessionSpec(model=model, queue=r, max_batch=sv["max_batch_size"], max_wait_s=sv["batch_wait_timeout_s"],
-                    buckets=eng.buckets, priority=cfg.priority, slo_ms=float(cfg.slo_ms or 0.0),
-                    drop_stale=cfg.drop_stale)
-    runner = EngineRunner(spec["job"], r, [s], pipeline_depth=eng.pipeline_depth, zero_copy=eng.zero_copy).build()
+    runner = build_engine_runner(spec, cfg, r, model)
+    logger.info("engine: %d compute streams, depth %d, policy %s, stagger %d us, tile table %s",
+                runner.compute_streams, runner.depth, runner.batch_policy, runner.stagger_us,
+                os.path.basename(runner.tune_file) or "tuned at start-up")
     runner.start()   # sets the replica READY in shm
     while not stop.is_set():
         err = runner.error()
@@ -192,6 +221,26 @@ def _run_engine(spec, cfg, job, r, stop) -> int:
         stop.wait(0.2)
     runner.stop()
     return 0
+
+
+def build_engine_runner(spec, cfg, r, model, runner_cls=None):
+    """The replica's native engine, configured from the deployment's
+    ``EngineConfig`` -- the same knobs ``bench.py`` runs the headline replica
+    with (compute streams, pipeline depth, batch policy, stagger, the shipped
+    tile table resolved by model signature, device warm-up)."""
+    from ..runtime.engine import EngineRunner, SessionSpec, resolve_tile_table
+
+    sv = spec["servable"]
+    eng = cfg.engine
+    s = SessionSpec(model=model, queue=r, max_batch=sv["max_batch_size"], max_wait_s=sv["batch_wait_timeout_s"],
+                    buckets=eng.buckets, priority=cfg.priority, slo_ms=float(cfg.slo_ms or 0.0),
+                    drop_stale=cfg.drop_stale)
+    table = resolve_tile_table(eng.tile_table, model, sv["max_batch_size"], eng.compute_streams, eng.pipeline_depth)
+    runner = (runner_cls or EngineRunner)(spec["job"], r, [s], pipeline_depth=eng.pipeline_depth,
+                                          zero_copy=eng.zero_copy, compute_streams=eng.compute_streams,
+                                          batch_policy=eng.batch_policy, stagger_us=eng.stagger_us,
+                                          tile_table=table)
+    return runner.build(warm_s=eng.warm_s)
 
 
 def _run_python(spec, cfg, job, r, stop, ctx) -> int:

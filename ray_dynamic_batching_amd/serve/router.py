@@ -234,17 +234,21 @@ class ShmRouter:
     _clients_lock = threading.Lock()
 
     def __init__(self, job_name: str, model_id: int, deployment: str, max_queued_requests: int = -1,
-                 tensor_codec=None, retry_timeout_s: float = 60.0):
+                 tensor_codec=None, retry_timeout_s: float = 60.0, max_retries: int = 3):
         self.job_name = job_name
         self.model_id = model_id
         self.deployment = deployment
         self.max_queued = max_queued_requests
         self.codec = tensor_codec
-        # Requests whose replica died are re-dispatched until this long after
-        # their submission (deadline-based like the reference's retry loop,
-        # python/ray/serve/_private/router.py:452-496, which retries until the
-        # caller gives up), not a fixed number of times.
+        # Requests whose replica died are re-dispatched at most `max_retries`
+        # times AND only until `retry_timeout_s` after their submission, then
+        # fail with ReplicaDiedError: a request that kills its replica is not
+        # replayed into every restarted replica (the reference retries only
+        # scheduling, python/ray/serve/_private/router.py:452-496; replaying an
+        # accepted request assumes an idempotent forward, hence the cap).
+        # DeploymentConfig.request_retry_timeout_s / max_request_retries set both.
         self.retry_timeout_s = retry_timeout_s
+        self.max_retries = max_retries
         self.metrics = RouterMetrics()
         with ShmRouter._clients_lock:
             hub = ShmRouter._clients.get(job_name)
@@ -335,10 +339,10 @@ class ShmRouter:
             kind = KIND_PICKLE
         route = _Route(self.model_id, mux_hash(meta.multiplexed_model_id)) if meta.multiplexed_model_id \
             else self.model_id
-        deadline = time.monotonic() + self.retry_timeout_s
+        budget = (time.monotonic() + self.retry_timeout_s, self.max_retries)   # (deadline, retries left)
         if sink is None:
             sink = ("stream", StreamSink()) if meta.stream else ("unary", concurrent.futures.Future())
-        self.hub.submit(route, payload, kind, sink, self.codec, deadline)
+        self.hub.submit(route, payload, kind, sink, self.codec, budget)
         if meta.stream:
             return DeploymentResponseGenerator(sink[1], meta, cancel_cb=lambda: self.hub.cancel(sink))
         return DeploymentResponse(sink[1], meta, cancel_cb=lambda: self.hub.cancel(sink))
@@ -438,28 +442,40 @@ class _ShmClientHub:
         if kind == "unary":
             obj.cancel()
         else:
+            obj.cancelled = True              # _sink_cancelled: still-queued items are dropped, not sent
             obj.put(("error", RequestCancelledError("stream cancelled")))
         with self.lock:
             for rid in [r for r, e in self.inflight.items() if e[3] is sink]:
                 del self.inflight[rid]
+            if self.pending:                  # drop it from the FIFO now (and its pending count)
+                keep = collections.deque()
+                for item in self.pending:
+                    if item[3] is sink:
+                        self._pending_by_model[item[0]] -= 1
+                    else:
+                        keep.append(item)
+                self.pending = keep
 
     # -- internals (lock held) -------------------------------------------------
     @staticmethod
     def _sink_cancelled(sink) -> bool:
-        return sink[0] == "unary" and sink[1].cancelled()
+        return sink[1].cancelled() if sink[0] == "unary" else bool(getattr(sink[1], "cancelled", False))
 
     def _retry(self, entry, why: str) -> None:
         """Re-dispatch a request whose replica died, at the front of the FIFO,
-        while its retry deadline has not passed; fail it after that."""
-        model_id, payload, kind, sink, codec, deadline = entry[:6]
+        while it has retries left and its retry deadline has not passed; fail it
+        with ReplicaDiedError after that."""
+        model_id, payload, kind, sink, codec, budget = entry[:6]
         if self._sink_cancelled(sink):
             return
-        if time.monotonic() < deadline:
+        deadline, left = budget
+        if left > 0 and time.monotonic() < deadline:
             self.retries += 1
-            self.pending.appendleft((model_id, payload, kind, sink, codec, deadline))
+            self.pending.appendleft((model_id, payload, kind, sink, codec, (deadline, left - 1)))
             self._pending_by_model[model_id] += 1
         else:
-            self._fail(sink, ReplicaDiedError(f"{why}; retry window exhausted"))
+            what = "retry window exhausted" if left > 0 else "retried too often"
+            self._fail(sink, ReplicaDiedError(f"{why}; {what}"))
 
     def _try_submit(self, model_id, payload, kind, sink, codec, retry_deadline) -> bool:
         if self._sink_cancelled(sink):

@@ -38,6 +38,8 @@ class DeploymentSchema(BaseModel):
     slo_ms: Optional[float] = None
     priority: Optional[int] = None
     drop_stale: Optional[bool] = None
+    max_request_retries: Optional[int] = None
+    request_retry_timeout_s: Optional[float] = None
     engine: Optional[Dict[str, Any]] = None
 
     def overrides(self) -> Dict[str, Any]:

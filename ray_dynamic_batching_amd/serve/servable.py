@@ -99,18 +99,28 @@ def _accepts_device(f) -> bool:
 
 
 def model_deployment(factory: Callable, name: str, *, max_batch_size: int = 32, batch_wait_timeout_s: float = 0.005,
-                     buckets: Optional[Sequence[int]] = None, pipeline_depth: int = 2, io_spec=None,
-                     **deployment_options) -> Deployment:
+                     buckets: Optional[Sequence[int]] = None, pipeline_depth: Optional[int] = None,
+                     compute_streams: Optional[int] = None, io_spec=None, **deployment_options) -> Deployment:
     """Declare a GPU servable-model deployment.  ``factory(device=...)`` returns a
     model exposing ``input_shape/input_dtype/output_shape/output_dtype`` and
     ``forward(x[B, ...])``; ``io_spec`` (or ``factory.io_spec``) =
     (input_shape, input_dtype, output_shape, output_dtype) lets the router encode
-    requests without instantiating the model (see models/factories.py)."""
+    requests without instantiating the model (see models/factories.py).
+    ``engine={...}`` takes every ``EngineConfig`` field (compute streams, batch
+    policy, tile table, NUMA pinning, ...); ``pipeline_depth`` /
+    ``compute_streams`` are shorthands for two of them.  The defaults are the
+    benchmarked replica's (2 streams x depth 4, shipped tile table)."""
     if io_spec is not None:
         factory.io_spec = tuple(io_spec)
     eng = dict(deployment_options.pop("engine", {}) or {})
     eng.setdefault("buckets", list(buckets) if buckets else None)
-    eng.setdefault("pipeline_depth", pipeline_depth)
+    if pipeline_depth is not None:
+        eng.setdefault("pipeline_depth", pipeline_depth)
+    if compute_streams is not None:
+        eng.setdefault("compute_streams", compute_streams)
+    if eng.get("pipeline_depth") is not None and eng.get("compute_streams") is None:
+        # an explicit shallow pipeline (depth 1) cannot hold two running batches
+        eng["compute_streams"] = min(2, int(eng["pipeline_depth"]))
     spec = getattr(factory, "io_spec", None)
     if spec is not None and not eng.get("request_slot_bytes"):
         eng["request_slot_bytes"] = TensorCodec(*spec).in_bytes

@@ -36,6 +36,15 @@ def load_runtime():
         if _rt is None:
             from .. import _build
 
+            alt = os.environ.get("RDB_RUNTIME_SO", "")
+            if alt:
+                # a sanitizer build (python -m ray_dynamic_batching_amd._build --sanitize thread):
+                # loaded from its own path, the production extension is never replaced
+                spec = importlib.util.spec_from_file_location("ray_dynamic_batching_amd._rdb_runtime", alt)
+                _rt = importlib.util.module_from_spec(spec)
+                spec.loader.exec_module(_rt)
+                sys.modules["ray_dynamic_batching_amd._rdb_runtime"] = _rt
+                return _rt
             if os.environ.get("RDB_NO_AUTOBUILD") != "1":
                 _build.build_runtime()
             _rt = importlib.import_module("ray_dynamic_batching_amd._rdb_runtime")

@@ -574,8 +574,11 @@ def test_linear_all_tiles_random(cfg, N):
 def test_linear_v4_tiles(cfg, dtype):
     """The 4-wave VGPR-staged tiles (gemm_v4.h, K % 64 == 0): ragged M / N edges,
     every epilogue combination, both 16-bit dtypes, against the fp32 reference;
-    K % 64 != 0 falls back to an 8-wave tile (still correct)."""
+    K % 64 != 0 falls back to an 8-wave tile (still correct).  Experimental build
+    only: no shipped table uses them (the default build falls back to tile 15)."""
     ops = _ops()
+    if not ops.experimental_kernels_built():
+        pytest.skip("tiles 26..28: opt-in RDB_EXPERIMENTAL_KERNELS build not loaded")
     torch.manual_seed(cfg)
     for M, N, K in ((300, 392, 512), (4096, 768, 768), (129, 200, 3072), (256, 96, 128)):
         x = torch.randn(M, K, device="cuda", dtype=dtype)

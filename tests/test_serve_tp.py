@@ -119,3 +119,38 @@ def test_tp_config_validation():
         serve.deployment(tensor_parallel_size=2, placement_group_bundles=[{"GPU": 1}])(TPEcho)
     d = serve.deployment(tensor_parallel_size=4, ray_actor_options={"num_gpus": 1})(TPEcho)
     assert d.config.tp_bundles() == [(1.0, 0.0)] * 4
+
+
+def test_bad_request_gets_an_error_and_the_group_keeps_running():
+    """A request that is not one model row (wrong shape -> the router falls back
+    to a pickled payload) is answered with an error by rank 0; the group never
+    restarts and the next good requests are served (one bad client
+    request must not crash-loop a TP deployment)."""
+    from ray_dynamic_batching_amd.serve.exceptions import RayServeException
+
+    h = _deploy(2)
+    good = np.ones(16, np.float32)
+    assert h.remote(good).result(timeout_s=60)[8] == 2
+    bad = h.remote(np.ones(5, np.float32))
+    with pytest.raises((RayServeException, RuntimeError, ValueError)):
+        bad.result(timeout_s=60)
+    outs = [h.remote(good) for _ in range(6)]
+    assert all(o.result(timeout_s=60)[8] == 2 for o in outs)
+    c, info = _group(2)
+    assert info["restarts"] == 0 and info["epoch"] == 0
+
+
+def test_stopping_a_tp_replica_forgets_its_group():
+    """Deleting the deployment stops the gang and erases the agent's Group entry
+    (every TP stop leaked one Group)."""
+    h = _deploy(2)
+    assert h.remote(np.ones(16, np.float32)).result(timeout_s=60)[8] == 2
+    from ray_dynamic_batching_amd.serve.controller import get_controller
+
+    c = get_controller()
+    assert c.agent.num_groups() == 1
+    serve.delete("default")
+    deadline = time.time() + 30
+    while c.agent.num_groups() and time.time() < deadline:
+        time.sleep(0.1)
+    assert c.agent.num_groups() == 0
