@@ -55,6 +55,13 @@ class BertConfig:
         return BertConfig(**d)
 
 
+def bert_tile_signature(cfg: BertConfig, backend: str = "hip"):
+    """Key of the shipped MI355X tile tables (runtime.engine.shipped_tile_table):
+    only the BERT-base dims were tuned, only for the HIP kernels."""
+    base = (cfg.hidden, cfg.heads, cfg.intermediate) == (768, 12, 3072)
+    return f"bert_L{cfg.layers}_S{cfg.seq_len}" if base and backend == "hip" else None
+
+
 class BertForSequenceClassification:
     """Weights are plain tensors (random N(0, 0.02) init, as BERT's initializer)."""
 
@@ -66,10 +73,7 @@ class BertForSequenceClassification:
         if backend == "hip" and self.device.type != "cuda":
             raise ValueError("the hip backend needs a GPU device")
         self.backend = backend
-        # shipped MI355X tile tables are keyed by this (runtime.engine.shipped_tile_table);
-        # only the BERT-base dims were tuned
-        base = (cfg.hidden, cfg.heads, cfg.intermediate) == (768, 12, 3072)
-        self.tile_signature = f"bert_L{cfg.layers}_S{cfg.seq_len}" if base and backend == "hip" else None
+        self.tile_signature = bert_tile_signature(cfg, backend)
         self.cls_only_last_layer = True
         # deferred LayerNorm (ops.linear_ln): the GEMMs around each LayerNorm
         # carry it, no LayerNorm kernel runs inside the layer stack

@@ -435,12 +435,15 @@ class Engine {
     else launcher_ = std::thread([this] { launcher_loop(); });
   }
   void stop() {
-    if (!running_) return;
-    running_ = false;
+    // The threads may have ended on their own (a launcher error, a TP follower
+    // after the leader's STOP) with running_ already false: they are still
+    // joined here -- a joinable std::thread reaching ~Engine would terminate().
+    const bool was_running = running_.exchange(false);
+    if (!was_running && !launcher_.joinable() && !completer_.joinable()) return;
     for (int i = 0; i < n_sess_.load(); ++i) sess_ptr_[i].load()->ring.ring_bell();
     cv_.notify_all();
     if (launcher_.joinable()) launcher_.join();   // a TP launcher re-checks running_ every 50 ms on the ring
-    if (bcast_) {
+    if (bcast_ && !bcast_->closed()) {
       // leader (the ring's only writer, its launcher has exited): a STOP record
       // for the followers (bounded wait), then close -- which also wakes anyone
       // still blocked on the ring; a follower closing tells the leader the group broke

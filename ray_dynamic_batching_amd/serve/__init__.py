@@ -12,7 +12,7 @@
 """
 from .api import Application, Deployment, delete, deployment, get_app_handle, get_deployment_handle, grpc_port, \
     http_port, metrics_text, run, shutdown, start, status
-from .batching import batch
+from .batching import batch, stack_to_device
 from .config import AutoscalingConfig, DeploymentConfig, EngineConfig
 from .context import get_replica_context
 from .exceptions import BackPressureError, RayServeException, RequestCancelledError, RequestDroppedError
@@ -24,7 +24,7 @@ from .servable import TensorCodec, model_deployment
 
 __all__ = [
     "ingress",
-    "Application", "Deployment", "deployment", "batch", "run", "start", "shutdown", "delete", "status",
+    "Application", "Deployment", "deployment", "batch", "stack_to_device", "run", "start", "shutdown", "delete", "status",
     "get_app_handle", "get_deployment_handle", "get_replica_context", "multiplexed", "get_multiplexed_model_id",
     "DeploymentHandle", "DeploymentResponse", "DeploymentResponseGenerator", "AutoscalingConfig",
     "DeploymentConfig", "EngineConfig", "BackPressureError", "RayServeException", "RequestCancelledError",

@@ -24,6 +24,7 @@ import asyncio
 import functools
 import inspect
 import logging
+import threading
 import time
 from dataclasses import dataclass, field
 from typing import Any, Callable, Dict, List, Optional, Tuple
@@ -371,3 +372,60 @@ def batch(_func: Optional[Callable] = None, /, max_batch_size: int = 10, batch_w
         return wrapper
 
     return deco(_func) if _func is not None else deco
+
+
+class _PinnedStager:
+    """Per-thread pinned host staging buffer + side stream for ``stack_to_device``."""
+
+    def __init__(self):
+        self.buf = None
+        self.stream = None
+        self.event = None
+
+
+_stagers = threading.local()
+
+
+def stack_to_device(items, device="cuda", dtype=None):
+    """Assemble a ``@serve.batch`` batch of same-shape arrays / CPU tensors in a
+    pinned host staging buffer and copy it to ``device`` with
+    ``non_blocking=True`` on a side stream; the caller's current stream waits on
+    that copy (an event), so the returned device tensor is ready for the next
+    kernel without a host sync.  The staging buffer is reused across batches
+    (grown when needed); the copy of batch k is retired before batch k+1 rewrites
+    it.  On a CPU ``device`` it is a plain ``torch.stack``.
+
+    The reference idiom (release/serve_tests/workloads/resnet_50.py:50-57) does
+    ``torch.stack(images).cuda()``: a pageable, synchronous H2D per batch."""
+    import numpy as np
+    import torch
+
+    xs = [torch.from_numpy(np.asarray(x)) if not isinstance(x, torch.Tensor) else x for x in items]
+    if not xs:
+        raise ValueError("stack_to_device: empty batch")
+    dev = torch.device(device)
+    if dev.type != "cuda":
+        out = torch.stack(xs)
+        return out.to(dtype) if dtype is not None else out
+    st = getattr(_stagers, "s", None)
+    if st is None:
+        st = _stagers.s = _PinnedStager()
+        st.stream = torch.cuda.Stream(device=dev)
+        st.event = torch.cuda.Event()
+    shape = (len(xs),) + tuple(xs[0].shape)
+    n = int(np.prod(shape))
+    src_dtype = xs[0].dtype
+    if st.buf is None or st.buf.numel() < n or st.buf.dtype != src_dtype:
+        st.event.synchronize()
+        st.buf = torch.empty(max(n, 1), dtype=src_dtype, pin_memory=True)
+    st.event.synchronize()                         # the previous batch's copy has left the buffer
+    host = st.buf[:n].view(shape)
+    torch.stack(xs, out=host)
+    cur = torch.cuda.current_stream(dev)
+    st.stream.wait_stream(cur)                     # the destination's allocator order
+    with torch.cuda.stream(st.stream):
+        out = host.to(dev, non_blocking=True)
+        st.event.record(st.stream)
+    cur.wait_event(st.event)
+    out.record_stream(cur)
+    return out.to(dtype) if dtype is not None else out

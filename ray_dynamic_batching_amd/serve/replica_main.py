@@ -247,6 +247,7 @@ def _run_python(spec, cfg, job, r, stop, ctx) -> int:
     import cloudpickle
 
     from ..runtime import job as rjob
+    from . import tensor_wire
     from .handle import RequestMeta
     from .replica import UserCallable
 
@@ -275,7 +276,12 @@ def _run_python(spec, cfg, job, r, stop, ctx) -> int:
             inflight[0] -= 1
             return
         try:
-            method, args, kwargs, mux, stream, user_rid = cloudpickle.loads(payload)
+            if kind == tensor_wire.KIND_TENSOR_CALL:
+                # one array argument as raw bytes in the ring slot (no unpickling): a view of the payload
+                method, arg, mux, user_rid, stream = tensor_wire.decode_call(payload)
+                args, kwargs = (arg,), {}
+            else:
+                method, args, kwargs, mux, stream, user_rid = cloudpickle.loads(payload)
             meta = RequestMeta(user_rid, method, mux, stream, spec["app_name"], spec["deployment"])
             if stream:
                 items = []
@@ -290,7 +296,11 @@ def _run_python(spec, cfg, job, r, stop, ctx) -> int:
                 await user.call_stream(meta, args, kwargs, emit)
             else:
                 res = await user.call(meta, args, kwargs)
-                if not cons.complete(client, rid, q, ST_OK, t_sub, cloudpickle.dumps(res), KIND_PICKLE):
+                if tensor_wire.result_encodable(res):
+                    out, okind = tensor_wire.encode_result(res), tensor_wire.KIND_TENSOR_RESULT
+                else:
+                    out, okind = cloudpickle.dumps(res), KIND_PICKLE
+                if not cons.complete(client, rid, q, ST_OK, t_sub, out, okind):
                     logger.error("result of request %d too large for the completion slot", rid)
         except Exception as e:
             cons.complete(client, rid, q, ST_ERROR, t_sub, _dump_exc(e), KIND_PICKLE)

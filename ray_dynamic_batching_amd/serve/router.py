@@ -23,6 +23,7 @@ from typing import Any, Callable, Deque, Dict, List, Optional, Tuple
 
 from .exceptions import (BackPressureError, DeploymentUnavailableError, RayServeException, ReplicaDiedError,
                          RequestCancelledError)
+from . import tensor_wire
 from .handle import DeploymentResponse, DeploymentResponseGenerator, RequestMeta, StreamSink
 
 logger = logging.getLogger("ray_dynamic_batching_amd.serve")
@@ -79,6 +80,7 @@ class RouterMetrics:
         self.num_queued = 0
         self.num_rejected_backpressure = 0
         self.num_retries = 0
+        self.num_raw_tensor_calls = 0     # array arguments sent as raw bytes (tensor_wire), not pickled
 
 
 class LocalRouter:
@@ -331,6 +333,13 @@ class ShmRouter:
         if self.codec is not None and not meta.stream and meta.method_name == "__call__" and len(args) == 1 \
                 and not kwargs and self.codec.accepts(args[0]):
             payload, kind = self.codec.encode(args[0]), KIND_TENSOR
+        elif self.codec is None and tensor_wire.encodable(args, kwargs):
+            # one array / CPU tensor argument to a Python deployment (the @serve.batch
+            # GPU idiom): header + raw bytes in the ring slot, never cloudpickled
+            payload = tensor_wire.encode_call(meta.method_name, args[0], meta.multiplexed_model_id or "",
+                                              meta.request_id or "", meta.stream)
+            kind = tensor_wire.KIND_TENSOR_CALL
+            self.metrics.num_raw_tensor_calls += 1
         else:
             import cloudpickle
 
@@ -518,8 +527,12 @@ class _ShmClientHub:
                 if sink[0] == "stream":
                     self._settle(lambda: _settle_sink(sink, "end", None))
                 else:
-                    val = codec.decode(payload) if kind == KIND_TENSOR else (
-                        cloudpickle.loads(payload) if payload else None)
+                    if kind == KIND_TENSOR:
+                        val = codec.decode(payload)
+                    elif kind == tensor_wire.KIND_TENSOR_RESULT:
+                        val = tensor_wire.decode_result(payload)
+                    else:
+                        val = cloudpickle.loads(payload) if payload else None
                     self._settle(lambda: _settle_sink(sink, "ok", val))
             elif st == St.ERROR:
                 self._fail(sink, cloudpickle.loads(payload) if payload else RayServeException("replica error"))

@@ -36,23 +36,26 @@ def test_bench_two_ranks_echo_backend(ingress):
 
 def test_bench_resolves_shipped_tile_table():
     """bench.py's default (--tile-table auto) replays the MI355X table shipped for
-    the headline config; other configs / 'none' / non-HIP backends tune at start-up."""
-    import argparse
-    import importlib.util
+    the headline config -- through the same resolver a Serve-deployed replica uses
+    (runtime.engine.resolve_tile_table, keyed by the model's tile signature);
+    other configs / 'none' / non-HIP backends tune at start-up."""
+    from types import SimpleNamespace
 
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(root, "bench.py"))
-    bench = importlib.util.module_from_spec(spec)
-    spec.loader.exec_module(bench)
-    a = argparse.Namespace(tile_table="auto", backend="hip", layers=12, seq=128, max_batch=32, compute_streams=2,
-                           pipeline_depth=4)
-    p = bench._tile_table(a)
+    from ray_dynamic_batching_amd.models.bert import BertConfig, bert_tile_signature
+    from ray_dynamic_batching_amd.runtime.engine import resolve_tile_table
+
+    def model(layers=12, backend="hip"):
+        return SimpleNamespace(tile_signature=bert_tile_signature(BertConfig(layers=layers, seq_len=128), backend))
+
+    p = resolve_tile_table("auto", model(), 32, 2, 4)
     assert p.endswith("mi355x_bert_L12_S128_B32_cs2_d4.json") and os.path.exists(p)
     table = json.load(open(p))
     assert any(k[0] == "gemm" and k[2:5] == [4096, 3072, 768] for k, _ in table)      # the bs32 FFN-up entry
-    assert bench._tile_table(argparse.Namespace(**dict(vars(a), layers=2))) == ""
-    assert bench._tile_table(argparse.Namespace(**dict(vars(a), tile_table="none"))) == ""
-    assert bench._tile_table(argparse.Namespace(**dict(vars(a), backend="torch"))) == ""
+    assert resolve_tile_table("auto", model(layers=2), 32, 2, 4) == ""
+    assert resolve_tile_table("none", model(), 32, 2, 4) == ""
+    assert resolve_tile_table("auto", model(backend="torch"), 32, 2, 4) == ""
+    src = open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "bench.py")).read()
+    assert "resolve_tile_table(" in src
 
 
 @pytest.mark.parametrize("n", [2, 4, 8])

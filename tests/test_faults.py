@@ -30,7 +30,10 @@ def env_knobs():
 
 def test_replica_killer_agent_restarts_and_requests_complete(env_knobs):
     env_knobs["RDB_FAULT_KILL_AFTER_BATCHES"] = "6"
-    h = serve.run(Mul.options(health_check_timeout_s=5).bind(3), mode="process")
+    # a replica that dies every 6 batches takes every request it holds with it:
+    # give them a re-dispatch budget above the default 3 (the cap exists for a
+    # request that kills every replica it reaches, tests/test_router_retry.py)
+    h = serve.run(Mul.options(health_check_timeout_s=5, max_request_retries=20).bind(3), mode="process")
     outs = [h.remote(i) for i in range(120)]
     assert [o.result(timeout_s=120) for o in outs] == [3 * i for i in range(120)]
     from ray_dynamic_batching_amd.serve.controller import get_controller

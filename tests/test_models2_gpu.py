@@ -80,7 +80,7 @@ def test_serve_gpu_replica_killer_restart(monkeypatch):
     fac = factories.bert_base(layers=2)
     d = serve.model_deployment(fac, "bert", max_batch_size=8, batch_wait_timeout_s=0.002,
                                ray_actor_options={"num_gpus": 1}, max_ongoing_requests=16,
-                               health_check_timeout_s=60)
+                               health_check_timeout_s=60, max_request_retries=20)
     try:
         h = serve.run(d.bind(), mode="process")
         ids = np.random.default_rng(0).integers(1, 30000, size=(120, 128)).astype(np.int32)

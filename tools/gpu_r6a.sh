@@ -13,5 +13,9 @@ timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 --json-out $O/b
 timeout -k 10 400 python bench/serve_bench.py --model bert-base --closed 96 --seconds 5 \
     --json-out $O/direct.json > $O/direct.log 2>&1 &&
 timeout -k 10 500 python bench/serve_bench.py --model bert-base --closed 96 --seconds 5 --via-serve \
-    --json-out $O/via_serve.json > $O/via_serve.log 2>&1
+    --json-out $O/via_serve.json > $O/via_serve.log 2>&1 &&
+timeout -k 10 400 python bench/serve_batch_slice.py --seconds 8 --concurrency 64 \
+    --json-out $O/slice.json > $O/slice.log 2>&1 &&
+timeout -k 10 400 python bench/serve_bench.py --model resnet50 --closed 96 --seconds 5 \
+    --json-out $O/resnet_direct.json > $O/resnet_direct.log 2>&1
 echo "exit $?"
