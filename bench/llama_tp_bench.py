@@ -33,6 +33,9 @@ def main(argv=None):
     ap.add_argument("--serve", action="store_true", help="serve prompts through the shm rings (TPReplica)")
     ap.add_argument("--requests", type=int, default=400)
     ap.add_argument("--concurrency", type=int, default=16)
+    ap.add_argument("--loop", default="native", choices=["native", "python"],
+                    help="--serve: the native engine TP loop (NativeTP) or the Python TPReplica loop")
+    ap.add_argument("--max-wait-ms", type=float, default=2.0, help="--serve: first-arrival batch timeout")
     ap.add_argument("--json-out", default="")
     ap.add_argument("--checkpoint", default="", help="Hugging Face Llama checkpoint dir (each rank loads its shard)")
     ap.add_argument("--allreduce", default="xgmi", choices=["xgmi", "rccl"],
@@ -141,7 +144,10 @@ def _serve(a, m, world, rank):
                        req_slot_bytes=a.seq * 4, cmp_capacity=2048, cmp_slot_bytes=64)
         job.configure_queue(0, 0, 0, 1024, 0.0, True)
     buckets = [1, 2, 4, 8]
-    rep = TPReplica(m, name if rank == 0 else None, 0, 0, buckets, "tp" if world > 1 else None).capture()
+    if a.loop == "native":
+        return _serve_native(a, m, world, rank, name, job, buckets)
+    rep = TPReplica(m, name if rank == 0 else None, 0, 0, buckets, "tp" if world > 1 else None,
+                    ring=f"{name}_ring").capture()
     if world > 1:
         dist.barrier()
     if rank != 0:
@@ -170,6 +176,59 @@ def _serve(a, m, world, rank):
                    layers=a.layers, prompts_per_s=round(res["ok"] / res["elapsed_s"], 1),
                    p50_ms=round(lat["p50_ms"], 3), p99_ms=round(lat["p99_ms"], 3), ok=res["ok"],
                    mean_batch=round(job.replica_stats(0)["batch_items"] / max(1, job.replica_stats(0)["batches"]), 2),
+                   data="synthetic token ids, random-init weights")
+    print(json.dumps(rep_out), flush=True)
+    if a.json_out:
+        with open(a.json_out, "w") as f:
+            json.dump(rep_out, f, indent=1)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    job.close()
+
+
+def _serve_native(a, m, world, rank, name, job, buckets):
+    """The native TP loop (runtime/tp_replica.py NativeTP): rank 0's engine forms
+    batches (first-arrival timeout), gathers them zero-copy on its copy stream and
+    publishes them on the group's broadcast ring; followers copy + replay the same
+    bucket graph; batch k+1 is formed and copied while batch k computes."""
+    import torch.distributed as dist
+
+    from ray_dynamic_batching_amd.runtime import job as rjob
+    from ray_dynamic_batching_amd.runtime.tp_replica import NativeTP
+
+    if world > 1:
+        dist.barrier()                        # rank 0 created the job
+    ntp = NativeTP(m, name, 0, buckets, rank, world, "tp" if world > 1 else None, f"{name}_ring", 8,
+                   a.max_wait_ms / 1e3, pipeline_depth=2)
+    if world == 1:
+        ntp.unlink()                          # no follower to wait for: drop the ring's name now
+    ntp.start()
+    if world > 1:
+        dist.barrier()
+    if rank != 0:
+        while ntp.check() == "":
+            time.sleep(0.05)
+        ntp.stop()
+        dist.barrier()
+        dist.destroy_process_group()
+        return
+    ids = m.example_input(64, seed=3).cpu()
+    payloads = [ids[i].numpy().tobytes() for i in range(64)]
+    c = rjob.Client(job, 1)
+    lg = rjob.LoadGen(c, 0, payloads)
+    lg.run(min(64, a.requests), a.concurrency, 0.0, 0.0, False, 600.0)   # warmup
+    job.reset_stats()
+    res = lg.run(a.requests, a.concurrency, 0.0, 0.0, True, 600.0)
+    err = ntp.check()
+    st = job.replica_stats(0)
+    ntp.stop()                                # STOP record: the followers leave
+    lat = res["latency"]
+    rep_out = dict(metric="Llama-3-8B bf16 TP prefill serving (<= 8 prompts / batch)", loop="native engine",
+                   tp=world, allreduce=a.allreduce if world > 1 else "none", seq_len=a.seq, layers=a.layers,
+                   prompts_per_s=round(res["ok"] / res["elapsed_s"], 1), p50_ms=round(lat["p50_ms"], 3),
+                   p99_ms=round(lat["p99_ms"], 3), ok=res["ok"], errors=res.get("errors", 0),
+                   mean_batch=round(st["batch_items"] / max(1, st["batches"]), 2), engine_error=err,
                    data="synthetic token ids, random-init weights")
     print(json.dumps(rep_out), flush=True)
     if a.json_out:
