@@ -74,6 +74,9 @@ def main(argv=None):
     ap.add_argument("--max-wait-ms", type=float, default=5.0)
     ap.add_argument("--backend", default="hip")
     ap.add_argument("--json-out", default="")
+    ap.add_argument("--native-client", action="store_true",
+                    help="also drive the deployment's queue with the native closed-loop client")
+    ap.add_argument("--native-concurrency", type=int, default=96)
     a = ap.parse_args(argv)
 
     h = serve.run(ResNet50Batch.bind(a.max_batch, a.max_wait_ms / 1e3, a.backend), name="slice", mode="process")
@@ -132,6 +135,26 @@ def main(argv=None):
         "mean_batch": round((s1["items"] - s0["items"]) / max(1, s1["batches"] - s0["batches"]), 2),
         "raw_tensor_calls": router.metrics.num_raw_tensor_calls, "router_requests": router.metrics.num_router_requests,
     }
+    if a.native_client:
+        # the same deployment driven by the native closed-loop client on its shm queue (the encoded
+        # call payloads the router would send): the replica's own capacity, without this process's
+        # Python handle threads in the loop
+        from ray_dynamic_batching_amd.runtime import job as rjob
+        from ray_dynamic_batching_amd.serve import tensor_wire
+
+        ctrl = get_controller()
+        st = ctrl.apps["slice"]["ResNet50Batch"]
+        j = ctrl.jobs["slice"]
+        lg = rjob.LoadGen(rjob.Client(j), st.model_id, [tensor_wire.encode_call("__call__", im) for im in imgs])
+        lg.run(1000, a.native_concurrency, 0.0, 0.0, False, 300.0)
+        s0 = h.stats.remote().result(timeout_s=60)
+        res = lg.run(int(max(2000, 6000 * a.seconds / 5)), a.native_concurrency, 0.0, 0.0, True, 600.0)
+        s1 = h.stats.remote().result(timeout_s=60)
+        lat = res["latency"]
+        out["native_client"] = {"req_per_s": round(res["ok"] / res["elapsed_s"], 1), "p50_ms": round(lat["p50_ms"], 3),
+                                "p99_ms": round(lat["p99_ms"], 3), "ok": res["ok"], "errors": res.get("errors", 0),
+                                "concurrency": a.native_concurrency,
+                                "mean_batch": round((s1["items"] - s0["items"]) / max(1, s1["batches"] - s0["batches"]), 2)}
     print(json.dumps(out), flush=True)
     if a.json_out:
         with open(a.json_out, "w") as f:

@@ -276,8 +276,9 @@ def _run_python(spec, cfg, job, r, stop, ctx) -> int:
             inflight[0] -= 1
             return
         try:
-            if kind == tensor_wire.KIND_TENSOR_CALL:
+            if kind == tensor_wire.KIND_TENSOR_CALL or (kind == KIND_TENSOR and payload[:4] == tensor_wire.MAGIC):
                 # one array argument as raw bytes in the ring slot (no unpickling): a view of the payload
+                # (kind 0 + the wire magic: a native client -- LoadGen -- submitting encoded calls)
                 method, arg, mux, user_rid, stream = tensor_wire.decode_call(payload)
                 args, kwargs = (arg,), {}
             else:

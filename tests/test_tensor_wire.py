@@ -83,3 +83,30 @@ def test_router_never_pickles_an_array_argument(monkeypatch):
 
     monkeypatch.setattr(cloudpickle, "dumps", guard)
     assert h.remote(np.ones((2, 2), np.float32)).result(timeout_s=60).sum() == 8
+
+
+def test_native_client_drives_a_batch_deployment():
+    """The native load generator's client submits encoded calls (kind 0 + the
+    wire magic) straight to the deployment's queue; the Python worker decodes
+    them as raw arrays (bench/serve_batch_slice.py --native-client)."""
+    import time
+
+    from ray_dynamic_batching_amd.runtime import job as rjob
+    from ray_dynamic_batching_amd.serve.controller import get_controller
+
+    h = serve.run(Doubler.bind(), mode="process")
+    assert h.remote(np.ones((2, 2), np.float32)).result(timeout_s=60).sum() == 8
+    ctrl = get_controller()
+    st = ctrl.apps["default"]["Doubler"]
+    c = rjob.Client(ctrl.jobs["default"])
+    q = c.choose_queue(st.model_id, 0)
+    x = np.arange(16, dtype=np.float32).reshape(4, 4)
+    rid = c.submit(q, tensor_wire.encode_call("__call__", x))
+    got = None
+    t_end = time.time() + 30
+    while got is None and time.time() < t_end:
+        for comp in c.poll(16, 0.2):
+            if comp[0] == rid:
+                got = comp
+    assert got is not None and got[1] == 0 and got[6] == tensor_wire.KIND_TENSOR_RESULT
+    np.testing.assert_array_equal(tensor_wire.decode_result(got[7]), x * 2)
