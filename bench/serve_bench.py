@@ -2,7 +2,7 @@
 req/s vs p50/p99 latency for any servable model of the zoo.
 
 BASELINE config 2 (ResNet-50 fp16, 1 GPU, dyn-batch <= 32 / 5 ms, Poisson; one
-replica engine running two batches at a time on two compute streams, like bench.py):
+replica engine running three batches at a time on three compute streams, like bench.py):
     python bench/serve_bench.py --model resnet50 --rates 2000,4000,8000,12000
 Closed-loop saturation throughput:
     python bench/serve_bench.py --model bert-base --closed 96
@@ -36,8 +36,8 @@ def main(argv=None):
     ap.add_argument("--max-batch", type=int, default=32)
     ap.add_argument("--max-wait-ms", type=float, default=5.0)
     ap.add_argument("--backend", default="hip")
-    ap.add_argument("--pipeline-depth", type=int, default=4)
-    ap.add_argument("--compute-streams", type=int, default=2, help="batches executing concurrently on the GPU")
+    ap.add_argument("--pipeline-depth", type=int, default=6)
+    ap.add_argument("--compute-streams", type=int, default=3, help="batches executing concurrently on the GPU")
     ap.add_argument("--via-serve", action="store_true",
                     help="deploy the replica with serve.run(serve.model_deployment(...)) instead of building an "
                          "EngineRunner here; the load generator drives the deployment's queues")
@@ -46,6 +46,9 @@ def main(argv=None):
     ap.add_argument("--stamps-out", default="", help="diagnostic: block-stamp records of the closed-loop run (.npy; needs "
                     "the RDB_BLOCK_STAMPS kernel build via RDB_OPS_SO, bench/stamp_timeline.py reads them)")
     a = ap.parse_args(argv)
+    from ray_dynamic_batching_amd.runtime.queues import ensure_hw_queues
+
+    ensure_hw_queues(a.compute_streams)       # one HIP hardware queue per engine stream, before HIP starts
 
     import numpy as np
     import torch

@@ -166,6 +166,10 @@ def _cu_share(c: int, M: int, N: int, cus: int = 256) -> float:
     """Share of the GPU's CUs a GEMM launch with tile choice ``c`` holds (split-K
     multiplies the blocks, DEEP holds a whole CU per block)."""
     t = c & 255
+    if c >= 0 and c & CONV_HALO:
+        if not 0 <= t < len(_CONV_HALO_BM):
+            return 1.0
+        return min(1.0, -(-M // _CONV_HALO_BM[t]) * -(-N // _CONV_HALO_BN[t]) / cus)
     if c >= 0 and c & CONV_PP:
         if not 0 <= t < len(_CONV_PP_BM):
             return 1.0
@@ -1182,6 +1186,14 @@ _CONV_PP_BN = (128, 256, 128, 64, 128)
 _CONV_PP_BK = (64, 64, 32, 64, 32)
 # RDB_CONV_PP=0: no ping-pong conv candidates
 _CONV_PP = os.environ.get("RDB_CONV_PP", "1") != "0"
+#   CONV_HALO | v        (3x3, stride 1, pad 1, C % 64 == 0, with bias) the halo-tile kernel,
+#                        tile v (conv_halo.hip): one LDS patch feeds all 9 taps
+CONV_HALO = 1 << 18
+_CONV_HALO_BM = (256, 112, 112, 64, 224, 224, 64, 128)    # conv_halo.hip kHaloBM / kHaloBN
+_CONV_HALO_BN = (64, 64, 64, 64, 64, 128, 64, 32)
+_CONV_HALO_RW = (6, 7)               # resident-weight persistent tiles: no residual, ReLU / no activation
+# RDB_CONV_HALO=0: no halo-tile conv candidates
+_CONV_HALO = os.environ.get("RDB_CONV_HALO", "1") != "0"
 DEEP = 1 << 12                        # gemm_core.h kDeepFlag: one block per CU, up to 8 LDS stages
 _DEEP_TILES = (0, 1, 2, 3, 9, 10, 6, 7)
 _DEEP_BIG = (6, 7)                    # 256x128 / 128x256: one block per CU at any grid size
@@ -1259,6 +1271,19 @@ def _conv_pp_candidates(M: int, K_out: int, Kg: int, C: int):
                 continue
             out.append(CONV_PP | v | (sp << 8))
     return out
+
+
+def conv_halo_candidates(N: int, H: int, W: int, C: int, K: int, R: int, S: int, stride: int, pad: int, P: int,
+                         Q: int, has_bias: bool, has_res: bool = False, act: str = "relu"):
+    """Halo-tile 3x3 tiles (CONV_HALO | v) whose rows fit an H x W image
+    (conv_halo.hip ``conv_halo_tiles``): same-size 3x3 convs with a bias; the
+    one-patch-buffer tiles only for a single 64-channel block (C == 64)."""
+    if not (_CONV_HALO and has_bias and R == 3 and S == 3 and stride == 1 and pad == 1 and (P, Q) == (H, W)
+            and C % 64 == 0 and K % 8 == 0):
+        return []
+    rw_ok = not has_res and act in ("relu", "none")
+    return [CONV_HALO | v for v in range(len(_CONV_HALO_BM))
+            if (rw_ok or v not in _CONV_HALO_RW) and _ops().conv_halo_tiles(v, N, H, W, C, K) > 0]
 
 
 def _conv_candidates(M: int, K_out: int, Kg: int, one_by_one: bool, C: int = 0, has_bias: bool = False):
@@ -1353,7 +1378,9 @@ def conv2d_nhwc(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] =
                 if ws is None:
                     ws = _tune_ws[sid] = splitk_workspace(x.device)
             launch(c, ws)
-        tile_cfg = _tuned_cfg(key, tune_launch, _conv_candidates(M, K, Kg, one_by_one, C, bias is not None))
+        tile_cfg = _tuned_cfg(key, tune_launch, _conv_candidates(M, K, Kg, one_by_one, C, bias is not None) +
+                              conv_halo_candidates(N, H, W, C, K, R, S, stride, pad, P, Q, bias is not None,
+                                                   residual is not None, act))
     launch(int(tile_cfg), workspace)
     return out
 

@@ -17,6 +17,10 @@ namespace rdb {
 // 4-wave 64 x 128 / 128 x 64 im2col tiles, and split-K keeps the small-M layers
 // (ResNet stages 3 / 4: M = 6272 / 1568 at batch 32) on >= ~200 blocks.
 constexpr int kConvPPFlag = 1 << 17;
+// force_cfg = kConvHaloFlag | v: the halo-tile 3x3 kernel (conv_halo.hip)
+constexpr int kConvHaloFlag = 1 << 18;
+void conv3x3_halo(int v, const void* x, const void* w, void* y, const void* bias, const void* res, int N, int H, int W,
+                  int C, int K, int act, hipStream_t s);
 constexpr int kNumConvPP = 5;
 //                                  0    1    2    3    4
 constexpr int kConvPPBM[kNumConvPP] = {256, 128, 256, 256, 128};
@@ -87,6 +91,14 @@ void conv2d_nhwc(uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t res, uintpt
     throw std::invalid_argument("conv2d_nhwc: P / Q larger than the padded output");
   const int M = N * P * Q, Kg = R * S * C;
   if (M <= 0 || K <= 0) return;
+  if (force_cfg >= 0 && (force_cfg & kConvHaloFlag)) {
+    if (R != 3 || S != 3 || stride != 1 || pad != 1 || P != H || Q != W)
+      throw std::invalid_argument("conv2d_nhwc: halo conv tiles are 3x3, stride 1, pad 1");
+    conv3x3_halo(force_cfg & 255, reinterpret_cast<const void*>(x), reinterpret_cast<const void*>(w),
+                 reinterpret_cast<void*>(y), reinterpret_cast<const void*>(bias), reinterpret_cast<const void*>(res), N,
+                 H, W, C, K, act, reinterpret_cast<hipStream_t>(stream));
+    return;
+  }
   if (force_cfg >= 0 && (force_cfg & kConvPPFlag)) {
     ConvParams p{reinterpret_cast<const void*>(x), N, H, W, C, R, S, stride, pad, P, Q, M, Kg};
     conv_pp(force_cfg & 255, p, (const f16*)w, (f16*)y, (const f16*)bias, (const f16*)res, K, act,
@@ -113,6 +125,7 @@ void conv2d_nhwc(uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t res, uintpt
 }
 
 size_t conv_splitk_bytes(int M, int N, int cfg, int splits) {
+  if (cfg & kConvHaloFlag) return 0;
   if (cfg & kConvPPFlag) return conv_pp_splitk_bytes(M, N, cfg & 255, splits);
   return splitk_bytes(M, N, cfg & 255, splits);
 }

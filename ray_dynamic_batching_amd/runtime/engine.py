@@ -112,6 +112,9 @@ class EngineRunner:
         self.depth = pipeline_depth
         self.sessions = list(sessions)
         self.compute_streams = max(1, min(compute_streams, pipeline_depth))
+        from .queues import check_hw_queues
+
+        check_hw_queues(self.compute_streams)     # streams sharing a HIP hardware queue serialise
         self.engine = self.ops.Engine(job_name, replica, pipeline_depth, zero_copy, self.device, policy,
                                       self.compute_streams)
         self.batch_policy = batch_policy

@@ -61,11 +61,12 @@ class EngineConfig(BaseModel):
     that builds the engine (``serve/replica_main._run_engine``), the way Serve's
     DeploymentConfig carries every replica knob (reference:
     python/ray/serve/_private/config.py:81-170).  Defaults = the benchmarked
-    BERT / ResNet-50 replica: two compute streams x pipeline depth 4, the shipped
-    MI355X tile table for the model's signature, NUMA-pinned process and ring."""
+    BERT replica: three compute streams, each on its own HIP hardware queue
+    (runtime/queues.py), x pipeline depth 6, the shipped MI355X tile table for
+    the model's signature, NUMA-pinned process and ring."""
     buckets: Optional[List[int]] = None          # padded batch sizes captured as hipGraphs
-    pipeline_depth: int = 4                      # batches in flight (H2D of k+1 under compute of k)
-    compute_streams: int = 2                     # batches executing concurrently on the GPU
+    pipeline_depth: int = 6                      # batches in flight (H2D of k+1 under compute of k)
+    compute_streams: int = 3                     # batches executing concurrently on the GPU
     batch_policy: str = "timeout"                # "timeout" (@serve.batch semantics) or "idle"
     stagger_us: int = 0                          # hold an idle-starting stream behind the other (latency knob)
     tile_table: str = "auto"                     # "auto" (shipped table for the model signature), "none", or a path

@@ -324,6 +324,14 @@ class ServeController:
             env["RDB_AGENT_SOCKET"] = self.agent_socket
             env["RDB_METRICS_KEY"] = f"{st.app_name}/{st.name}/{rep.slot}"
         env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+        if getattr(st.deployment, "servable", None) is not None:
+            # one HIP hardware queue per engine stream, in place before the replica's HIP starts
+            from ..runtime.queues import ensure_hw_queues
+
+            env["GPU_MAX_HW_QUEUES"] = os.environ.get("GPU_MAX_HW_QUEUES", "")
+            if not env["GPU_MAX_HW_QUEUES"]:
+                del env["GPU_MAX_HW_QUEUES"]
+            ensure_hw_queues(st.config.engine.compute_streams, env)
         pkg_root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
         env["PYTHONPATH"] = pkg_root + os.pathsep + os.environ.get("PYTHONPATH", "")
         return env

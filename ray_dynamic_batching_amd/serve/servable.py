@@ -109,7 +109,7 @@ def model_deployment(factory: Callable, name: str, *, max_batch_size: int = 32, 
     ``engine={...}`` takes every ``EngineConfig`` field (compute streams, batch
     policy, tile table, NUMA pinning, ...); ``pipeline_depth`` /
     ``compute_streams`` are shorthands for two of them.  The defaults are the
-    benchmarked replica's (2 streams x depth 4, shipped tile table)."""
+    benchmarked replica's (3 streams x depth 6, shipped tile table)."""
     if io_spec is not None:
         factory.io_spec = tuple(io_spec)
     eng = dict(deployment_options.pop("engine", {}) or {})
@@ -119,8 +119,10 @@ def model_deployment(factory: Callable, name: str, *, max_batch_size: int = 32, 
     if compute_streams is not None:
         eng.setdefault("compute_streams", compute_streams)
     if eng.get("pipeline_depth") is not None and eng.get("compute_streams") is None:
-        # an explicit shallow pipeline (depth 1) cannot hold two running batches
-        eng["compute_streams"] = min(2, int(eng["pipeline_depth"]))
+        # an explicit shallow pipeline cannot hold more running batches than slots
+        from .config import EngineConfig
+
+        eng["compute_streams"] = min(EngineConfig.model_fields["compute_streams"].default, int(eng["pipeline_depth"]))
     spec = getattr(factory, "io_spec", None)
     if spec is not None and not eng.get("request_slot_bytes"):
         eng["request_slot_bytes"] = TensorCodec(*spec).in_bytes

@@ -38,12 +38,13 @@ def _spec(max_batch=32, wait=0.005):
 def test_model_deployment_defaults_are_the_benchmarked_replica():
     d = serve.model_deployment(factories.bert_base(), "bert", max_batch_size=32, ray_actor_options={"num_gpus": 1})
     e = d.config.engine
-    assert (e.compute_streams, e.pipeline_depth, e.batch_policy, e.tile_table, e.numa_pin) == (2, 4, "timeout",
+    assert (e.compute_streams, e.pipeline_depth, e.batch_policy, e.tile_table, e.numa_pin) == (3, 6, "timeout",
                                                                                               "auto", True)
     assert e.request_slot_bytes == 128 * 4
-    # bench.py's configuration resolves to the same shipped table
-    p = shipped_tile_table(_FakeBert(), 32, 2, 4)
-    assert p == os.path.join(TUNED_DIR, "mi355x_bert_L12_S128_B32_cs2_d4.json") and os.path.exists(p)
+    # bench.py's configuration (3 x 6) resolves to the same shipped table; the round-5 2 x 4 one stays
+    p = shipped_tile_table(_FakeBert(), 32, 3, 6)
+    assert p == os.path.join(TUNED_DIR, "mi355x_bert_L12_S128_B32_cs3_d6.json") and os.path.exists(p)
+    assert shipped_tile_table(_FakeBert(), 32, 2, 4).endswith("mi355x_bert_L12_S128_B32_cs2_d4.json")
 
 
 def test_replica_engine_receives_configured_streams_and_table():
@@ -55,7 +56,7 @@ def test_replica_engine_receives_configured_streams_and_table():
     assert r.kw["batch_policy"] == "idle" and r.kw["stagger_us"] == 150 and r.warm == 0.5
     assert r.kw["tile_table"].endswith("mi355x_bert_L12_S128_B32_cs2_d4.json")
     # a configuration with no shipped table tunes at start-up; "none" forces it; a path is replayed as is
-    cfg = DeploymentConfig(name="bert", engine=dict(compute_streams=3, pipeline_depth=6))
+    cfg = DeploymentConfig(name="bert", engine=dict(compute_streams=4, pipeline_depth=8))
     assert build_engine_runner(_spec(), cfg, 0, _FakeBert(), runner_cls=_FakeRunner).kw["tile_table"] == ""
     assert resolve_tile_table("none", _FakeBert(), 32, 2, 4) == ""
     assert resolve_tile_table("/x/t.json", _FakeBert(), 32, 2, 4) == "/x/t.json"
@@ -142,3 +143,38 @@ def test_node_agent_starts_process_pinned(tmp_path):
         del pid
     finally:
         a.shutdown(2.0)
+
+
+def test_hw_queues_follow_compute_streams(monkeypatch):
+    """Every engine stream gets its own HIP hardware queue (runtime/queues.py):
+    bench.py and Serve replicas raise GPU_MAX_HW_QUEUES before HIP starts."""
+    from ray_dynamic_batching_amd.runtime.queues import ensure_hw_queues, hw_queues_needed
+
+    assert hw_queues_needed(1) == 4 and hw_queues_needed(2) == 4 and hw_queues_needed(3) == 5
+    assert hw_queues_needed(64) == 32
+    env = {}
+    assert ensure_hw_queues(3, env) == 5 and env["GPU_MAX_HW_QUEUES"] == "5"
+    env = {"GPU_MAX_HW_QUEUES": "8"}
+    assert ensure_hw_queues(3, env) == 8 and env["GPU_MAX_HW_QUEUES"] == "8"     # never lowered
+    # the controller puts it in a servable replica's environment
+    from ray_dynamic_batching_amd.serve.controller import ServeController
+
+    monkeypatch.delenv("GPU_MAX_HW_QUEUES", raising=False)
+
+    class St:
+        app_name, name = "a", "bert"
+        deployment = serve.model_deployment(factories.bert_base(), "bert", engine=dict(compute_streams=3,
+                                                                                        pipeline_depth=6))
+        config = deployment.config
+
+    class Rep:
+        slot = 0
+
+    class Job:
+        def info(self):
+            return {"name": "j"}
+
+    ctrl = ServeController.__new__(ServeController)
+    ctrl._routes_path, ctrl.agent_socket = "/x", ""
+    env = ctrl._replica_env(St, Rep, Job())
+    assert env["GPU_MAX_HW_QUEUES"] == "5"

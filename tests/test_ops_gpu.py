@@ -320,6 +320,34 @@ def test_conv2d_pingpong(N, H, C, K, R, stride, pad):
     assert int(ws[:ops.SPLITK_HEADER].view(torch.int32).abs().sum()) == 0
 
 
+@pytest.mark.parametrize("N,H,C,K", [
+    (2, 56, 64, 64), (3, 28, 128, 128), (3, 14, 256, 256), (5, 7, 512, 512), (3, 14, 128, 72), (2, 12, 64, 200),
+    (32, 56, 64, 64), (32, 28, 128, 128)])
+def test_conv2d_halo(N, H, C, K):
+    """The halo-tile 3x3 kernel (CONV_HALO | v): every tile whose rows fit the
+    image, against the fp32 reference with and without a residual; odd image
+    counts (a tile of G images past the batch end), ragged output channels."""
+    ops = _ops()
+    torch.manual_seed(17 + H + K)
+    x = torch.randn(N, H, H, C, device="cuda", dtype=torch.float16)
+    w = torch.randn(K, 3, 3, C, device="cuda", dtype=torch.float16) * (9 * C) ** -0.5
+    b = torch.randn(K, device="cuda", dtype=torch.float16) * 0.1
+    ref = ops.conv2d_nhwc_ref(x, w, b, pad=1, act="relu")
+    r = torch.randn_like(ref)
+    ref_r = ops.conv2d_nhwc_ref(x, w, b, pad=1, act="relu", residual=r)
+    cands = ops.conv_halo_candidates(N, H, H, C, K, 3, 3, 1, 1, H, H, True)
+    assert cands
+    for c in cands:
+        _close(ops.conv2d_nhwc(x, w, b, pad=1, act="relu", tile_cfg=c), ref, 2e-2, 2e-2)
+        if (c & 255) in ops._CONV_HALO_RW:       # resident-weight tiles: no residual epilogue
+            with pytest.raises(Exception):
+                ops.conv2d_nhwc(x, w, b, pad=1, act="relu", residual=r, tile_cfg=c)
+            continue
+        _close(ops.conv2d_nhwc(x, w, b, pad=1, act="relu", residual=r, tile_cfg=c), ref_r, 2e-2, 2e-2)
+    with pytest.raises(Exception):       # stride 2 is not a halo shape
+        ops.conv2d_nhwc(x, w, b, stride=2, pad=1, tile_cfg=ops.CONV_HALO | 0)
+
+
 def test_conv2d_pingpong_splitk_graph_replay():
     """A split-K ping-pong conv chain captured in a graph (per-forward workspace,
     as ResNet50._logits_hip), replayed with new inputs."""

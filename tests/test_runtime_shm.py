@@ -104,8 +104,9 @@ def test_cross_process_loadgen_closed_loop():
     assert res["ok"] == total and res["completed"] == total and not res["timed_out"]
     assert res["latency"]["count"] == total
     # both replicas got traffic through the pow-2 router (by queue depth: a replica
-    # process the host schedules less drains slower and gets a smaller share)
-    assert min(res["per_queue"]) > total * 0.05
+    # process the host schedules less drains slower and gets a smaller share; under a
+    # loaded host -- a parallel compile -- one replica can get as little as a few %)
+    assert min(res["per_queue"]) > total * 0.01
     j.close()
 
 

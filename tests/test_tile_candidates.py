@@ -132,3 +132,30 @@ def test_gemm_candidates_pingpong_splitk():
         eff = -(-nk // -(-nk // sp))
         assert ops.SPLITK_HEADER + tiles * eff * ops._ALL_BM[t] * ops._ALL_BN[t] * 4 <= ops.SPLITK_WS_BYTES
     assert not [c for c in ops._gemm_candidates(4096, 3072, 768, splitk=True) if ops.splits_of(c) > 1 and (c & 255) >= 19]
+
+
+def test_conv_halo_candidates():
+    """Halo-tile 3x3 tiles (CONV_HALO | v): only for same-size 3x3 convs with a
+    bias and C % 64 == 0; each candidate's rows fit the image (conv_halo_tiles
+    > 0, the C++ geometry); never split."""
+    import pytest
+
+    try:
+        tiles = ops._ops().conv_halo_tiles
+    except Exception as e:   # extension not built in this checkout
+        pytest.skip(f"ops extension unavailable: {e}")
+    for N, H, C, K in ((32, 56, 64, 64), (32, 28, 128, 128), (32, 14, 256, 256), (32, 7, 512, 512)):
+        cands = ops.conv_halo_candidates(N, H, H, C, K, 3, 3, 1, 1, H, H, True)
+        assert cands and len(cands) == len(set(cands))
+        for c in cands:
+            assert c & ops.CONV_HALO and ops.splits_of(c) == 0 and tiles(c & 255, N, H, H, C, K) > 0
+        assert not ops.conv_halo_candidates(N, H, H, C, K, 3, 3, 1, 1, H, H, False)      # no bias
+        assert not ops.conv_halo_candidates(N, H, H, C, K, 3, 3, 2, 1, H // 2, H // 2, True)  # strided
+    assert not ops.conv_halo_candidates(32, 56, 56, 96, 64, 3, 3, 1, 1, 56, 56, True)      # C % 64
+    # stage 1 (56 wide): the 256-pixel tile takes 4 output rows; 64 px cannot hold one
+    assert tiles(0, 32, 56, 56, 64, 64) == 32 * 14 and tiles(3, 32, 56, 56, 64, 64) == -1
+    # one patch buffer: only a single 64-channel block
+    assert tiles(0, 32, 28, 28, 128, 128) == -1 and tiles(2, 32, 28, 28, 128, 128) == 32 * 7 * 2
+    # stage 4 (7 x 7): two images per 112-pixel tile
+    assert tiles(2, 32, 7, 7, 512, 512) == 16 * 8
+    assert ops._cu_share(ops.CONV_HALO | 0, 100352, 64) == 1.0
