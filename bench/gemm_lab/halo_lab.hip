@@ -4,6 +4,7 @@
 // issue, MFMA taps, epilogue) and the kernel span.  Never part of the real build.
 //   hipcc -O3 -std=c++17 --offload-arch=gfx950 -I../../ray_dynamic_batching_amd/ops/csrc \
 //         -DRDB_HALO_STAMPS halo_lab.hip -o halo_lab && ./halo_lab 6 32 56 64 64
+// (without -DRDB_HALO_STAMPS: the real kernels, timing only -- for counter runs)
 #include "conv_halo.hip"
 #include <cstdio>
 #include <cstdlib>
@@ -40,7 +41,9 @@ int main(int argc, char** argv) {
   float ms = 0.f;
   RDB_HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
   static unsigned long long st[4096][8];
+#ifdef RDB_HALO_STAMPS
   RDB_HIP_CHECK(hipMemcpyFromSymbol(st, HIP_SYMBOL(rdb_halo_stamps), sizeof(st)));
+#endif
   double sum[8] = {0};
   int nw_ = 0;
   unsigned long long tmin = ~0ull, tmax = 0;
