@@ -1189,9 +1189,9 @@ _CONV_PP = os.environ.get("RDB_CONV_PP", "1") != "0"
 #   CONV_HALO | v        (3x3, stride 1, pad 1, C % 64 == 0, with bias) the halo-tile kernel,
 #                        tile v (conv_halo.hip): one LDS patch feeds all 9 taps
 CONV_HALO = 1 << 18
-_CONV_HALO_BM = (256, 112, 112, 64, 224, 224, 64, 128, 64, 112, 64, 112, 256)    # conv_halo.hip kHaloBM / kHaloBN
-_CONV_HALO_BN = (64, 64, 64, 64, 64, 128, 64, 32, 64, 128, 128, 64, 64)
-_CONV_HALO_RW = (6, 7, 8, 9, 10, 11, 12)   # persistent resident / register-weight tiles: no residual, ReLU / none
+_CONV_HALO_BM = (256, 112, 112, 64, 224, 224, 64, 128, 256)    # conv_halo.hip kHaloBM / kHaloBN
+_CONV_HALO_BN = (64, 64, 64, 64, 64, 128, 64, 32, 64)
+_CONV_HALO_RW = (6, 7, 8)          # persistent resident-weight tiles: no residual, ReLU / none
 # RDB_CONV_HALO=0: no halo-tile conv candidates
 _CONV_HALO = os.environ.get("RDB_CONV_HALO", "1") != "0"
 DEEP = 1 << 12                        # gemm_core.h kDeepFlag: one block per CU, up to 8 LDS stages

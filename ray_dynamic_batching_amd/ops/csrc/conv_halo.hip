@@ -219,20 +219,24 @@ conv3x3_halo_kernel(const f16* __restrict__ x, const f16* __restrict__ w, f16* _
     const char* pw = smem + W_OFF + (s % WST) * W_BYTES;
     const int r3 = tap / 3;
     const int toff = r3 * g.Wp + (tap - r3 * 3);
+    // both k-halves' fragments are read before the first MFMA: the second half's LDS
+    // latency runs under the first half's MFMAs (k-step 1 is chunk fg + 4 = byte ^ 64)
+    frag wf[2][TN], af[2][TM];
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      const int chunk = ks * 4 + fg;
-      frag wf[TN], af[TM];
 #pragma unroll
-      for (int i = 0; i < TN; ++i) wf[i] = *reinterpret_cast<const frag*>(pw + swz_off(wn * WN + i * 16 + fr, chunk));
+      for (int i = 0; i < TN; ++i)
+        wf[ks][i] = *reinterpret_cast<const frag*>(pw + swz_off(wn * WN + i * 16 + fr, ks * 4 + fg));
 #pragma unroll
-      for (int j = 0; j < TM; ++j) af[j] = *reinterpret_cast<const frag*>(pa + swz_off(prow[j] + toff, chunk));
+      for (int j = 0; j < TM; ++j)
+        af[ks][j] = *reinterpret_cast<const frag*>(pa + (swz_off(prow[j] + toff, fg) ^ (ks << 6)));
+    }
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
       for (int i = 0; i < TN; ++i)
 #pragma unroll
-        for (int j = 0; j < TM; ++j) acc[i][j] = MfmaOp<f16>::mma(wf[i], af[j], acc[i][j]);
-      if constexpr (TM * TN >= 16) __builtin_amdgcn_sched_barrier(0);
-    }
+        for (int j = 0; j < TM; ++j) acc[i][j] = MfmaOp<f16>::mma(wf[ks][i], af[ks][j], acc[i][j]);
   }
   __syncthreads();
 
@@ -540,253 +544,6 @@ conv3x3_halo_rw_kernel(const f16* __restrict__ x, const f16* __restrict__ w, f16
 #endif
 }
 
-// ---- register-weight persistent variant ---------------------------------------------
-// The resident-weight kernel spent ~35 cycles per 16-cycle MFMA re-reading weight
-// fragments from LDS (1 KiB of ds_read_b128 per MFMA at 4 waves: the CU's LDS
-// read bandwidth, bench/gemm_lab/halo_lab.hip stamps).  Here every wave keeps
-// ITS output-channel slice of the weights -- all 9 taps x C/64 channel blocks
-// x 2 MFMA k-steps x TN fragments, 72 * TN * NCB VGPRs -- in registers for the
-// whole launch, so LDS only serves the patch: TM reads per TM x TN MFMAs.  The
-// next patch's DMA pieces are spread one per tap between the MFMAs (an LDS-DMA
-// issue costs 100-185 cycles inside a busy phase) instead of one burst.
-template <int TM, int TN, int WGM, int WGN, int NCB, int PROWS, int NPB>
-__global__ void __launch_bounds__(256, 1)
-conv3x3_halo_rg_kernel(const f16* __restrict__ x, const f16* __restrict__ w, f16* __restrict__ y,
-                       const f16* __restrict__ bias, HaloGeom g, int act, int tpb) {
-  static_assert(WGM * WGN == 4, "4 waves");
-  constexpr int BK = 64;
-  constexpr int WM = TM * 16, WN = TN * 16, BN = WGN * WN;
-  static_assert(PROWS % 32 == 0, "whole 4-wave DMA rounds");
-  static_assert(NPB == 2 || NPB == 3, "patch buffers");
-  constexpr int P_BYTES = PROWS * 128;
-  constexpr int LP = PROWS / 32;
-  static_assert(LP <= 9, "one patch piece per tap");
-  constexpr int S = TM * TN;
-  static_assert(LP + 2 * S < 64, "vmcnt");
-  constexpr int SMEM = NPB * P_BYTES;
-  __shared__ __attribute__((aligned(16))) char smem[SMEM];
-  typedef f16x8 frag;
-
-#ifdef RDB_HALO_STAMPS
-  unsigned long long tk0 = 0, ts0 = 0, ta = 0, tb = 0, sw = 0, sb = 0, si = 0, sc = 0, se = 0;
-  HSTAMP(tk0);
-#endif
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wm = wid / WGN, wn = wid % WGN;
-  const int wid_u = __builtin_amdgcn_readfirstlane(wid);
-  const int fr = lane & 15, fg = lane >> 4;
-
-  const int runs_per_slice = g.tiles_m / tpb;
-  const int tile_n = blockIdx.x / runs_per_slice;
-  const int tm_first = (blockIdx.x - tile_n * runs_per_slice) * tpb;
-  const int n0 = tile_n * BN;
-  const int HW = g.H * g.W, M = g.N * HW;
-  const int bmv = g.G * g.TH * g.W;
-  const int Kg = 9 * g.C;
-  const int THp = g.TH + 2, rb_per_img = g.H / g.TH;
-  const int U = tpb * NCB;
-
-  float bv[TN][4];
-  {
-    const __amdgpu_buffer_rsrc_t bsrc = make_rsrc(bias, (uint32_t)(g.K * 2));
-#pragma unroll
-    for (int i = 0; i < TN; ++i) {
-      const u32x2 raw = bload8(bsrc, (uint32_t)((n0 + wn * WN + i * 16 + fg * 4) * 2));
-      const f16* e = reinterpret_cast<const f16*>(&raw);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) bv[i][q] = (float)e[q];
-    }
-  }
-  // this wave's weight fragments: row n0 + wn*WN + i*16 + fr, 8 channels at fg*8 of each 32-deep k-step
-  frag wr[NCB][9][2][TN];
-  {
-    const __amdgpu_buffer_rsrc_t wsrc = make_rsrc(w, (uint32_t)((size_t)g.K * Kg * 2));
-#pragma unroll
-    for (int i = 0; i < TN; ++i) {
-      const int n = n0 + wn * WN + i * 16 + fr;
-      const uint32_t rowb = n < g.K ? (uint32_t)(n * Kg * 2 + fg * 16) : kOOB;
-#pragma unroll
-      for (int cb = 0; cb < NCB; ++cb)
-#pragma unroll
-        for (int tap = 0; tap < 9; ++tap)
-#pragma unroll
-          for (int ks = 0; ks < 2; ++ks)
-            wr[cb][tap][ks][i] = __builtin_bit_cast(
-                frag, bload16(wsrc, rowb == kOOB ? kOOB : rowb + (uint32_t)((tap * g.C + cb * BK + ks * 32) * 2)));
-    }
-  }
-  vm_wait<0>();      // bias and weights are in registers before the first LDS-DMA is counted
-
-  const __amdgpu_buffer_rsrc_t xsrc = make_rsrc(x, (uint32_t)((size_t)M * g.C * 2));
-  const __amdgpu_buffer_rsrc_t ysrc = make_rsrc(y, (uint32_t)((size_t)M * g.K * 2));
-
-  int pgi[LP], pph[LP], ppw[LP];
-  {
-    int row = dma_row(tid, LP, 0);
-    int gi = row / (THp * g.Wp);
-    int rem = row - gi * THp * g.Wp;
-    int ph = rem / g.Wp, pw = rem - ph * g.Wp;
-#pragma unroll
-    for (int i = 0; i < LP; ++i) {
-      pgi[i] = row < g.PR ? gi : 1 << 20;
-      pph[i] = ph;
-      ppw[i] = pw;
-      row += 8;
-      pw += 8;
-      if (pw >= g.Wp) { pw -= g.Wp; ++ph; }
-      if (ph >= THp) { ph -= THp; ++gi; }
-    }
-  }
-  auto tile_origin = [&](int k, int& n_first, int& p0) {
-    const int tm = tm_first + k;
-    const int grp = tm / rb_per_img;
-    n_first = grp * g.G;
-    p0 = (tm - grp * rb_per_img) * g.TH;
-  };
-  auto issue_piece = [&](int u, int i) {
-    const int k = u / NCB, cb = u - k * NCB;
-    int n_first, p0;
-    tile_origin(k, n_first, p0);
-    const int n = n_first + pgi[i], h = p0 - 1 + pph[i], ww = ppw[i] - 1;
-    const int ch = dma_chunk(tid, dma_row(tid, LP, i));
-    const bool ok = n < g.N && (unsigned)h < (unsigned)g.H && (unsigned)ww < (unsigned)g.W;
-    dma16(xsrc, smem + (u % NPB) * P_BYTES + (wid_u * LP + i) * 1024,
-          ok ? (uint32_t)((((n * g.H + h) * g.W + ww) * g.C + cb * BK) * 2 + ch * 16) : kOOB);
-  };
-  int prow[TM];
-  {
-    const int l0 = wm * WM + fr;
-    const int per = g.TH * g.W;
-    int gi = l0 / per;
-    int rem = l0 - gi * per;
-    int p = rem / g.W, q = rem - p * g.W;
-#pragma unroll
-    for (int j = 0; j < TM; ++j) {
-      prow[j] = wm * WM + j * 16 + fr < bmv ? gi * THp * g.Wp + p * g.Wp + q : 0;
-      q += 16;
-      while (q >= g.W) { q -= g.W; ++p; }
-      while (p >= g.TH) { p -= g.TH; ++gi; }
-    }
-  }
-
-  f32x4 acc[TN][TM];
-#pragma unroll
-  for (int i = 0; i < TN; ++i)
-#pragma unroll
-    for (int j = 0; j < TM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-#pragma unroll
-  for (int i = 0; i < LP; ++i) issue_piece(0, i);
-  if (NPB == 3 && U > 1) {
-#pragma unroll
-    for (int i = 0; i < LP; ++i) issue_piece(1, i);
-  }
-  const bool relu = act == ACT_RELU;
-#ifdef RDB_HALO_STAMPS
-  HSTAMP(ts0);
-#endif
-
-#pragma unroll 1
-  for (int k = 0; k < tpb; ++k) {
-#pragma unroll
-    for (int cb = 0; cb < NCB; ++cb) {
-#ifdef RDB_HALO_STAMPS
-      HSTAMP(ta);
-#endif
-      const int u = k * NCB + cb;
-      // retire P(u); younger in flight: the next patch (NPB 3) and the stores of the tiles ended since
-      const bool end1 = u >= 1 && cb == 0;               // unit u-1 ended a tile
-      const bool end2 = u >= 2 && (NCB == 1 || cb == 1);  // unit u-2 ended a tile
-      int code;
-      if constexpr (NPB == 3) {
-        code = (u + 1 < U ? 1 : 0) + 2 * ((end1 ? 1 : 0) + (end2 ? 1 : 0));
-      } else {
-        code = 2 * (end1 ? 1 : 0);
-      }
-      switch (code) {
-        case 0: vm_wait<0>(); break;
-        case 1: vm_wait<LP>(); break;
-        case 2: vm_wait<S>(); break;
-        case 3: vm_wait<LP + S>(); break;
-        case 4: vm_wait<2 * S>(); break;
-        default: vm_wait<LP + 2 * S>(); break;
-      }
-#ifdef RDB_HALO_STAMPS
-      HSTAMP(tb);
-      sw += tb - ta;
-      ta = tb;
-#endif
-      asm volatile("" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-#ifdef RDB_HALO_STAMPS
-      HSTAMP(tb);
-      sb += tb - ta;
-      ta = tb;
-#endif
-      const bool refill = u + NPB - 1 < U;
-      const char* pa = smem + (u % NPB) * P_BYTES;
-#pragma unroll
-      for (int tap = 0; tap < 9; ++tap) {
-        if (tap < LP && refill) issue_piece(u + NPB - 1, tap);
-        const int toff = (tap / 3) * g.Wp + tap % 3;
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
-          const int chunk = ks * 4 + fg;
-          frag af[TM];
-#pragma unroll
-          for (int j = 0; j < TM; ++j) af[j] = *reinterpret_cast<const frag*>(pa + swz_off(prow[j] + toff, chunk));
-#pragma unroll
-          for (int i = 0; i < TN; ++i)
-#pragma unroll
-            for (int j = 0; j < TM; ++j) acc[i][j] = MfmaOp<f16>::mma(wr[cb][tap][ks][i], af[j], acc[i][j]);
-        }
-      }
-#ifdef RDB_HALO_STAMPS
-      HSTAMP(tb);
-      sc += tb - ta;
-      ta = tb;
-#endif
-      if (cb == NCB - 1) {
-        int n_first, p0;
-        tile_origin(k, n_first, p0);
-        const int m0 = n_first * HW + p0 * g.W;
-#pragma unroll
-        for (int j = 0; j < TM; ++j) {
-          const int l = wm * WM + j * 16 + fr;
-          const int m = m0 + l;
-          const bool mok = l < bmv && m < M;
-#pragma unroll
-          for (int i = 0; i < TN; ++i) {
-            const int n = n0 + wn * WN + i * 16 + fg * 4;
-            float v[4];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-              const float a = acc[i][j][q] + bv[i][q];
-              v[q] = relu ? fmaxf(a, 0.f) : a;
-            }
-            const f16x4 o = {(f16)v[0], (f16)v[1], (f16)v[2], (f16)v[3]};
-            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, o), ysrc,
-                                                  mok && n < g.K ? (uint32_t)((m * g.K + n) * 2) : kOOB, 0, 0);
-            acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-          }
-        }
-      }
-#ifdef RDB_HALO_STAMPS
-      HSTAMP(tb);
-      se += tb - ta;
-#endif
-    }
-  }
-#ifdef RDB_HALO_STAMPS
-  HSTAMP(tb);
-  if (lane == 0 && blockIdx.x * 4 + wid < 4096) {
-    unsigned long long* o = rdb_halo_stamps[blockIdx.x * 4 + wid];
-    o[0] = tb - ts0; o[1] = sw; o[2] = sb; o[3] = si + (ts0 - tk0); o[4] = sc; o[5] = se; o[6] = (unsigned long long)U; o[7] = tk0;
-  }
-#endif
-}
-
 // Tile variants (force_cfg = kConvHaloFlag | v):
 //   v  TM TN WGM WGN  BM x BN  patch rows x buffers  ring  blocks/CU  ResNet-50 bs32 layer
 //   0   4  4  4   1  256 x  64    352 x 1            4     2         stage 1 (56 x 56 x 64): 4 rows x 56
@@ -797,20 +554,17 @@ conv3x3_halo_rg_kernel(const f16* __restrict__ x, const f16* __restrict__ w, f16
 //   5   7  4  2   2  224 x 128    288 x 2            3     1         stage 2 / 3 with the whole 128-channel tile
 //   6   2  2  2   2   64 x  64    192 x 3   resident weights (576 rows), persistent   stage 1: 1 row x 56
 //   7   2  2  4   1  128 x  32    192 x 3   resident weights (576 rows), persistent   stage 2: 4 rows x 28, 32-ch slices
-//   8   1  4  4   1   64 x  64    192 x 3   register weights (C = 64), persistent    stage 1: 1 row x 56
-//  12   4  4  4   1  256 x  64    352 x 2   resident weights (576 rows), persistent   stage 1: 4 rows x 56 (160 KiB LDS)
-//   9   7  2  1   4  112 x 128    192 x 3   register weights (C = 128), persistent   stage 2: 4 rows x 28
-//  10   4  2  1   4   64 x 128    128 x 3   register weights (C = 128), persistent   stage 2: 2 rows x 28
-//  11   7  1  1   4  112 x  64    160 x 3   register weights (C = 256), persistent   stage 3: 7 rows x 14
-// (one patch buffer: a single 64-channel block, C == 64; resident weights: 9 * C/64 * BN <= 576 rows;
-//  register weights: C == 64 * NCB exactly)
-constexpr int kNumHalo = 13;
-constexpr int kHaloBM[kNumHalo] = {256, 112, 112, 64, 224, 224, 64, 128, 64, 112, 64, 112, 256};
-constexpr int kHaloBN[kNumHalo] = {64, 64, 64, 64, 64, 128, 64, 32, 64, 128, 128, 64, 64};
-constexpr int kHaloPM[kNumHalo] = {352, 256, 192, 96, 288, 288, 192, 192, 192, 192, 128, 160, 352};
-constexpr int kHaloNPB[kNumHalo] = {1, 1, 2, 2, 2, 2, 3, 3, 3, 3, 3, 3, 2};
-constexpr int kHaloWR[kNumHalo] = {0, 0, 0, 0, 0, 0, 576, 576, 0, 0, 0, 0, 576};   // resident weight rows (0: none)
-constexpr int kHaloNCB[kNumHalo] = {0, 0, 0, 0, 0, 0, 0, 0, 1, 2, 2, 4, 0};      // register weights: C / 64 (0: none)
+//   8   4  4  4   1  256 x  64    352 x 2   resident weights (576 rows), persistent   stage 1: 4 rows x 56 (160 KiB LDS)
+// (one patch buffer: a single 64-channel block, C == 64; resident weights: 9 * C/64 * BN <= 576 rows.
+//  Measured and dropped: weights held in VGPRs per wave -- loading 72 KiB per wave from L2 costs more
+//  than it saves, and above 256 VGPRs the fragments spill or bounce through AGPRs,
+//  profiles/resnet50_conv_halo_r6.json)
+constexpr int kNumHalo = 9;
+constexpr int kHaloBM[kNumHalo] = {256, 112, 112, 64, 224, 224, 64, 128, 256};
+constexpr int kHaloBN[kNumHalo] = {64, 64, 64, 64, 64, 128, 64, 32, 64};
+constexpr int kHaloPM[kNumHalo] = {352, 256, 192, 96, 288, 288, 192, 192, 352};
+constexpr int kHaloNPB[kNumHalo] = {1, 1, 2, 2, 2, 2, 3, 3, 2};
+constexpr int kHaloWR[kNumHalo] = {0, 0, 0, 0, 0, 0, 576, 576, 576};   // resident weight rows (0: streamed)
 
 // (TH, G) of variant v for an H x W image: the most output rows (then images)
 // whose pixels fit BM and whose patch fits the LDS patch buffer; TH divides H.
@@ -820,7 +574,6 @@ static bool halo_geom(int v, int N, int H, int W, int C, int& TH, int& G) {
   G = 1;
   if (C % 64 != 0 || (kHaloNPB[v] == 1 && C != 64) || W + 2 < 9) return false;
   if (kHaloWR[v] && 9 * (C / 64) * kHaloBN[v] > kHaloWR[v]) return false;
-  if (kHaloNCB[v] && C != 64 * kHaloNCB[v]) return false;
   for (int th = H; th >= 1; --th)
     if (H % th == 0 && th * W <= bm && (th + 2) * (W + 2) <= pm) { TH = th; break; }
   if (TH == 0) return false;
@@ -871,17 +624,6 @@ static void launch_halo_rw(const HaloGeom& g, const f16* x, const f16* w, f16* y
                      act, tpb);
 }
 
-template <int TM, int TN, int WGM, int WGN, int NCB, int PROWS, int NPB>
-static void launch_halo_rg(const HaloGeom& g, const f16* x, const f16* w, f16* y, const f16* bias, int act,
-                           hipStream_t s) {
-  constexpr int BN = WGN * TN * 16;
-  const int tiles_n = (g.K + BN - 1) / BN;
-  const int tpb = rw_tpb(g.tiles_m, tiles_n, device_cus());
-  const dim3 grid(tiles_n * (g.tiles_m / tpb)), block(256);
-  hipLaunchKernelGGL((conv3x3_halo_rg_kernel<TM, TN, WGM, WGN, NCB, PROWS, NPB>), grid, block, 0, s, x, w, y, bias, g,
-                     act, tpb);
-}
-
 int conv_halo_tiles(int v, int N, int H, int W, int C, int K) {
   if (v < 0 || v >= kNumHalo) return -1;
   int TH, G;
@@ -898,7 +640,7 @@ void conv3x3_halo(int v, const void* x, const void* w, void* y, const void* bias
     throw std::invalid_argument("conv2d_nhwc: halo conv tiles need 16-B aligned y / residual");
   if ((size_t)N * H * W * C * 2 >= (size_t(1) << 31) || (size_t)K * 9 * C * 2 >= (size_t(1) << 31))
     throw std::invalid_argument("conv2d_nhwc: halo conv operands must stay under 2 GiB");
-  if ((kHaloWR[v] || kHaloNCB[v]) && (res != nullptr || (act != ACT_NONE && act != ACT_RELU)))
+  if (kHaloWR[v] && (res != nullptr || (act != ACT_NONE && act != ACT_RELU)))
     throw std::invalid_argument("conv2d_nhwc: resident-weight halo tiles: no residual, ReLU or no activation");
   HaloGeom g{N, H, W, C, K, 0, 1, W + 2, 0, 0};
   if (!halo_geom(v, N, H, W, C, g.TH, g.G))
@@ -916,10 +658,6 @@ void conv3x3_halo(int v, const void* x, const void* w, void* y, const void* bias
     case 5: launch_halo<7, 4, 2, 2, 288, 2, 3, 1>(g, xp, wp, yp, bp, rp, act, s); break;
     case 6: launch_halo_rw<2, 2, 2, 2, 192, 3, 576>(g, xp, wp, yp, bp, act, s); break;
     case 7: launch_halo_rw<2, 2, 4, 1, 192, 3, 576>(g, xp, wp, yp, bp, act, s); break;
-    case 8: launch_halo_rg<1, 4, 4, 1, 1, 192, 3>(g, xp, wp, yp, bp, act, s); break;
-    case 9: launch_halo_rg<7, 2, 1, 4, 2, 192, 3>(g, xp, wp, yp, bp, act, s); break;
-    case 10: launch_halo_rg<4, 2, 1, 4, 2, 128, 3>(g, xp, wp, yp, bp, act, s); break;
-    case 11: launch_halo_rg<7, 1, 1, 4, 4, 160, 3>(g, xp, wp, yp, bp, act, s); break;
     default: launch_halo_rw<4, 4, 4, 1, 352, 2, 576>(g, xp, wp, yp, bp, act, s); break;
   }
   RDB_HIP_CHECK(hipGetLastError());
