@@ -54,8 +54,8 @@ def main(argv=None):
         ref = ops.conv2d_nhwc_ref(x, w, b, pad=1, act="relu").float()
         flop = 2.0 * N * H * H * K * 9 * C
         cur = current.get((N, H, H, C, K), -1)
-        choices = [("table", cur)] + [(f"halo{c & 255}", c) for c in
-                                      ops.conv_halo_candidates(N, H, H, C, K, 3, 3, 1, 1, H, H, True)]
+        choices = [("table", cur)] + [(f"halo{c & 255}" + (f"s{ops.splits_of(c)}" if ops.splits_of(c) else ""), c)
+                                      for c in ops.conv_halo_candidates(N, H, H, C, K, 3, 3, 1, 1, H, H, True)]
         if a.choices:
             choices = [ch for ch in choices if ch[0] in a.choices.split(",")]
         ws = [ops.splitk_workspace("cuda") for _ in streams]

@@ -169,7 +169,7 @@ def _cu_share(c: int, M: int, N: int, cus: int = 256) -> float:
     if c >= 0 and c & CONV_HALO:
         if not 0 <= t < len(_CONV_HALO_BM):
             return 1.0
-        return min(1.0, -(-M // _CONV_HALO_BM[t]) * -(-N // _CONV_HALO_BN[t]) / cus)
+        return min(1.0, -(-M // _CONV_HALO_BM[t]) * -(-N // _CONV_HALO_BN[t]) * max(1, (c >> 8) & 15) / cus)
     if c >= 0 and c & CONV_PP:
         if not 0 <= t < len(_CONV_PP_BM):
             return 1.0
@@ -1189,9 +1189,10 @@ _CONV_PP = os.environ.get("RDB_CONV_PP", "1") != "0"
 #   CONV_HALO | v        (3x3, stride 1, pad 1, C % 64 == 0, with bias) the halo-tile kernel,
 #                        tile v (conv_halo.hip): one LDS patch feeds all 9 taps
 CONV_HALO = 1 << 18
-_CONV_HALO_BM = (256, 112, 112, 64, 224, 224, 64, 128, 256)    # conv_halo.hip kHaloBM / kHaloBN
-_CONV_HALO_BN = (64, 64, 64, 64, 64, 128, 64, 32, 64)
+_CONV_HALO_BM = (256, 112, 112, 64, 224, 224, 64, 128, 256, 256)    # conv_halo.hip kHaloBM / kHaloBN
+_CONV_HALO_BN = (64, 64, 64, 64, 64, 128, 64, 32, 64, 64)
 _CONV_HALO_RW = (6, 7, 8)          # persistent resident-weight tiles: no residual, ReLU / none
+_CONV_HALO_SK = (2, 3, 4, 5, 9)    # two-patch-buffer streamed tiles: split-K over the 64-channel blocks
 # RDB_CONV_HALO=0: no halo-tile conv candidates
 _CONV_HALO = os.environ.get("RDB_CONV_HALO", "1") != "0"
 DEEP = 1 << 12                        # gemm_core.h kDeepFlag: one block per CU, up to 8 LDS stages
@@ -1282,8 +1283,25 @@ def conv_halo_candidates(N: int, H: int, W: int, C: int, K: int, R: int, S: int,
             and C % 64 == 0 and K % 8 == 0):
         return []
     rw_ok = not has_res and act in ("relu", "none")
-    return [CONV_HALO | v for v in range(len(_CONV_HALO_BM))
-            if (rw_ok or v not in _CONV_HALO_RW) and _ops().conv_halo_tiles(v, N, H, W, C, K) > 0]
+    out = []
+    for v in range(len(_CONV_HALO_BM)):
+        tiles = _ops().conv_halo_tiles(v, N, H, W, C, K)
+        if tiles <= 0 or (v in _CONV_HALO_RW and not rw_ok):
+            continue
+        out.append(CONV_HALO | v)
+        if v not in _CONV_HALO_SK or not _CONV_SPLITK or tiles >= 256:
+            continue
+        # split-K where the tile grid leaves CUs idle (stages 3 / 4 of ResNet-50 at small batch)
+        ncb = C // 64
+        for sp in (2, 3, 4, 8):
+            cpb = -(-ncb // sp)
+            eff = -(-ncb // cpb)
+            if eff < 2 or eff != sp or tiles * eff > 1024:
+                continue
+            if _ops().conv_halo_ws_bytes(v, N, H, W, C, K, sp) > SPLITK_WS_BYTES:
+                continue
+            out.append(CONV_HALO | v | (sp << 8))
+    return out
 
 
 def _conv_candidates(M: int, K_out: int, Kg: int, one_by_one: bool, C: int = 0, has_bias: bool = False):
@@ -1362,7 +1380,9 @@ def conv2d_nhwc(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] =
             return
         sp = splits_of(c)
         if sp > 1 and ws is None:
-            ws = _private_splitk_ws(x.device, int(_ops().conv_splitk_bytes(M, K, c & ~0xF00, sp)))
+            need = _ops().conv_halo_ws_bytes(c & 255, N, H, W, C, K, sp) if c & CONV_HALO else \
+                _ops().conv_splitk_bytes(M, K, c & ~0xF00, sp)
+            ws = _private_splitk_ws(x.device, int(need))
         fn(*args, _stream(), int(c), _ptr(ws), 0 if ws is None else ws.numel())
 
     if tile_cfg < 0:

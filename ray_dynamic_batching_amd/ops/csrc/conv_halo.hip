@@ -34,6 +34,7 @@ struct HaloGeom {
   int TH, G;           // output rows per tile; images per tile (G > 1 only with TH == H)
   int Wp, PR;          // W + 2; patch rows G * (TH + 2) * Wp
   int tiles_m;         // ceil(N / G) * (H / TH)
+  int cpb;             // split-K: 64-channel blocks per split (gridDim.y splits; cpb = C / 64 unsplit)
 };
 
 // Diagnostic build only (bench/gemm_lab/halo_lab.hip defines RDB_HALO_STAMPS): per-wave
@@ -64,10 +65,17 @@ __device__ __forceinline__ void vm_wait() {
 // WST weight-ring slots; OCC blocks per CU the LDS and register budgets allow
 // (2 keeps a second block -- of this launch or another stream's -- resident to
 // cover the patch latency and the epilogue).
-template <int TM, int TN, int WGM, int WGN, int PROWS, int NPB, int WST, int OCC, bool HAS_RES>
+// SK: split-K over the 64-channel blocks -- split z = blockIdx.y runs blocks
+// [z * cpb, z * cpb + cpb); partial tiles go to `sk_part` and the last split of a
+// tile to arrive at its `sk_cnt` counter adds the others and runs the epilogue
+// (the gemm_core.h hand-off: sc1 stores / loads, relaxed agent-scope counter, the
+// last arriver resets it).  For the small-image layers (ResNet-50 stages 3 / 4:
+// 128 / 64 tiles of 256 px) whose tile grid leaves most CUs idle.
+template <int TM, int TN, int WGM, int WGN, int PROWS, int NPB, int WST, int OCC, bool HAS_RES, bool SK = false>
 __global__ void __launch_bounds__(256, OCC)
 conv3x3_halo_kernel(const f16* __restrict__ x, const f16* __restrict__ w, f16* __restrict__ y,
-                    const f16* __restrict__ bias, const f16* __restrict__ res, HaloGeom g, int act) {
+                    const f16* __restrict__ bias, const f16* __restrict__ res, HaloGeom g, int act,
+                    float* __restrict__ sk_part, int* __restrict__ sk_cnt) {
   static_assert(WGM * WGN == 4, "4 waves");
   constexpr int BK = 64, NT = 256;
   constexpr int WM = TM * 16, WN = TN * 16, BM = WGM * WM, BN = WGN * WN;
@@ -149,17 +157,19 @@ conv3x3_halo_kernel(const f16* __restrict__ x, const f16* __restrict__ w, f16* _
     }
   }
 
-  const int ncb = g.C / BK, nsteps = ncb * 9;
+  // this split's channel blocks [cb0, cb0 + ncb); cb below counts from cb0
+  const int cb0 = SK ? (int)blockIdx.y * g.cpb : 0;
+  const int ncb = SK ? min(g.cpb, g.C / BK - cb0) : g.C / BK, nsteps = ncb * 9;
   auto issue_w = [&](int s) {
     const int cb = s / 9, tap = s - cb * 9;
     char* base = smem + W_OFF + (s % WST) * W_BYTES;
-    const uint32_t add = (uint32_t)((tap * g.C + cb * BK) * 2);
+    const uint32_t add = (uint32_t)((tap * g.C + (cb0 + cb) * BK) * 2);
 #pragma unroll
     for (int i = 0; i < LW; ++i) dma16(wsrc, base + (wid_u * LW + i) * 1024, wof[i] == kOOB ? kOOB : wof[i] + add);
   };
   auto issue_p = [&](int cb) {
     char* base = smem + (NPB == 2 ? (cb & 1) * P_BYTES : 0);
-    const uint32_t add = (uint32_t)(cb * BK * 2);
+    const uint32_t add = (uint32_t)((cb0 + cb) * BK * 2);
 #pragma unroll
     for (int i = 0; i < LP; ++i) dma16(xsrc, base + (wid_u * LP + i) * 1024, poff[i] == kOOB ? kOOB : poff[i] + add);
   };
@@ -239,6 +249,46 @@ conv3x3_halo_kernel(const f16* __restrict__ x, const f16* __restrict__ w, f16* _
         for (int j = 0; j < TM; ++j) acc[i][j] = MfmaOp<f16>::mma(wf[ks][i], af[ks][j], acc[i][j]);
   }
   __syncthreads();
+  if constexpr (SK) {
+    if (gridDim.y > 1) {
+      __shared__ int sk_flag;
+      const int splits = gridDim.y, z = blockIdx.y;
+      const int nwg = g.tiles_m * tiles_n;
+      int* cnt = sk_cnt + t;
+      const __amdgpu_buffer_rsrc_t psrc =
+          make_rsrc(sk_part, (uint32_t)((size_t)nwg * splits * BM * BN * sizeof(float)));
+      auto slot_off = [&](int zz, int i, int j) {
+        return (uint32_t)(((((size_t)t * splits + zz) * (TN * TM) + i * TM + j) * NT + tid) * 16);
+      };
+      if (tid == 0) sk_flag = __hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == splits - 1;
+      __syncthreads();
+      bool last = sk_flag != 0;
+      __syncthreads();
+      if (!last) {
+#pragma unroll
+        for (int i = 0; i < TN; ++i)
+#pragma unroll
+          for (int j = 0; j < TM; ++j)
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i][j]), psrc, slot_off(z, i, j), 0, 16);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0)
+          sk_flag = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == splits - 1;
+        __syncthreads();
+        last = sk_flag != 0;
+      }
+      if (!last) return;
+      if (tid == 0) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      for (int zz = 0; zz < splits; ++zz) {
+        if (zz == z) continue;
+#pragma unroll
+        for (int i = 0; i < TN; ++i)
+#pragma unroll
+          for (int j = 0; j < TM; ++j)
+            acc[i][j] += __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(psrc, slot_off(zz, i, j), 0, 16));
+      }
+    }
+  }
 
   auto go = [&](auto actf) {
     staged_epilogue<f16, f16, BM, BN, SMEM, NT, TM, TN, true, HAS_RES, decltype(actf)>(
@@ -555,16 +605,20 @@ conv3x3_halo_rw_kernel(const f16* __restrict__ x, const f16* __restrict__ w, f16
 //   6   2  2  2   2   64 x  64    192 x 3   resident weights (576 rows), persistent   stage 1: 1 row x 56
 //   7   2  2  4   1  128 x  32    192 x 3   resident weights (576 rows), persistent   stage 2: 4 rows x 28, 32-ch slices
 //   8   4  4  4   1  256 x  64    352 x 2   resident weights (576 rows), persistent   stage 1: 4 rows x 56 (160 KiB LDS)
+//   9   4  4  4   1  256 x  64    352 x 2            4     1         stages 3 / 4 (a 14 x 14 image; four 7 x 7 images), split-K
+// Split-K (force_cfg | splits << 8): the two-patch-buffer streamed tiles (2, 3, 4, 5, 9).
 // (one patch buffer: a single 64-channel block, C == 64; resident weights: 9 * C/64 * BN <= 576 rows.
 //  Measured and dropped: weights held in VGPRs per wave -- loading 72 KiB per wave from L2 costs more
 //  than it saves, and above 256 VGPRs the fragments spill or bounce through AGPRs,
 //  profiles/resnet50_conv_halo_r6.json)
-constexpr int kNumHalo = 9;
-constexpr int kHaloBM[kNumHalo] = {256, 112, 112, 64, 224, 224, 64, 128, 256};
-constexpr int kHaloBN[kNumHalo] = {64, 64, 64, 64, 64, 128, 64, 32, 64};
-constexpr int kHaloPM[kNumHalo] = {352, 256, 192, 96, 288, 288, 192, 192, 352};
-constexpr int kHaloNPB[kNumHalo] = {1, 1, 2, 2, 2, 2, 3, 3, 2};
-constexpr int kHaloWR[kNumHalo] = {0, 0, 0, 0, 0, 0, 576, 576, 576};   // resident weight rows (0: streamed)
+constexpr int kNumHalo = 10;
+constexpr int kHaloBM[kNumHalo] = {256, 112, 112, 64, 224, 224, 64, 128, 256, 256};
+constexpr int kHaloBN[kNumHalo] = {64, 64, 64, 64, 64, 128, 64, 32, 64, 64};
+constexpr int kHaloPM[kNumHalo] = {352, 256, 192, 96, 288, 288, 192, 192, 352, 352};
+constexpr int kHaloNPB[kNumHalo] = {1, 1, 2, 2, 2, 2, 3, 3, 2, 2};
+constexpr int kHaloWR[kNumHalo] = {0, 0, 0, 0, 0, 0, 576, 576, 576, 0};   // resident weight rows (0: streamed)
+
+static bool halo_splittable(int v) { return kHaloNPB[v] == 2 && kHaloWR[v] == 0; }
 
 // (TH, G) of variant v for an H x W image: the most output rows (then images)
 // whose pixels fit BM and whose patch fits the LDS patch buffer; TH divides H.
@@ -584,15 +638,26 @@ static bool halo_geom(int v, int N, int H, int W, int C, int& TH, int& G) {
 
 template <int TM, int TN, int WGM, int WGN, int PROWS, int NPB, int WST, int OCC>
 static void launch_halo(const HaloGeom& g, const f16* x, const f16* w, f16* y, const f16* bias, const f16* res, int act,
-                        hipStream_t s) {
+                        hipStream_t s, int eff, float* part, int* cnt) {
   constexpr int BN = WGN * TN * 16;
-  const dim3 grid(g.tiles_m * ((g.K + BN - 1) / BN)), block(256);
+  const dim3 grid(g.tiles_m * ((g.K + BN - 1) / BN), eff), block(256);
+  if constexpr (NPB == 2) {
+    if (eff > 1) {
+      if (res)
+        hipLaunchKernelGGL((conv3x3_halo_kernel<TM, TN, WGM, WGN, PROWS, NPB, WST, OCC, true, true>), grid, block, 0, s,
+                           x, w, y, bias, res, g, act, part, cnt);
+      else
+        hipLaunchKernelGGL((conv3x3_halo_kernel<TM, TN, WGM, WGN, PROWS, NPB, WST, OCC, false, true>), grid, block, 0, s,
+                           x, w, y, bias, res, g, act, part, cnt);
+      return;
+    }
+  }
   if (res)
     hipLaunchKernelGGL((conv3x3_halo_kernel<TM, TN, WGM, WGN, PROWS, NPB, WST, OCC, true>), grid, block, 0, s, x, w, y,
-                       bias, res, g, act);
+                       bias, res, g, act, part, cnt);
   else
     hipLaunchKernelGGL((conv3x3_halo_kernel<TM, TN, WGM, WGN, PROWS, NPB, WST, OCC, false>), grid, block, 0, s, x, w,
-                       y, bias, res, g, act);
+                       y, bias, res, g, act, part, cnt);
 }
 
 // Resident-weight launches: runs of tpb tiles (tpb divides the tile rows of a
@@ -631,8 +696,25 @@ int conv_halo_tiles(int v, int N, int H, int W, int C, int K) {
   return ((N + G - 1) / G) * (H / TH) * ((K + kHaloBN[v] - 1) / kHaloBN[v]);
 }
 
+// Splits that actually run for `splits` requested over C / 64 channel blocks (every split non-empty).
+static int halo_eff_splits(int C, int splits, int& cpb) {
+  const int ncb = C / 64;
+  cpb = splits > 1 ? (ncb + splits - 1) / splits : ncb;
+  return (ncb + cpb - 1) / cpb;
+}
+
+// Workspace bytes a split-K halo launch needs (0: the tile does not split / runs unsplit).
+size_t conv_halo_ws_bytes(int v, int N, int H, int W, int C, int K, int splits) {
+  const int tiles = conv_halo_tiles(v, N, H, W, C, K);
+  if (tiles <= 0 || splits < 2 || !halo_splittable(v)) return 0;
+  int cpb;
+  const int eff = halo_eff_splits(C, splits, cpb);
+  if (eff < 2) return 0;
+  return kSplitKHeader + (size_t)tiles * eff * kHaloBM[v] * kHaloBN[v] * sizeof(float);
+}
+
 void conv3x3_halo(int v, const void* x, const void* w, void* y, const void* bias, const void* res, int N, int H, int W,
-                  int C, int K, int act, hipStream_t s) {
+                  int C, int K, int act, hipStream_t s, int splits, void* ws, size_t ws_bytes) {
   if (v < 0 || v >= kNumHalo) throw std::invalid_argument("conv2d_nhwc: unknown halo conv tile");
   if (C % 64 != 0 || K % 8 != 0 || bias == nullptr)
     throw std::invalid_argument("conv2d_nhwc: halo conv tiles need C % 64 == 0, K % 8 == 0 and a bias");
@@ -642,20 +724,39 @@ void conv3x3_halo(int v, const void* x, const void* w, void* y, const void* bias
     throw std::invalid_argument("conv2d_nhwc: halo conv operands must stay under 2 GiB");
   if (kHaloWR[v] && (res != nullptr || (act != ACT_NONE && act != ACT_RELU)))
     throw std::invalid_argument("conv2d_nhwc: resident-weight halo tiles: no residual, ReLU or no activation");
-  HaloGeom g{N, H, W, C, K, 0, 1, W + 2, 0, 0};
+  HaloGeom g{N, H, W, C, K, 0, 1, W + 2, 0, 0, C / 64};
   if (!halo_geom(v, N, H, W, C, g.TH, g.G))
     throw std::invalid_argument("conv2d_nhwc: halo conv tile " + std::to_string(v) + " does not fit this conv");
   g.PR = g.G * (g.TH + 2) * g.Wp;
   g.tiles_m = ((N + g.G - 1) / g.G) * (H / g.TH);
+  // split-K: only when the workspace holds every split's partial tiles, else unsplit
+  int eff = 1;
+  float* part = nullptr;
+  int* cnt = nullptr;
+  if (splits > 1) {
+    if (!halo_splittable(v)) throw std::invalid_argument("conv2d_nhwc: halo conv tile " + std::to_string(v) + " has no split-K");
+    const size_t need = conv_halo_ws_bytes(v, N, H, W, C, K, splits);
+    const int tiles = conv_halo_tiles(v, N, H, W, C, K);
+    int cpb;
+    const int e = halo_eff_splits(C, splits, cpb);
+    if (need > 0 && ws != nullptr && need <= ws_bytes && tiles <= kSplitKMaxTiles &&
+        need - kSplitKHeader <= (size_t(1) << 31)) {
+      eff = e;
+      g.cpb = cpb;
+      cnt = static_cast<int*>(ws);
+      part = reinterpret_cast<float*>(static_cast<char*>(ws) + kSplitKHeader);
+    }
+  }
   const f16 *xp = (const f16*)x, *wp = (const f16*)w, *bp = (const f16*)bias, *rp = (const f16*)res;
   f16* yp = (f16*)y;
   switch (v) {
-    case 0: launch_halo<4, 4, 4, 1, 352, 1, 4, 2>(g, xp, wp, yp, bp, rp, act, s); break;
-    case 1: launch_halo<7, 1, 1, 4, 256, 1, 4, 2>(g, xp, wp, yp, bp, rp, act, s); break;
-    case 2: launch_halo<7, 1, 1, 4, 192, 2, 3, 2>(g, xp, wp, yp, bp, rp, act, s); break;
-    case 3: launch_halo<4, 1, 1, 4, 96, 2, 4, 2>(g, xp, wp, yp, bp, rp, act, s); break;
-    case 4: launch_halo<7, 2, 2, 2, 288, 2, 3, 1>(g, xp, wp, yp, bp, rp, act, s); break;
-    case 5: launch_halo<7, 4, 2, 2, 288, 2, 3, 1>(g, xp, wp, yp, bp, rp, act, s); break;
+    case 0: launch_halo<4, 4, 4, 1, 352, 1, 4, 2>(g, xp, wp, yp, bp, rp, act, s, 1, part, cnt); break;
+    case 1: launch_halo<7, 1, 1, 4, 256, 1, 4, 2>(g, xp, wp, yp, bp, rp, act, s, 1, part, cnt); break;
+    case 2: launch_halo<7, 1, 1, 4, 192, 2, 3, 2>(g, xp, wp, yp, bp, rp, act, s, eff, part, cnt); break;
+    case 3: launch_halo<4, 1, 1, 4, 96, 2, 4, 2>(g, xp, wp, yp, bp, rp, act, s, eff, part, cnt); break;
+    case 4: launch_halo<7, 2, 2, 2, 288, 2, 3, 1>(g, xp, wp, yp, bp, rp, act, s, eff, part, cnt); break;
+    case 5: launch_halo<7, 4, 2, 2, 288, 2, 3, 1>(g, xp, wp, yp, bp, rp, act, s, eff, part, cnt); break;
+    case 9: launch_halo<4, 4, 4, 1, 352, 2, 4, 1>(g, xp, wp, yp, bp, rp, act, s, eff, part, cnt); break;
     case 6: launch_halo_rw<2, 2, 2, 2, 192, 3, 576>(g, xp, wp, yp, bp, act, s); break;
     case 7: launch_halo_rw<2, 2, 4, 1, 192, 3, 576>(g, xp, wp, yp, bp, act, s); break;
     default: launch_halo_rw<4, 4, 4, 1, 352, 2, 576>(g, xp, wp, yp, bp, act, s); break;

@@ -322,7 +322,7 @@ def test_conv2d_pingpong(N, H, C, K, R, stride, pad):
 
 @pytest.mark.parametrize("N,H,C,K", [
     (2, 56, 64, 64), (3, 28, 128, 128), (3, 14, 256, 256), (5, 7, 512, 512), (3, 14, 128, 72), (2, 12, 64, 200),
-    (32, 56, 64, 64), (32, 28, 128, 128)])
+    (32, 56, 64, 64), (32, 28, 128, 128), (32, 14, 256, 256), (32, 7, 512, 512)])
 def test_conv2d_halo(N, H, C, K):
     """The halo-tile 3x3 kernel (CONV_HALO | v): every tile whose rows fit the
     image, against the fp32 reference with and without a residual; odd image
@@ -337,8 +337,15 @@ def test_conv2d_halo(N, H, C, K):
     ref_r = ops.conv2d_nhwc_ref(x, w, b, pad=1, act="relu", residual=r)
     cands = ops.conv_halo_candidates(N, H, H, C, K, 3, 3, 1, 1, H, H, True)
     assert cands
+    ws = ops.splitk_workspace("cuda")
     for c in cands:
         _close(ops.conv2d_nhwc(x, w, b, pad=1, act="relu", tile_cfg=c), ref, 2e-2, 2e-2)
+        if ops.splits_of(c) > 1:       # split-K on a shared workspace: the tile counters end at zero
+            _close(ops.conv2d_nhwc(x, w, b, pad=1, act="relu", tile_cfg=c, workspace=ws), ref, 2e-2, 2e-2)
+            _close(ops.conv2d_nhwc(x, w, b, pad=1, act="relu", residual=r, tile_cfg=c, workspace=ws), ref_r, 2e-2, 2e-2)
+            torch.cuda.synchronize()
+            assert int(ws[:ops.SPLITK_HEADER].view(torch.int32).abs().sum()) == 0
+            continue
         if (c & 255) in ops._CONV_HALO_RW:       # resident-weight tiles: no residual epilogue
             with pytest.raises(Exception):
                 ops.conv2d_nhwc(x, w, b, pad=1, act="relu", residual=r, tile_cfg=c)

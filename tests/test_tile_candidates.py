@@ -148,7 +148,12 @@ def test_conv_halo_candidates():
         cands = ops.conv_halo_candidates(N, H, H, C, K, 3, 3, 1, 1, H, H, True)
         assert cands and len(cands) == len(set(cands))
         for c in cands:
-            assert c & ops.CONV_HALO and ops.splits_of(c) == 0 and tiles(c & 255, N, H, H, C, K) > 0
+            v, sp = c & 255, ops.splits_of(c)
+            assert c & ops.CONV_HALO and tiles(v, N, H, H, C, K) > 0
+            if sp:      # split-K: a two-buffer streamed tile, an under-filled grid, every split non-empty
+                assert v in ops._CONV_HALO_SK and tiles(v, N, H, H, C, K) < 256 and C // 64 >= 2
+                need = ops._ops().conv_halo_ws_bytes(v, N, H, H, C, K, sp)
+                assert ops.SPLITK_HEADER < need <= ops.SPLITK_WS_BYTES
         assert not ops.conv_halo_candidates(N, H, H, C, K, 3, 3, 1, 1, H, H, False)      # no bias
         assert not ops.conv_halo_candidates(N, H, H, C, K, 3, 3, 2, 1, H // 2, H // 2, True)  # strided
     assert not ops.conv_halo_candidates(32, 56, 56, 96, 64, 3, 3, 1, 1, 56, 56, True)      # C % 64
@@ -158,4 +163,7 @@ def test_conv_halo_candidates():
     assert tiles(0, 32, 28, 28, 128, 128) == -1 and tiles(2, 32, 28, 28, 128, 128) == 32 * 7 * 2
     # stage 4 (7 x 7): two images per 112-pixel tile
     assert tiles(2, 32, 7, 7, 512, 512) == 16 * 8
+    # split-K offered for the small-image layers only (stage 1 has one channel block)
+    assert any(ops.splits_of(c) for c in ops.conv_halo_candidates(32, 7, 7, 512, 512, 3, 3, 1, 1, 7, 7, True))
+    assert not any(ops.splits_of(c) for c in ops.conv_halo_candidates(32, 56, 56, 64, 64, 3, 3, 1, 1, 56, 56, True))
     assert ops._cu_share(ops.CONV_HALO | 0, 100352, 64) == 1.0
