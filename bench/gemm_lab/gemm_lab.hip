@@ -74,7 +74,17 @@ Variant core1(const char* nm) {
                                                                                1.f, ACT_NONE, s);
           }};
 }
-#if !defined(LAB_SET_GELU) && !defined(LAB_SET_FFN2) && !defined(LAB_FAST)   // the whole tile table: minutes of compile time
+// one production-kernel tile with DEEP (one block per CU, launch bounds for 512 VGPRs): the 4-wave
+// 256x256 tile with 128x128 per wave halves the LDS bytes per MFMA of the 64x64-per-wave tiles
+template <int BM, int BN, int WGM, int NW>
+Variant core1d(const char* nm) {
+  return {nm, [](const bf16* A, const bf16* W, const bf16* b, bf16* C, int M, int N, int K, hipStream_t s) {
+            DenseParams p{A, K, M, K};
+            launch_one<bf16, bf16, DenseLoader, true, false, BM, BN, WGM, NW, 0, 1>(p, W, K, C, N, b, nullptr, 0, M, N,
+                                                                                    K, 1.f, ACT_NONE, s);
+          }};
+}
+#if !defined(LAB_SET_GELU) && !defined(LAB_SET_FFN2) && !defined(LAB_FAST) && !defined(LAB_SET_BIG)   // the whole tile table: minutes of compile time
 Variant core(int cfg) {
   char nm[64];
   snprintf(nm, sizeof nm, "core cfg%d %dx%d/%dw", cfg, kTileBM[cfg], kTileBN[cfg], 4 * kTileNW[cfg] / 4);
@@ -129,6 +139,13 @@ int main(int argc, char** argv) {
       pp<4, 128, 128, 1, 2, 4, 32, 2>("pp4 128x128 bk32 s4"),
       pp<4, 128, 128, 1, 2, 3, 32, 3>("pp4 128x128 bk32 s3 occ3"),
       core(10), core(9),
+#elif defined(LAB_SET_BIG)
+      // per-wave tile size vs LDS bytes per MFMA (round 6): 128x128 per wave on 4 waves
+      core1d<256, 256, 2, 4>("core 256x256 4w (128x128/wave) deep"),
+      core1d<256, 128, 2, 4>("core 256x128 4w (128x64/wave) deep"),
+      core1d<128, 256, 2, 4>("core 128x256 4w (64x128/wave) deep"),
+      pp<8, 256, 128, 2, 2, 3>("pp8 256x128 2x2 s3"),
+      pp<8, 256, 256, 2, 2, 4, 32>("pp8 256x256 bk32 s4"),
 #elif defined(LAB_FAST)
       LAB_FAST
 #else
