@@ -199,7 +199,60 @@ class record_tuning_keys:
         return False
 
 
+# RDB_TUNE_GRAPH=1: time tuning candidates from a replayed hipGraph instead of eager launches.  Off by
+# default: it ranks the kernels themselves without the Python launch path, but tables tuned that way
+# served no better than eager-tuned ones (BERT 35.3k vs 35.0-35.8k, ResNet-50 41.1k vs 41.8-44.2k
+# img/s, profiles/tuner_graph_timing_r6.json) -- the in-context pass decides among the top candidates
+_TUNE_GRAPH = os.environ.get("RDB_TUNE_GRAPH", "0") == "1"
+_tune_graph_broken = False
+_TUNE_STREAMS: Dict[tuple, list] = {}
+
+
+def _tune_streams(n: int) -> list:
+    """The tuner's own streams on the current device (created once: per-stream
+    split-K workspaces are cached by stream, so fresh streams per shape would
+    each pin another workspace): [capture stream, side stream 1, ...]."""
+    key = (torch.cuda.current_device(), n)
+    st = _TUNE_STREAMS.get(key)
+    if st is None:
+        st = _TUNE_STREAMS[key] = [torch.cuda.Stream() for _ in range(n)]
+    return st
+
+
+def _time_tile_graph(launch: Callable[[int], None], c: int, cap, side: list, s, e, reps: int = 4) -> float:
+    """Best-of-3 time of ``reps`` launches of tile ``c`` on the current stream
+    (plus one per side stream each) replayed from a captured hipGraph.  Eager
+    timing includes the Python launch path (~15 us per launch, as long as the
+    faster BERT / ResNet kernels themselves at RDB_TUNE_STREAMS=3).  Every
+    lazily allocated buffer (split-K workspaces) exists before the capture:
+    the caller launched ``c`` eagerly on every stream first."""
+    cur = torch.cuda.current_stream()
+    cap.wait_stream(cur)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=cap, capture_error_mode="thread_local"):
+        for _ in range(reps):
+            launch(c)
+            for sd in side:
+                sd.wait_stream(cap)
+                with torch.cuda.stream(sd):
+                    launch(c)
+        for sd in side:
+            cap.wait_stream(sd)
+    cur.wait_stream(cap)
+    g.replay()                       # first replay: uploads the graph
+    t = float("inf")
+    for _trial in range(3):          # best of 3: clock / neighbour noise only ever adds time
+        s.record()
+        g.replay()
+        e.record()
+        e.synchronize()
+        t = min(t, s.elapsed_time(e))
+    del g
+    return t
+
+
 def _tuned_cfg(key: tuple, launch: Callable[[int], None], candidates=range(NUM_TILE_CFGS)) -> int:
+    global _tune_graph_broken
     if _KEY_LOG is not None and key not in _KEY_LOG:
         _KEY_LOG.append(key)
     cfg = _TUNE.get(key)
@@ -215,25 +268,38 @@ def _tuned_cfg(key: tuple, launch: Callable[[int], None], candidates=range(NUM_T
     # instead of the isolated latency, which favours small tiles that fill the
     # CUs alone but cost more LDS/VMEM traffic per FLOP when streams overlap.
     ns = max(1, int(os.environ.get("RDB_TUNE_STREAMS", "1")))
-    side = [torch.cuda.Stream() for _ in range(ns - 1)]
+    streams = _tune_streams(ns)
+    cap, side = streams[0], streams[1:]
     cur = torch.cuda.current_stream()
     for c in candidates:
         launch(c)
-        t = float("inf")
-        for _trial in range(3):          # best of 3: clock / neighbour noise only ever adds time
-            s.record()
-            for sd in side:
-                sd.wait_stream(cur)
-            for _ in range(4):
+        for sd in streams:               # every stream's lazily allocated buffers, outside any capture
+            sd.wait_stream(cur)
+            with torch.cuda.stream(sd):
                 launch(c)
+            cur.wait_stream(sd)
+        t = float("inf")
+        if _TUNE_GRAPH and not _tune_graph_broken:
+            try:
+                t = _time_tile_graph(launch, c, cap, side, s, e)
+            except Exception:            # a launch path that cannot be captured: eager timing from here on
+                _tune_graph_broken = True
+                torch.cuda.synchronize()
+        if t == float("inf"):
+            for _trial in range(3):          # best of 3: clock / neighbour noise only ever adds time
+                s.record()
                 for sd in side:
-                    with torch.cuda.stream(sd):
-                        launch(c)
-            for sd in side:
-                cur.wait_stream(sd)
-            e.record()
-            e.synchronize()
-            t = min(t, s.elapsed_time(e))
+                    sd.wait_stream(cur)
+                for _ in range(4):
+                    launch(c)
+                    for sd in side:
+                        with torch.cuda.stream(sd):
+                            launch(c)
+                for sd in side:
+                    cur.wait_stream(sd)
+                e.record()
+                e.synchronize()
+                t = min(t, s.elapsed_time(e))
         times[c] = t
         if t < best_t:
             best_t, best_c = t, c
