@@ -1255,10 +1255,10 @@ _CONV_PP = os.environ.get("RDB_CONV_PP", "1") != "0"
 #   CONV_HALO | v        (3x3, stride 1, pad 1, C % 64 == 0, with bias) the halo-tile kernel,
 #                        tile v (conv_halo.hip): one LDS patch feeds all 9 taps
 CONV_HALO = 1 << 18
-_CONV_HALO_BM = (256, 112, 112, 64, 224, 224, 64, 128, 256, 256)    # conv_halo.hip kHaloBM / kHaloBN
-_CONV_HALO_BN = (64, 64, 64, 64, 64, 128, 64, 32, 64, 64)
-_CONV_HALO_RW = (6, 7, 8)          # persistent resident-weight tiles: no residual, ReLU / none
-_CONV_HALO_SK = (2, 3, 4, 5, 9)    # two-patch-buffer streamed tiles: split-K over the 64-channel blocks
+_CONV_HALO_BM = (256, 112, 112, 64, 224, 224, 64, 128, 256, 256, 64, 64)    # conv_halo.hip kHaloBM / kHaloBN
+_CONV_HALO_BN = (64, 64, 64, 64, 64, 128, 64, 32, 64, 64, 128, 64)
+_CONV_HALO_RW = (6, 7, 8)          # persistent resident-weight tiles: no residual, ReLU / none (stride 1)
+_CONV_HALO_SK = (2, 3, 4, 5, 9, 10, 11)   # two-patch-buffer streamed tiles: split-K over the 64-channel blocks
 # RDB_CONV_HALO=0: no halo-tile conv candidates
 _CONV_HALO = os.environ.get("RDB_CONV_HALO", "1") != "0"
 DEEP = 1 << 12                        # gemm_core.h kDeepFlag: one block per CU, up to 8 LDS stages
@@ -1342,16 +1342,18 @@ def _conv_pp_candidates(M: int, K_out: int, Kg: int, C: int):
 
 def conv_halo_candidates(N: int, H: int, W: int, C: int, K: int, R: int, S: int, stride: int, pad: int, P: int,
                          Q: int, has_bias: bool, has_res: bool = False, act: str = "relu"):
-    """Halo-tile 3x3 tiles (CONV_HALO | v) whose rows fit an H x W image
-    (conv_halo.hip ``conv_halo_tiles``): same-size 3x3 convs with a bias; the
-    one-patch-buffer tiles only for a single 64-channel block (C == 64)."""
-    if not (_CONV_HALO and has_bias and R == 3 and S == 3 and stride == 1 and pad == 1 and (P, Q) == (H, W)
-            and C % 64 == 0 and K % 8 == 0):
+    """Halo-tile 3x3 tiles (CONV_HALO | v [| splits << 8]) whose rows fit the image
+    (conv_halo.hip ``conv_halo_tiles_s``): 3x3 convs with pad 1, stride 1 or 2, the full
+    output, a bias; the one-patch-buffer tiles only for a single 64-channel block
+    (C == 64), the resident-weight tiles only at stride 1; split-K where the tile
+    grid leaves CUs idle."""
+    if not (_CONV_HALO and has_bias and R == 3 and S == 3 and stride in (1, 2) and pad == 1
+            and (P, Q) == ((H - 1) // stride + 1, (W - 1) // stride + 1) and C % 64 == 0 and K % 8 == 0):
         return []
     rw_ok = not has_res and act in ("relu", "none")
     out = []
     for v in range(len(_CONV_HALO_BM)):
-        tiles = _ops().conv_halo_tiles(v, N, H, W, C, K)
+        tiles = _ops().conv_halo_tiles_s(v, N, H, W, C, K, stride)
         if tiles <= 0 or (v in _CONV_HALO_RW and not rw_ok):
             continue
         out.append(CONV_HALO | v)
@@ -1364,7 +1366,7 @@ def conv_halo_candidates(N: int, H: int, W: int, C: int, K: int, R: int, S: int,
             eff = -(-ncb // cpb)
             if eff < 2 or eff != sp or tiles * eff > 1024:
                 continue
-            if _ops().conv_halo_ws_bytes(v, N, H, W, C, K, sp) > SPLITK_WS_BYTES:
+            if _ops().conv_halo_ws_bytes(v, N, H, W, C, K, sp, stride) > SPLITK_WS_BYTES:
                 continue
             out.append(CONV_HALO | v | (sp << 8))
     return out
@@ -1446,7 +1448,7 @@ def conv2d_nhwc(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] =
             return
         sp = splits_of(c)
         if sp > 1 and ws is None:
-            need = _ops().conv_halo_ws_bytes(c & 255, N, H, W, C, K, sp) if c & CONV_HALO else \
+            need = _ops().conv_halo_ws_bytes(c & 255, N, H, W, C, K, sp, stride) if c & CONV_HALO else \
                 _ops().conv_splitk_bytes(M, K, c & ~0xF00, sp)
             ws = _private_splitk_ws(x.device, int(need))
         fn(*args, _stream(), int(c), _ptr(ws), 0 if ws is None else ws.numel())

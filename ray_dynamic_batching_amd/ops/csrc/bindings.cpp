@@ -19,7 +19,8 @@ void gemm_tn_sk(int in_dtype, int out_dtype, uintptr_t A, int lda, uintptr_t W, 
                 int act, uintptr_t stream, int force_cfg, uintptr_t ws, size_t ws_bytes);
 size_t conv_splitk_bytes(int M, int N, int cfg, int splits);
 int conv_halo_tiles(int v, int N, int H, int W, int C, int K);
-size_t conv_halo_ws_bytes(int v, int N, int H, int W, int C, int K, int splits);
+size_t conv_halo_ws_bytes(int v, int N, int H, int W, int C, int K, int splits, int S);
+int conv_halo_tiles_s(int v, int N, int H, int W, int C, int K, int S);
 void gemm_tn_ln(uintptr_t A, int lda, uintptr_t W, int ldw, uintptr_t C, int ldc, uintptr_t bias, uintptr_t R,
                 int ldr, int M, int N, int K, float alpha, int act, int mode, uintptr_t a_stats, int a_ld,
                 uintptr_t a_colsum, uintptr_t a_bias, uintptr_t r_stats, int r_ld, uintptr_t r_g, uintptr_t r_b,
@@ -126,6 +127,7 @@ PYBIND11_MODULE(_rdb_ops, m) {
   m.def("conv_splitk_bytes", &rdb::conv_splitk_bytes);
   m.def("conv_halo_tiles", &rdb::conv_halo_tiles);
   m.def("conv_halo_ws_bytes", &rdb::conv_halo_ws_bytes);
+  m.def("conv_halo_tiles_s", &rdb::conv_halo_tiles_s);
   m.def("maxpool_nhwc", &rdb::maxpool_nhwc, py::call_guard<py::gil_scoped_release>());
   m.def("avgpool_nhwc", &rdb::avgpool_nhwc, py::call_guard<py::gil_scoped_release>());
   m.def("dwconv_nhwc", &rdb::dwconv_nhwc, py::call_guard<py::gil_scoped_release>());

@@ -20,7 +20,7 @@ constexpr int kConvPPFlag = 1 << 17;
 // force_cfg = kConvHaloFlag | v: the halo-tile 3x3 kernel (conv_halo.hip)
 constexpr int kConvHaloFlag = 1 << 18;
 void conv3x3_halo(int v, const void* x, const void* w, void* y, const void* bias, const void* res, int N, int H, int W,
-                  int C, int K, int act, hipStream_t s, int splits, void* ws, size_t ws_bytes);
+                  int C, int K, int stride, int act, hipStream_t s, int splits, void* ws, size_t ws_bytes);
 constexpr int kNumConvPP = 5;
 //                                  0    1    2    3    4
 constexpr int kConvPPBM[kNumConvPP] = {256, 128, 256, 256, 128};
@@ -92,11 +92,12 @@ void conv2d_nhwc(uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t res, uintpt
   const int M = N * P * Q, Kg = R * S * C;
   if (M <= 0 || K <= 0) return;
   if (force_cfg >= 0 && (force_cfg & kConvHaloFlag)) {
-    if (R != 3 || S != 3 || stride != 1 || pad != 1 || P != H || Q != W)
-      throw std::invalid_argument("conv2d_nhwc: halo conv tiles are 3x3, stride 1, pad 1");
+    if (R != 3 || S != 3 || (stride != 1 && stride != 2) || pad != 1 || P != (H - 1) / stride + 1 ||
+        Q != (W - 1) / stride + 1)
+      throw std::invalid_argument("conv2d_nhwc: halo conv tiles are 3x3, stride 1 or 2, pad 1, full output");
     conv3x3_halo(force_cfg & 255, reinterpret_cast<const void*>(x), reinterpret_cast<const void*>(w),
                  reinterpret_cast<void*>(y), reinterpret_cast<const void*>(bias), reinterpret_cast<const void*>(res), N,
-                 H, W, C, K, act, reinterpret_cast<hipStream_t>(stream), (force_cfg >> 8) & 15,
+                 H, W, C, K, stride, act, reinterpret_cast<hipStream_t>(stream), (force_cfg >> 8) & 15,
                  reinterpret_cast<void*>(ws), ws_bytes);
     return;
   }

@@ -30,11 +30,12 @@ namespace rdb {
 constexpr int kConvHaloFlag = 1 << 18;
 
 struct HaloGeom {
-  int N, H, W, C, K;   // input [N, H, W, C]; output [N, H, W, K] (3x3, stride 1, pad 1)
-  int TH, G;           // output rows per tile; images per tile (G > 1 only with TH == H)
-  int Wp, PR;          // W + 2; patch rows G * (TH + 2) * Wp
-  int tiles_m;         // ceil(N / G) * (H / TH)
+  int N, H, W, C, K;   // input [N, H, W, C]; output [N, P, Q, K] (3x3, pad 1, stride S)
+  int TH, G;           // output rows per tile; images per tile (G > 1 only with TH == P)
+  int Wp, PR;          // patch width S * (Q - 1) + 3; patch rows G * THp * Wp
+  int tiles_m;         // ceil(N / G) * ceil(P / TH)
   int cpb;             // split-K: 64-channel blocks per split (gridDim.y splits; cpb = C / 64 unsplit)
+  int P, Q, S, THp;    // output rows / columns, stride, patch rows per image S * (TH - 1) + 3
 };
 
 // Diagnostic build only (bench/gemm_lab/halo_lab.hip defines RDB_HALO_STAMPS): per-wave
@@ -99,17 +100,17 @@ conv3x3_halo_kernel(const f16* __restrict__ x, const f16* __restrict__ w, f16* _
   const int tiles_n = (g.K + BN - 1) / BN;
   const int t = xcd_remap(blockIdx.x, g.tiles_m * tiles_n);
   const int tile_m = t / tiles_n, tile_n = t - tile_m * tiles_n;
-  const int rb_per_img = g.H / g.TH;
+  const int rb_per_img = (g.P + g.TH - 1) / g.TH;
   const int grp = tile_m / rb_per_img, rb = tile_m - grp * rb_per_img;
   const int n_first = grp * g.G, p0 = rb * g.TH;
-  const int HW = g.H * g.W;
-  const int m0 = n_first * HW + p0 * g.W, n0 = tile_n * BN;
-  const int bmv = g.G * g.TH * g.W;
-  const int m_lim = min(g.N * HW, m0 + bmv);
+  const int PQ = g.P * g.Q;
+  const int m0 = n_first * PQ + p0 * g.Q, n0 = tile_n * BN;
+  const int bmv = g.G * min(g.TH, g.P - p0) * g.Q;   // the last row block of an image may be partial
+  const int m_lim = min(g.N * PQ, m0 + bmv);
   const int Kg = 9 * g.C;
-  const int THp = g.TH + 2;
+  const int THp = g.THp;
 
-  const __amdgpu_buffer_rsrc_t xsrc = make_rsrc(x, (uint32_t)((size_t)g.N * HW * g.C * 2));
+  const __amdgpu_buffer_rsrc_t xsrc = make_rsrc(x, (uint32_t)((size_t)g.N * g.H * g.W * g.C * 2));
   const __amdgpu_buffer_rsrc_t wsrc = make_rsrc(w, (uint32_t)((size_t)g.K * Kg * 2));
 
   // this lane's patch DMA pieces: rows (wid * LP + i) * 8 + lane / 8, i.e. 8 rows apart --
@@ -123,7 +124,7 @@ conv3x3_halo_kernel(const f16* __restrict__ x, const f16* __restrict__ w, f16* _
 #pragma unroll
     for (int i = 0; i < LP; ++i) {
       const int ch = dma_chunk(tid, row);
-      const int n = n_first + gi, h = p0 - 1 + ph, ww = pw - 1;
+      const int n = n_first + gi, h = g.S * p0 - 1 + ph, ww = pw - 1;
       const bool ok = row < g.PR && n < g.N && (unsigned)h < (unsigned)g.H && (unsigned)ww < (unsigned)g.W;
       poff[i] = ok ? (uint32_t)((((n * g.H + h) * g.W + ww) * g.C) * 2 + ch * 16) : kOOB;
       row += 8;
@@ -141,18 +142,19 @@ conv3x3_halo_kernel(const f16* __restrict__ x, const f16* __restrict__ w, f16* _
     wof[i] = n0 + row < g.K ? (uint32_t)((n0 + row) * Kg * 2 + ch * 16) : kOOB;
   }
   // the A fragment rows: patch row of output pixel wm*WM + j*16 + fr at tap (0, 0)
+  // (output (p, q) reads patch rows S*p + r, columns S*q + s)
   int prow[TM];
   {
     const int l0 = wm * WM + fr;
-    const int per = g.TH * g.W;
+    const int per = g.TH * g.Q;
     int gi = l0 / per;
     int rem = l0 - gi * per;
-    int p = rem / g.W, q = rem - p * g.W;
+    int p = rem / g.Q, q = rem - p * g.Q;
 #pragma unroll
     for (int j = 0; j < TM; ++j) {
-      prow[j] = wm * WM + j * 16 + fr < bmv ? gi * THp * g.Wp + p * g.Wp + q : 0;
+      prow[j] = wm * WM + j * 16 + fr < bmv ? gi * THp * g.Wp + g.S * (p * g.Wp + q) : 0;
       q += 16;
-      while (q >= g.W) { q -= g.W; ++p; }
+      while (q >= g.Q) { q -= g.Q; ++p; }
       while (p >= g.TH) { p -= g.TH; ++gi; }
     }
   }
@@ -606,33 +608,41 @@ conv3x3_halo_rw_kernel(const f16* __restrict__ x, const f16* __restrict__ w, f16
 //   7   2  2  4   1  128 x  32    192 x 3   resident weights (576 rows), persistent   stage 2: 4 rows x 28, 32-ch slices
 //   8   4  4  4   1  256 x  64    352 x 2   resident weights (576 rows), persistent   stage 1: 4 rows x 56 (160 KiB LDS)
 //   9   4  4  4   1  256 x  64    352 x 2            4     1         stages 3 / 4 (a 14 x 14 image; four 7 x 7 images), split-K
-// Split-K (force_cfg | splits << 8): the two-patch-buffer streamed tiles (2, 3, 4, 5, 9).
+//  10   4  2  1   4   64 x 128    288 x 2            3     1         stride 2: 2 rows x 28 of 56 x 56; 4 of 28; one 7 x 7
+//  11   4  1  1   4   64 x  64    288 x 2            4     1         stride 2, 64-channel N tiles
+// Split-K (force_cfg | splits << 8): the two-patch-buffer streamed tiles (2, 3, 4, 5, 9, 10, 11).
+// Stride 2 (pad 1): the streamed tiles; output (p, q) reads patch rows 2p + r, columns 2q + s.
 // (one patch buffer: a single 64-channel block, C == 64; resident weights: 9 * C/64 * BN <= 576 rows.
 //  Measured and dropped: weights held in VGPRs per wave -- loading 72 KiB per wave from L2 costs more
 //  than it saves, and above 256 VGPRs the fragments spill or bounce through AGPRs,
 //  profiles/resnet50_conv_halo_r6.json)
-constexpr int kNumHalo = 10;
-constexpr int kHaloBM[kNumHalo] = {256, 112, 112, 64, 224, 224, 64, 128, 256, 256};
-constexpr int kHaloBN[kNumHalo] = {64, 64, 64, 64, 64, 128, 64, 32, 64, 64};
-constexpr int kHaloPM[kNumHalo] = {352, 256, 192, 96, 288, 288, 192, 192, 352, 352};
-constexpr int kHaloNPB[kNumHalo] = {1, 1, 2, 2, 2, 2, 3, 3, 2, 2};
-constexpr int kHaloWR[kNumHalo] = {0, 0, 0, 0, 0, 0, 576, 576, 576, 0};   // resident weight rows (0: streamed)
+constexpr int kNumHalo = 12;
+constexpr int kHaloBM[kNumHalo] = {256, 112, 112, 64, 224, 224, 64, 128, 256, 256, 64, 64};
+constexpr int kHaloBN[kNumHalo] = {64, 64, 64, 64, 64, 128, 64, 32, 64, 64, 128, 64};
+constexpr int kHaloPM[kNumHalo] = {352, 256, 192, 96, 288, 288, 192, 192, 352, 352, 288, 288};
+constexpr int kHaloNPB[kNumHalo] = {1, 1, 2, 2, 2, 2, 3, 3, 2, 2, 2, 2};
+constexpr int kHaloWR[kNumHalo] = {0, 0, 0, 0, 0, 0, 576, 576, 576, 0, 0, 0};   // resident weight rows (0: streamed)
 
 static bool halo_splittable(int v) { return kHaloNPB[v] == 2 && kHaloWR[v] == 0; }
 
-// (TH, G) of variant v for an H x W image: the most output rows (then images)
-// whose pixels fit BM and whose patch fits the LDS patch buffer; TH divides H.
-static bool halo_geom(int v, int N, int H, int W, int C, int& TH, int& G) {
+// (TH, G) of variant v for an H x W input at stride S (pad 1; output P x Q): the most
+// output rows (then images) whose pixels fit BM and whose patch -- S * (TH - 1) + 3 rows
+// of S * (Q - 1) + 3 pixels -- fits the LDS patch buffer.  Stride 1: TH divides P;
+// stride 2: the last row block of an image may be partial.
+static bool halo_geom(int v, int N, int H, int W, int C, int S, int& TH, int& G) {
   const int bm = kHaloBM[v], pm = kHaloPM[v];
   TH = 0;
   G = 1;
-  if (C % 64 != 0 || (kHaloNPB[v] == 1 && C != 64) || W + 2 < 9) return false;
-  if (kHaloWR[v] && 9 * (C / 64) * kHaloBN[v] > kHaloWR[v]) return false;
-  for (int th = H; th >= 1; --th)
-    if (H % th == 0 && th * W <= bm && (th + 2) * (W + 2) <= pm) { TH = th; break; }
+  if (S != 1 && S != 2) return false;
+  const int P = (H - 1) / S + 1, Q = (W - 1) / S + 1, Wp = S * (Q - 1) + 3;
+  if (C % 64 != 0 || (kHaloNPB[v] == 1 && C != 64) || Wp < 9) return false;
+  if (kHaloWR[v] && (S != 1 || 9 * (C / 64) * kHaloBN[v] > kHaloWR[v])) return false;
+  for (int th = P; th >= 1; --th)
+    if ((S == 2 || P % th == 0) && th * Q <= bm && (S * (th - 1) + 3) * Wp <= pm) { TH = th; break; }
   if (TH == 0) return false;
-  if (TH == H)
-    while (G < N && (G + 1) * H * W <= bm && (G + 1) * (H + 2) * (W + 2) <= pm) ++G;
+  const int THp = S * (TH - 1) + 3;
+  if (TH == P)
+    while (G < N && (G + 1) * P * Q <= bm && (G + 1) * THp * Wp <= pm) ++G;
   return true;
 }
 
@@ -689,12 +699,14 @@ static void launch_halo_rw(const HaloGeom& g, const f16* x, const f16* w, f16* y
                      act, tpb);
 }
 
-int conv_halo_tiles(int v, int N, int H, int W, int C, int K) {
+int conv_halo_tiles_s(int v, int N, int H, int W, int C, int K, int S) {
   if (v < 0 || v >= kNumHalo) return -1;
   int TH, G;
-  if (!halo_geom(v, N, H, W, C, TH, G)) return -1;
-  return ((N + G - 1) / G) * (H / TH) * ((K + kHaloBN[v] - 1) / kHaloBN[v]);
+  if (!halo_geom(v, N, H, W, C, S, TH, G)) return -1;
+  const int P = (H - 1) / S + 1;
+  return ((N + G - 1) / G) * ((P + TH - 1) / TH) * ((K + kHaloBN[v] - 1) / kHaloBN[v]);
 }
+int conv_halo_tiles(int v, int N, int H, int W, int C, int K) { return conv_halo_tiles_s(v, N, H, W, C, K, 1); }
 
 // Splits that actually run for `splits` requested over C / 64 channel blocks (every split non-empty).
 static int halo_eff_splits(int C, int splits, int& cpb) {
@@ -704,8 +716,8 @@ static int halo_eff_splits(int C, int splits, int& cpb) {
 }
 
 // Workspace bytes a split-K halo launch needs (0: the tile does not split / runs unsplit).
-size_t conv_halo_ws_bytes(int v, int N, int H, int W, int C, int K, int splits) {
-  const int tiles = conv_halo_tiles(v, N, H, W, C, K);
+size_t conv_halo_ws_bytes(int v, int N, int H, int W, int C, int K, int splits, int S) {
+  const int tiles = conv_halo_tiles_s(v, N, H, W, C, K, S);
   if (tiles <= 0 || splits < 2 || !halo_splittable(v)) return 0;
   int cpb;
   const int eff = halo_eff_splits(C, splits, cpb);
@@ -714,7 +726,7 @@ size_t conv_halo_ws_bytes(int v, int N, int H, int W, int C, int K, int splits) 
 }
 
 void conv3x3_halo(int v, const void* x, const void* w, void* y, const void* bias, const void* res, int N, int H, int W,
-                  int C, int K, int act, hipStream_t s, int splits, void* ws, size_t ws_bytes) {
+                  int C, int K, int stride, int act, hipStream_t s, int splits, void* ws, size_t ws_bytes) {
   if (v < 0 || v >= kNumHalo) throw std::invalid_argument("conv2d_nhwc: unknown halo conv tile");
   if (C % 64 != 0 || K % 8 != 0 || bias == nullptr)
     throw std::invalid_argument("conv2d_nhwc: halo conv tiles need C % 64 == 0, K % 8 == 0 and a bias");
@@ -724,19 +736,21 @@ void conv3x3_halo(int v, const void* x, const void* w, void* y, const void* bias
     throw std::invalid_argument("conv2d_nhwc: halo conv operands must stay under 2 GiB");
   if (kHaloWR[v] && (res != nullptr || (act != ACT_NONE && act != ACT_RELU)))
     throw std::invalid_argument("conv2d_nhwc: resident-weight halo tiles: no residual, ReLU or no activation");
-  HaloGeom g{N, H, W, C, K, 0, 1, W + 2, 0, 0, C / 64};
-  if (!halo_geom(v, N, H, W, C, g.TH, g.G))
+  HaloGeom g{N, H, W, C, K, 0, 1, 0, 0, 0, C / 64, (H - 1) / stride + 1, (W - 1) / stride + 1, stride, 0};
+  if (!halo_geom(v, N, H, W, C, stride, g.TH, g.G))
     throw std::invalid_argument("conv2d_nhwc: halo conv tile " + std::to_string(v) + " does not fit this conv");
-  g.PR = g.G * (g.TH + 2) * g.Wp;
-  g.tiles_m = ((N + g.G - 1) / g.G) * (H / g.TH);
+  g.Wp = stride * (g.Q - 1) + 3;
+  g.THp = stride * (g.TH - 1) + 3;
+  g.PR = g.G * g.THp * g.Wp;
+  g.tiles_m = ((N + g.G - 1) / g.G) * ((g.P + g.TH - 1) / g.TH);
   // split-K: only when the workspace holds every split's partial tiles, else unsplit
   int eff = 1;
   float* part = nullptr;
   int* cnt = nullptr;
   if (splits > 1) {
     if (!halo_splittable(v)) throw std::invalid_argument("conv2d_nhwc: halo conv tile " + std::to_string(v) + " has no split-K");
-    const size_t need = conv_halo_ws_bytes(v, N, H, W, C, K, splits);
-    const int tiles = conv_halo_tiles(v, N, H, W, C, K);
+    const size_t need = conv_halo_ws_bytes(v, N, H, W, C, K, splits, stride);
+    const int tiles = conv_halo_tiles_s(v, N, H, W, C, K, stride);
     int cpb;
     const int e = halo_eff_splits(C, splits, cpb);
     if (need > 0 && ws != nullptr && need <= ws_bytes && tiles <= kSplitKMaxTiles &&
@@ -757,6 +771,8 @@ void conv3x3_halo(int v, const void* x, const void* w, void* y, const void* bias
     case 4: launch_halo<7, 2, 2, 2, 288, 2, 3, 1>(g, xp, wp, yp, bp, rp, act, s, eff, part, cnt); break;
     case 5: launch_halo<7, 4, 2, 2, 288, 2, 3, 1>(g, xp, wp, yp, bp, rp, act, s, eff, part, cnt); break;
     case 9: launch_halo<4, 4, 4, 1, 352, 2, 4, 1>(g, xp, wp, yp, bp, rp, act, s, eff, part, cnt); break;
+    case 10: launch_halo<4, 2, 1, 4, 288, 2, 3, 1>(g, xp, wp, yp, bp, rp, act, s, eff, part, cnt); break;
+    case 11: launch_halo<4, 1, 1, 4, 288, 2, 4, 1>(g, xp, wp, yp, bp, rp, act, s, eff, part, cnt); break;
     case 6: launch_halo_rw<2, 2, 2, 2, 192, 3, 576>(g, xp, wp, yp, bp, act, s); break;
     case 7: launch_halo_rw<2, 2, 4, 1, 192, 3, 576>(g, xp, wp, yp, bp, act, s); break;
     default: launch_halo_rw<4, 4, 4, 1, 352, 2, 576>(g, xp, wp, yp, bp, act, s); break;

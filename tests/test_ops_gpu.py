@@ -351,8 +351,34 @@ def test_conv2d_halo(N, H, C, K):
                 ops.conv2d_nhwc(x, w, b, pad=1, act="relu", residual=r, tile_cfg=c)
             continue
         _close(ops.conv2d_nhwc(x, w, b, pad=1, act="relu", residual=r, tile_cfg=c), ref_r, 2e-2, 2e-2)
-    with pytest.raises(Exception):       # stride 2 is not a halo shape
-        ops.conv2d_nhwc(x, w, b, stride=2, pad=1, tile_cfg=ops.CONV_HALO | 0)
+    with pytest.raises(Exception):       # pad 0 is not a halo shape
+        ops.conv2d_nhwc(x, w, b, stride=1, pad=0, tile_cfg=ops.CONV_HALO | 0)
+
+
+@pytest.mark.parametrize("N,H,C,K", [(2, 56, 128, 128), (3, 28, 256, 256), (5, 14, 512, 512), (32, 56, 128, 128),
+                                     (32, 14, 512, 512), (2, 15, 64, 72)])
+def test_conv2d_halo_stride2(N, H, C, K):
+    """The halo tiles at stride 2 (pad 1): patch rows 2p + r, columns 2q + s; the last
+    row block of an image may be partial (odd sizes); split-K candidates on a shared
+    workspace leave its counters at zero."""
+    ops = _ops()
+    torch.manual_seed(23 + H + K)
+    x = torch.randn(N, H, H, C, device="cuda", dtype=torch.float16)
+    w = torch.randn(K, 3, 3, C, device="cuda", dtype=torch.float16) * (9 * C) ** -0.5
+    b = torch.randn(K, device="cuda", dtype=torch.float16) * 0.1
+    ref = ops.conv2d_nhwc_ref(x, w, b, stride=2, pad=1, act="relu")
+    r = torch.randn_like(ref)
+    ref_r = ops.conv2d_nhwc_ref(x, w, b, stride=2, pad=1, act="relu", residual=r)
+    P = (H - 1) // 2 + 1
+    cands = ops.conv_halo_candidates(N, H, H, C, K, 3, 3, 2, 1, P, P, True)
+    assert cands and all((c & 255) not in ops._CONV_HALO_RW for c in cands)
+    ws = ops.splitk_workspace("cuda")
+    for c in cands:
+        _close(ops.conv2d_nhwc(x, w, b, stride=2, pad=1, act="relu", tile_cfg=c, workspace=ws), ref, 2e-2, 2e-2)
+        _close(ops.conv2d_nhwc(x, w, b, stride=2, pad=1, act="relu", residual=r, tile_cfg=c, workspace=ws), ref_r,
+               2e-2, 2e-2)
+    torch.cuda.synchronize()
+    assert int(ws[:ops.SPLITK_HEADER].view(torch.int32).abs().sum()) == 0
 
 
 def test_conv2d_pingpong_splitk_graph_replay():

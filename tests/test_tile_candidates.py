@@ -152,10 +152,13 @@ def test_conv_halo_candidates():
             assert c & ops.CONV_HALO and tiles(v, N, H, H, C, K) > 0
             if sp:      # split-K: a two-buffer streamed tile, an under-filled grid, every split non-empty
                 assert v in ops._CONV_HALO_SK and tiles(v, N, H, H, C, K) < 256 and C // 64 >= 2
-                need = ops._ops().conv_halo_ws_bytes(v, N, H, H, C, K, sp)
+                need = ops._ops().conv_halo_ws_bytes(v, N, H, H, C, K, sp, 1)
                 assert ops.SPLITK_HEADER < need <= ops.SPLITK_WS_BYTES
         assert not ops.conv_halo_candidates(N, H, H, C, K, 3, 3, 1, 1, H, H, False)      # no bias
-        assert not ops.conv_halo_candidates(N, H, H, C, K, 3, 3, 2, 1, H // 2, H // 2, True)  # strided
+        # stride 2 (pad 1): streamed tiles only, never the resident-weight ones
+        s2 = ops.conv_halo_candidates(N, 2 * H, 2 * H, C, K, 3, 3, 2, 1, H, H, True)
+        assert all((c & 255) not in ops._CONV_HALO_RW for c in s2)
+        assert not ops.conv_halo_candidates(N, H, H, C, K, 3, 3, 2, 0, H // 2, H // 2, True)   # pad 0
     assert not ops.conv_halo_candidates(32, 56, 56, 96, 64, 3, 3, 1, 1, 56, 56, True)      # C % 64
     # stage 1 (56 wide): the 256-pixel tile takes 4 output rows; 64 px cannot hold one
     assert tiles(0, 32, 56, 56, 64, 64) == 32 * 14 and tiles(3, 32, 56, 56, 64, 64) == -1
