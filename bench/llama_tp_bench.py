@@ -36,11 +36,17 @@ def main(argv=None):
     ap.add_argument("--loop", default="native", choices=["native", "python"],
                     help="--serve: the native engine TP loop (NativeTP) or the Python TPReplica loop")
     ap.add_argument("--max-wait-ms", type=float, default=2.0, help="--serve: first-arrival batch timeout")
+    ap.add_argument("--compute-streams", type=int, default=1,
+                    help="--serve --loop native at TP = 1: batches overlapping on the GPU (TP > 1 runs one)")
+    ap.add_argument("--pipeline-depth", type=int, default=2)
     ap.add_argument("--json-out", default="")
     ap.add_argument("--checkpoint", default="", help="Hugging Face Llama checkpoint dir (each rank loads its shard)")
     ap.add_argument("--allreduce", default="xgmi", choices=["xgmi", "rccl"],
                     help="TP all-reduce: custom push-based xGMI kernel (fused RMSNorm) or RCCL")
     a = ap.parse_args(argv)
+    from ray_dynamic_batching_amd.runtime.queues import ensure_hw_queues
+
+    ensure_hw_queues(a.compute_streams)       # one HIP hardware queue per engine stream, before HIP starts
 
     import torch
     import torch.distributed as dist
@@ -200,7 +206,8 @@ def _serve_native(a, m, world, rank, name, job, buckets):
     if world > 1:
         dist.barrier()                        # rank 0 created the job
     ntp = NativeTP(m, name, 0, buckets, rank, world, "tp" if world > 1 else None, f"{name}_ring", 8,
-                   a.max_wait_ms / 1e3, pipeline_depth=2)
+                   a.max_wait_ms / 1e3, pipeline_depth=max(a.pipeline_depth, a.compute_streams),
+                   compute_streams=a.compute_streams if world == 1 else 1)
     if world == 1:
         ntp.unlink()                          # no follower to wait for: drop the ring's name now
     ntp.start()
@@ -225,6 +232,7 @@ def _serve_native(a, m, world, rank, name, job, buckets):
     ntp.stop()                                # STOP record: the followers leave
     lat = res["latency"]
     rep_out = dict(metric="Llama-3-8B bf16 TP prefill serving (<= 8 prompts / batch)", loop="native engine",
+                   compute_streams=a.compute_streams if world == 1 else 1,
                    tp=world, allreduce=a.allreduce if world > 1 else "none", seq_len=a.seq, layers=a.layers,
                    prompts_per_s=round(res["ok"] / res["elapsed_s"], 1), p50_ms=round(lat["p50_ms"], 3),
                    p99_ms=round(lat["p99_ms"], 3), ok=res["ok"], errors=res.get("errors", 0),

@@ -236,35 +236,41 @@ class NativeTP:
 
     def __init__(self, model, job_name: str, replica: int, buckets: List[int], rank: int, world: int,
                  group: Optional[str], ring: str, max_batch: int, max_wait_s: float, pipeline_depth: int = 2,
-                 batch_policy: str = "timeout", attach_timeout_s: float = 120.0):
+                 batch_policy: str = "timeout", attach_timeout_s: float = 120.0, compute_streams: int = 1):
         from ..parallel import collective as col
         from .engine import EngineRunner, SessionSpec
 
+        # one compute stream when world > 1: every rank must launch the same graphs (all-reduces
+        # inside) in the same order; a TP = 1 replica has no collectives and may overlap batches
+        if world > 1 and compute_streams != 1:
+            raise ValueError("NativeTP: a TP group runs one compute stream per rank (collectives in order)")
         self.rank, self.world, self.group = rank, world, group
         spec = SessionSpec(model=model, queue=replica, max_batch=max_batch, max_wait_s=max_wait_s, buckets=buckets)
-        # one compute stream: every rank must launch the same graphs in the same order
-        self.runner = EngineRunner(job_name, replica, [spec], pipeline_depth=max(2, pipeline_depth),
-                                   zero_copy=rank == 0, compute_streams=1, batch_policy=batch_policy,
+        self.runner = EngineRunner(job_name, replica, [spec], pipeline_depth=max(2, pipeline_depth, compute_streams),
+                                   zero_copy=rank == 0, compute_streams=compute_streams, batch_policy=batch_policy,
                                    tile_table="")
         # whole-forward tile tuning and the timed warm-up replay different numbers
         # of forwards per rank -- with collectives inside they would not pair up
         self.runner.tune_in_context = False
         self.runner.build(warm_s=0.0)
         eng = self.runner.engine
-        if rank == 0:
+        if world == 1:
+            pass                              # TP = 1: a plain engine, nothing to publish
+        elif rank == 0:
             eng.set_tp_leader(ring, world - 1, 8)
         else:
             eng.set_tp_follower(ring, rank - 1, attach_timeout_s)
         if group is not None:
             if world > 1:
                 col.barrier(group)            # every follower attached: the name can go
-            if rank == 0:
+            if rank == 0 and world > 1:
                 eng.unlink_tp()
         # (group None: ranks in one process -- tests; the caller unlinks via unlink())
         self.xg = col.get_xgmi(group) if (group and world > 1) else None
 
     def unlink(self) -> None:
-        self.runner.engine.unlink_tp()
+        if self.world > 1:
+            self.runner.engine.unlink_tp()
 
     def start(self) -> "NativeTP":
         self.runner.start()                   # rank 0: replica READY in shm
