@@ -1,6 +1,9 @@
-// Halo-tile 3x3 convolution (stride 1, pad 1, NHWC f16) on MFMA -- the ResNet-50
-// bottleneck 3x3 layers (the reference serves torchvision's
-// ResNet-50, 293-project/profiling/resnet50_*_summary.csv).
+// Halo-tile 3x3 convolution (pad 1, stride 1 or 2, NHWC f16) on MFMA -- the
+// ResNet-50 bottleneck 3x3 layers (the reference serves
+// torchvision's ResNet-50, 293-project/profiling/resnet50_*_summary.csv).
+// Stride 2 reads patch rows 2p + r / columns 2q + s (the formulas below are
+// written for stride 1); split-K over channel blocks and a persistent
+// resident-weight variant follow the streamed kernel.
 //
 // The im2col kernels (gemm_core.h Im2colLoader, gemm_pp.h CONV) stage one
 // (tap, 64-channel) K-tile at a time: every output pixel's input is fetched
