@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round 6: the driver's round-end GPU tier on this tree (cs3/d6 defaults, halo convs): smoke + pytest -m gpu.
 set -o pipefail
-O=gpurun_out/r6l
+O=gpurun_out/r6w
 mkdir -p $O
 export PYTHONUNBUFFERED=1
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail -20 $O/smoke.log; exit 1; }
