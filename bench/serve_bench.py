@@ -3,7 +3,8 @@ req/s vs p50/p99 latency for any servable model of the zoo.
 
 BASELINE config 2 (ResNet-50 fp16, 1 GPU, dyn-batch <= 32 / 5 ms, Poisson; one
 replica engine running three batches at a time on three compute streams, like bench.py):
-    python bench/serve_bench.py --model resnet50 --rates 2000,4000,8000,12000
+    python bench/serve_bench.py --model resnet50 --rates 8000,16000,32000,46000
+    python bench/serve_bench.py --model resnet50 --closed 128   # a 4th batch forms while 3 run
 Closed-loop saturation throughput:
     python bench/serve_bench.py --model bert-base --closed 96
 The same replica deployed through Serve (serve.run(model_deployment(...)) in
