@@ -201,6 +201,14 @@ class Engine {
     // (same kernel types at the same time: profiles/stamp_timeline_r5.json), staggered
     // ones pair different kernels
     stagger_ns_ = knob("RDB_ENGINE_STAGGER_US") * 1000;
+    // On the registered ring a batch's rows move with strided hipMemcpy2DAsync
+    // (one per run of consecutive ring slots) instead of the gather_rows kernel,
+    // so the H2D copy holds no CU: ResNet-50 closed loop 51.2k vs 49.1k img/s
+    // (profiles/engine_input_copy_r6.json).  RDB_ENGINE_DMA_GATHER=0 keeps the kernel.
+    {
+      const char* v = getenv("RDB_ENGINE_DMA_GATHER");
+      dma_gather_ = zero_copy_ && (v == nullptr || atoi(v) != 0);
+    }
     stream_running_.reset(new std::atomic<int>[compute_streams_.size()]);
     for (size_t i = 0; i < compute_streams_.size(); ++i) stream_running_[i].store(0);
     for (int s = 0; s < depth_; ++s) {
@@ -802,7 +810,26 @@ class Engine {
             bcast_->commit(r);
           }
           const uintptr_t in = s.in_dev[slot];
-          if (zero_copy_) {
+          if (dma_gather_) {
+            // rows of one batch are consecutive ring slots except at the wrap:
+            // one strided copy per run of equally spaced payloads
+            char* dst = reinterpret_cast<char*>(in);
+            int i0 = 0;
+            while (i0 < n) {
+              int i1 = i0 + 1;
+              const int64_t pitch = n > i0 + 1 ? (int64_t)(tbl[i0 + 1] - tbl[i0]) : (int64_t)s.in_row_bytes;
+              if (pitch >= s.in_row_bytes)
+                while (i1 < n && (int64_t)(tbl[i1] - tbl[i1 - 1]) == pitch) ++i1;
+              const char* src = host_base_ + (reinterpret_cast<char*>(tbl[i0]) - dev_base_);
+              ENG_CHECK(hipMemcpy2DAsync(dst + (size_t)i0 * s.in_row_bytes, s.in_row_bytes, src,
+                                         (size_t)std::max<int64_t>(pitch, s.in_row_bytes), s.in_row_bytes,
+                                         i1 - i0, hipMemcpyHostToDevice, copy_stream_));
+              i0 = i1;
+            }
+            if (rows > n)
+              ENG_CHECK(hipMemsetAsync(dst + (size_t)n * s.in_row_bytes, 0,
+                                       (size_t)(rows - n) * s.in_row_bytes, copy_stream_));
+          } else if (zero_copy_) {
             gather_rows(reinterpret_cast<uintptr_t>(tbl), n, rows, s.in_row_bytes, in,
                         reinterpret_cast<uintptr_t>(copy_stream_));
           } else {
@@ -1044,6 +1071,7 @@ class Engine {
   uint32_t replica_;
   int depth_;
   bool zero_copy_;
+  bool dma_gather_ = false;
   int device_;
   int policy_;
   bool registered_ = false;

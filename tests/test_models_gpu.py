@@ -163,6 +163,39 @@ def test_engine_serves_bert_tiny_correctly():
         j.close()
 
 
+@pytest.mark.parametrize("dma", ["1", "0"])
+def test_engine_input_copy_across_ring_wrap(dma, monkeypatch):
+    """Both input paths -- strided SDMA copies of consecutive ring slots (default)
+    and the gather_rows kernel (RDB_ENGINE_DMA_GATHER=0) -- serve the model's outputs,
+    including batches whose rows wrap around a small request ring."""
+    monkeypatch.setenv("RDB_ENGINE_DMA_GATHER", dma)
+    from ray_dynamic_batching_amd.models.bert import BertConfig, BertForSequenceClassification
+    from ray_dynamic_batching_amd.runtime import job as rjob
+    from ray_dynamic_batching_amd.runtime.engine import EngineRunner, SessionSpec
+
+    m = BertForSequenceClassification(BertConfig.tiny(seq_len=64), device="cuda", backend="hip", seed=4)
+    name = rjob.unique_job_name("engwrap")
+    j = rjob.Job(name, create=True, n_replicas=1, n_queues=1, n_clients=1, req_capacity=64,
+                 req_slot_bytes=64 * 4, cmp_slot_bytes=64)
+    j.configure_queue(0, 0, 0, 1024, 0.0, True)
+    runner = EngineRunner(name, 0, [SessionSpec(model=m, queue=0, max_batch=16, max_wait_s=0.002)]).build()
+    runner.start()
+    try:
+        c = rjob.Client(j)
+        ids = m.example_input(200, seed=13).cpu()
+        got = {}
+        for c0 in range(0, 200, 40):   # 40 in flight: the ring (64 slots) wraps every other chunk
+            part = _serve_all(c, rjob, 0, [ids[i].numpy().tobytes() for i in range(c0, c0 + 40)])
+            got.update({c0 + k: v for k, v in part.items()})
+        ref = m(ids.cuda()).cpu()
+        out = torch.stack([torch.tensor(struct.unpack("<2f", got[i])) for i in range(200)])
+        assert torch.allclose(out, ref, atol=2e-2, rtol=2e-2), (out - ref).abs().max()
+        assert runner.error() == ""
+    finally:
+        runner.stop()
+        j.close()
+
+
 def test_engine_stale_drop_with_deadline():
     from ray_dynamic_batching_amd.models.bert import BertConfig, BertForSequenceClassification
     from ray_dynamic_batching_amd.runtime import job as rjob
