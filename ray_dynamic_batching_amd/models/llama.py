@@ -152,6 +152,20 @@ class LlamaTP:
             return t.unsqueeze(0)
         from ..parallel import collective as col
 
+        xg = self._xgmi()
+        if xg is not None and t.element_size() == 4:
+            # over the xGMI all-reduce (graph-capturable on any host group, gloo
+            # included): rank r writes its tensor's BYTES as bf16 integers 0..255
+            # into row r of a zero [tp, D] block; the sum over ranks is then the
+            # gather, exactly (x + 0 in f32, integers < 256 exact in bf16)
+            nb = t.numel() * 4
+            D = -(-nb // 8) * 8
+            buf = torch.zeros((self.tp, D), device=t.device, dtype=xg.dtype)
+            buf[self.rank, :nb] = t.contiguous().view(-1).view(torch.uint8).to(xg.dtype)
+            if self.pre_collective is not None:
+                self.pre_collective()
+            g = xg.all_reduce(buf)[:, :nb].to(torch.uint8).contiguous()
+            return g.view(t.dtype).view((self.tp,) + tuple(t.shape))
         out = torch.empty((self.tp,) + tuple(t.shape), device=t.device, dtype=t.dtype)
         col.allgather_into(out.view(self.tp * t.shape[0], *t.shape[1:]) if t.dim() else out, t,
                            self.group or "default")

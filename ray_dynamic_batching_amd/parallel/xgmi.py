@@ -101,6 +101,11 @@ class XgmiCommunicator:
         import os
 
         self.norm_store = int(os.environ.get("RDB_XGMI_NORM_STORE", "0"))
+        # cap on the kernel's blocks (rows are grid-strided; every rank of a group
+        # must use the same cap: barriers are per block).  A TP group rehearsed on
+        # ONE GPU sets it low (RDB_XGMI_MAX_GRID=8): ranks spinning in the kernel
+        # then hold at most world x 8 CU slots, never every CU a peer's GEMM needs.
+        self.max_grid = max(1, min(256, int(os.environ.get("RDB_XGMI_MAX_GRID", "256"))))
         self.debug_ptr = 0          # set by enable_debug(): per-block launch-view records
 
     # -- construction ---------------------------------------------------------
@@ -173,7 +178,7 @@ class XgmiCommunicator:
         if two_shot is None:
             two_shot = self.world > 1 and nbytes > self.one_shot_max_bytes
         rows_per_block = -(-T // self.world) if two_shot else T
-        grid = max(1, min(256, rows_per_block))
+        grid = max(1, min(self.max_grid, rows_per_block))
         _ops().xgmi_allreduce(_DT[self.dtype], self.recv, self.gather, self.sig, self.rank, x.data_ptr(),
                               norm_out.data_ptr() if norm_out is not None else 0,
                               gamma.data_ptr() if gamma is not None else 0, float(eps), T, D, self.slot_elems,

@@ -131,8 +131,11 @@ def _run_tp(spec, cfg, r, stop, tp, gpu) -> int:
     init_tp_group(backend, "tp", tp)
     logger.info("TP rank %d/%d joined group %s epoch %d over %s in %.2fs", tp.rank, tp.world, tp.group, tp.epoch,
                 backend, time.time() - t0)
-    if use_gpu and backend == "nccl" and os.environ.get("RDB_TP_XGMI", "0") == "1":
-        col.enable_xgmi("tp")           # the custom xGMI all-reduce (fused residual + RMSNorm)
+    if use_gpu and os.environ.get("RDB_TP_XGMI", "0") == "1":
+        # the custom xGMI all-reduce (fused residual + RMSNorm), over RCCL or -- a TP
+        # group rehearsed on ONE GPU, where RCCL refuses two ranks per device -- gloo
+        # host groups (IPC handles exchanged over either)
+        col.enable_xgmi("tp")
     factory = sv["factory"]
     model = factory(device="cuda" if use_gpu else "cpu", tp_rank=tp.rank, tp_size=tp.world, group_name="tp")
     if use_gpu and tp.world > 1 and os.environ.get("RDB_TP_LINE_UP", "0") == "1" and hasattr(model, "pre_collective"):
