@@ -37,7 +37,12 @@ def shipped_tile_table(model, max_batch: int, compute_streams: int, pipeline_dep
         p = os.path.join(TUNED_DIR, n)
         if os.path.exists(p):
             return p
-    return ""
+    # same stream count, another pipeline depth: the tiles were picked for as many
+    # overlapped batches, which the depth (slots waiting for a stream) does not change
+    import glob
+
+    same_cs = sorted(glob.glob(os.path.join(TUNED_DIR, f"mi355x_{sig}_B{max_batch}_cs{compute_streams}_d*.json")))
+    return same_cs[0] if same_cs else ""
 
 
 def resolve_tile_table(choice: str, model, max_batch: int, compute_streams: int, pipeline_depth: int) -> str:

@@ -45,6 +45,9 @@ def test_model_deployment_defaults_are_the_benchmarked_replica():
     p = shipped_tile_table(_FakeBert(), 32, 3, 6)
     assert p == os.path.join(TUNED_DIR, "mi355x_bert_L12_S128_B32_cs3_d6.json") and os.path.exists(p)
     assert shipped_tile_table(_FakeBert(), 32, 2, 4).endswith("mi355x_bert_L12_S128_B32_cs2_d4.json")
+    # a single-stream replica replays the single-stream table whatever its depth
+    assert shipped_tile_table(_FakeBert(), 32, 1, 2).endswith("mi355x_bert_L12_S128_B32_cs1_d2.json")
+    assert shipped_tile_table(_FakeBert(), 32, 1, 4).endswith("mi355x_bert_L12_S128_B32_cs1_d2.json")
 
 
 def test_replica_engine_receives_configured_streams_and_table():
