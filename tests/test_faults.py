@@ -30,6 +30,10 @@ def env_knobs():
 
 def test_replica_killer_agent_restarts_and_requests_complete(env_knobs):
     env_knobs["RDB_FAULT_KILL_AFTER_BATCHES"] = "6"
+    # restarts back off 0.5 s doubling per restart (cap 30 s): a replica killed every
+    # 6 batches restarts ~8 times for 120 requests, whose doubling delays alone can
+    # outlast the 60 s re-dispatch window when batches are small (CPU load) -- cap them
+    env_knobs["RDB_RESTART_BACKOFF_MAX_S"] = "1.0"
     # a replica that dies every 6 batches takes every request it holds with it:
     # give them a re-dispatch budget above the default 3 (the cap exists for a
     # request that kills every replica it reaches, tests/test_router_retry.py)
@@ -52,7 +56,8 @@ def test_replica_killer_agent_restarts_and_requests_complete(env_knobs):
 
 def test_injected_message_loss_is_redispatched(env_knobs):
     env_knobs["RDB_FAULT_DROP_EVERY"] = "5"
-    h = serve.run(Mul.bind(2), mode="process")
+    # a re-dispatched request can land on the 5th slot again: budget above the default 3
+    h = serve.run(Mul.options(max_request_retries=20).bind(2), mode="process")
     outs = [h.remote(i) for i in range(60)]
     assert [o.result(timeout_s=60) for o in outs] == [2 * i for i in range(60)]
 
