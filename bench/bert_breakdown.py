@@ -43,7 +43,8 @@ def main():
     s.wait_stream(torch.cuda.current_stream())
     with torch.cuda.stream(s):
         m(ids)
-        with torch.cuda.graph(g, stream=s):
+        # split-K launches share one workspace, as in the engine's graphs (ops.capture_splitk_workspace)
+        with torch.cuda.graph(g, stream=s), ops.capture_splitk_workspace(ops.splitk_workspace("cuda:0")):
             m(ids)
     torch.cuda.synchronize()
     for _ in range(5):

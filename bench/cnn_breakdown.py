@@ -41,7 +41,8 @@ def main():
     s.wait_stream(torch.cuda.current_stream())
     with torch.cuda.stream(s):
         m(x)
-        with torch.cuda.graph(g, stream=s):
+        # split-K launches share one workspace, as in the engine's graphs (ops.capture_splitk_workspace)
+        with torch.cuda.graph(g, stream=s), ops.capture_splitk_workspace(ops.splitk_workspace("cuda:0")):
             m(x)
     torch.cuda.synchronize()
     for _ in range(5):

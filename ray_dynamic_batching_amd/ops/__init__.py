@@ -10,8 +10,10 @@ eager baseline path of the models (``backend="torch"``).
 """
 from __future__ import annotations
 
+import contextlib
 import math
 import os
+import threading
 from typing import Callable, Dict, Optional, Tuple
 
 import torch
@@ -1273,7 +1275,22 @@ _TILE_BM = (128, 64, 128, 64, 128, 192, 256, 128, 128, 64, 128, 256, 128)   # ge
 _TILE_BN = (128, 128, 64, 64, 192, 128, 128, 256, 144, 96, 96, 144, 48)
 _tune_ws: Dict[int, torch.Tensor] = {}
 _priv_ws: Dict[tuple, torch.Tensor] = {}
-_cap_ws: Dict[tuple, tuple] = {}   # (device, stream) -> (capture id, split-K workspace of that capture)
+_cap_ws_local = threading.local()    # .ws: the split-K workspace of the capture running on this thread
+
+
+@contextlib.contextmanager
+def capture_splitk_workspace(ws: Optional[torch.Tensor]):
+    """Graph captures inside this block give their split-K launches (those
+    without a caller workspace) ``ws`` instead of a memset graph-pool workspace per
+    launch.  ``ws`` (``splitk_workspace``, zeroed counters) must be used only by
+    graphs that never run concurrently -- the engine keeps one per compute stream.
+    Thread-local: a live capture on another thread is unaffected."""
+    prev = getattr(_cap_ws_local, "ws", None)
+    _cap_ws_local.ws = ws
+    try:
+        yield ws
+    finally:
+        _cap_ws_local.ws = prev
 
 
 def splits_of(c: int) -> int:
@@ -1289,29 +1306,19 @@ def _private_splitk_ws(device, need: int) -> torch.Tensor:
     (device, stream), grown on demand, so a forward that passes none pays no
     allocation or counter memset per call.  Split-K launches leave the counters
     zero, so consecutive launches on one stream may share it (two streams never do).
-    Inside a graph capture the workspace comes from the graph's own pool, zeroed
-    by ONE memset node, and is shared only by the launches of that capture on that
-    stream (keyed by the HIP capture id; they run in stream order and leave the
-    counters zero): one memset per graph instead of one per split-K launch (12
-    fill kernels, ~45 us, per single-stream BERT forward with split-K FFN-down).
-    It is never shared across captures -- graphs the engine replays concurrently
-    on different streams must not share one -- and the first launch outside a
-    capture drops it, so it does not pin the capture pool past the graph."""
+    Inside a graph capture it is the workspace the capturing code installed with
+    ``capture_splitk_workspace`` (the engine: one per compute stream, shared by the
+    graphs replayed on that stream, which run in stream order and leave the
+    counters zero -- no memset node at all), else a fresh one from the graph's own
+    pool zeroed by a memset node per launch (never cached: a cached one would be
+    shared by graphs replayed concurrently on different streams, and would keep
+    the capture pool alive past the graph)."""
     need = max(SPLITK_HEADER, int(need))
     if torch.cuda.is_current_stream_capturing():
-        sid = _stream()
-        cid = int(_ops().stream_capture_id(sid))
-        key = (str(device), sid)
-        ent = _cap_ws.get(key)
-        if cid == 0 or ent is None or ent[0] != cid or ent[1].numel() < need:
-            ent = (cid, splitk_workspace(device, need))
-            if cid != 0:
-                for k in [k for k, v in _cap_ws.items() if int(_ops().stream_capture_id(k[1])) != v[0]]:
-                    del _cap_ws[k]        # captures that have ended: release their pool blocks
-                _cap_ws[key] = ent
-        return ent[1]
-    if _cap_ws:
-        _cap_ws.clear()
+        ws = getattr(_cap_ws_local, "ws", None)
+        if ws is not None and ws.numel() >= need:
+            return ws
+        return splitk_workspace(device, need)
     key = (str(device), _stream())
     ws = _priv_ws.get(key)
     if ws is None or ws.numel() < need:

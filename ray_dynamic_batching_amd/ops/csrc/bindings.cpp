@@ -128,14 +128,6 @@ PYBIND11_MODULE(_rdb_ops, m) {
   m.def("conv_halo_tiles", &rdb::conv_halo_tiles);
   m.def("conv_halo_ws_bytes", &rdb::conv_halo_ws_bytes);
   m.def("conv_halo_tiles_s", &rdb::conv_halo_tiles_s);
-  // id of the graph capture running on `stream` (0 = not capturing): lets a
-  // capture share one split-K workspace across its launches (ops._private_splitk_ws)
-  m.def("stream_capture_id", [](uintptr_t stream) -> unsigned long long {
-    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
-    unsigned long long id = 0;
-    if (hipStreamGetCaptureInfo(reinterpret_cast<hipStream_t>(stream), &st, &id) != hipSuccess) return 0ULL;
-    return st == hipStreamCaptureStatusActive ? id : 0ULL;
-  });
   m.def("maxpool_nhwc", &rdb::maxpool_nhwc, py::call_guard<py::gil_scoped_release>());
   m.def("avgpool_nhwc", &rdb::avgpool_nhwc, py::call_guard<py::gil_scoped_release>());
   m.def("dwconv_nhwc", &rdb::dwconv_nhwc, py::call_guard<py::gil_scoped_release>());

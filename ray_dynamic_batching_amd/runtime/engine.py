@@ -267,11 +267,18 @@ class EngineRunner:
         s.graphs = [[None] * self.depth for _ in buckets]
         s.outputs = [[None] * self.depth for _ in buckets]
         mode = "thread_local" if live else "global"
+        from .. import ops
+
+        # one split-K workspace per compute stream, shared by every graph replayed
+        # on that stream (they run in stream order): no memset node per split-K launch
+        if not getattr(self, "_stream_ws", None):
+            self._stream_ws = [ops.splitk_workspace(dev) for _ in range(self.compute_streams)]
         for bi, b in enumerate(buckets):
             for slot in range(self.depth):
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g, pool=pools[slot % self.compute_streams], stream=side,
-                                      capture_error_mode=mode):
+                                      capture_error_mode=mode), \
+                        ops.capture_splitk_workspace(self._stream_ws[slot % self.compute_streams]):
                     y = m.forward(s.inputs[slot][:b])
                 if not y.is_contiguous():
                     raise RuntimeError("servable model output must be contiguous")
@@ -363,6 +370,7 @@ class EngineRunner:
         streams = max(1, streams)
         pools = [torch.cuda.graph_pool_handle() for _ in range(streams)]
         sts = [torch.cuda.Stream(device=dev) for _ in range(streams)]
+        sk_ws = [ops.splitk_workspace(dev) for _ in range(streams)]     # as the engine's graphs get them
 
         def time_forward() -> float:
             gs = []
@@ -370,7 +378,7 @@ class EngineRunner:
                 g = torch.cuda.CUDAGraph()
                 sts[i].wait_stream(torch.cuda.current_stream())
                 with torch.cuda.stream(sts[i]):
-                    with torch.cuda.graph(g, pool=pools[i], stream=sts[i]):
+                    with torch.cuda.graph(g, pool=pools[i], stream=sts[i]), ops.capture_splitk_workspace(sk_ws[i]):
                         m.forward(x)
                 gs.append(g)
             torch.cuda.synchronize()

@@ -467,45 +467,42 @@ def test_linear_splitk(M, N, K):
         _close(y, x.float() @ w.float().t() + b.float() + r.float(), 2e-2, 2e-2)
 
 
-def test_linear_splitk_one_workspace_per_capture():
-    """Consecutive split-K launches of ONE capture share one graph-pool workspace
-    (one memset node per graph, not one per launch), keyed by the HIP capture id;
-    every chained output is right on replay, and an eager launch drops the entry."""
+def test_linear_splitk_capture_workspace():
+    """``capture_splitk_workspace``: every split-K launch of a capture (no caller
+    workspace) uses the installed workspace -- no memset node per launch, the
+    engine's per-compute-stream workspace -- chained outputs are right on every
+    replay and the counters are back to zero; outside the block the private
+    per-launch behaviour is unchanged."""
     ops = _ops()
     torch.manual_seed(5)
     M, N, K = 512, 768, 3072
     x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
     ws_ = [torch.randn(N, K, device="cuda", dtype=torch.bfloat16) * K ** -0.5 for _ in range(3)]
     w2 = torch.randn(K, N, device="cuda", dtype=torch.bfloat16) * N ** -0.5
+    cws = ops.splitk_workspace("cuda")
     side = torch.cuda.Stream()
     side.wait_stream(torch.cuda.current_stream())
-    assert int(ops._ops().stream_capture_id(side.cuda_stream)) == 0
     with torch.cuda.stream(side):
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, stream=side):
-            cid = int(ops._ops().stream_capture_id(torch.cuda.current_stream().cuda_stream))
+        with torch.cuda.graph(g, stream=side), ops.capture_splitk_workspace(cws):
+            assert ops._private_splitk_ws(x.device, 1 << 20) is cws
             ys = []
             h = x
             for w in ws_:
-                y = ops.linear(h, w, tile_cfg=19 | (2 << 8))           # split-K, private workspace
+                y = ops.linear(h, w, tile_cfg=19 | (2 << 8))           # split-K, no caller workspace
                 ys.append(y)
                 h = ops.linear(y, w2, tile_cfg=19 | (2 << 8))          # back to K wide, split-K again
-        assert cid != 0
-        mine = [k for k, v in ops._cap_ws.items() if v[0] == cid]
-        assert len(mine) == 1 and mine[0][1] == side.cuda_stream
-        assert len(ops._cap_ws) == 1           # entries of ended captures were released
+        assert getattr(ops._cap_ws_local, "ws", None) is None
     torch.cuda.synchronize()
-    for _ in range(2):
+    for _ in range(3):
         x.copy_(torch.randn_like(x))
         g.replay()
         torch.cuda.synchronize()
         h = x.float()
         for w, y in zip(ws_, ys):
-            ref = h @ w.float().t()
-            _close(y, ref, 3e-2, 3e-2)
+            _close(y, h @ w.float().t(), 3e-2, 3e-2)
             h = y.float() @ w2.float().t()
-    ops.linear(x, ws_[0], tile_cfg=19 | (2 << 8))
-    assert len(ops._cap_ws) == 0
+        assert int(cws[:ops.SPLITK_HEADER].view(torch.int32).abs().sum()) == 0
 
 
 def test_linear_splitk_private_workspace_per_graph():
