@@ -31,6 +31,27 @@ import torch.nn.functional as F
 from .. import ops
 
 
+def gather_rows_for_sum(t: torch.Tensor, rank: int, world: int, dtype: torch.dtype) -> torch.Tensor:
+    """An all-gather carried by a SUM all-reduce: rank ``rank``'s 4-byte tensor
+    ``t`` as its raw bytes (integers 0..255, exact in bf16 / f16) in row ``rank``
+    of an otherwise zero [world, D] block (D = bytes rounded up to 8, the xGMI
+    kernel's row granularity).  Summing the blocks of all ranks (x + 0, f32
+    accumulation) yields every rank's bytes; ``gathered_from_sum`` decodes."""
+    if t.element_size() != 4:
+        raise ValueError("gather_rows_for_sum: 4-byte elements")
+    nb = t.numel() * 4
+    buf = torch.zeros((world, -(-nb // 8) * 8), device=t.device, dtype=dtype)
+    buf[rank, :nb] = t.contiguous().view(-1).view(torch.uint8).to(dtype)
+    return buf
+
+
+def gathered_from_sum(summed: torch.Tensor, like: torch.Tensor) -> torch.Tensor:
+    """[world, D] summed byte rows -> [world, *like.shape] tensors of like's dtype."""
+    nb = like.numel() * 4
+    g = summed[:, :nb].to(torch.uint8).contiguous()
+    return g.view(like.dtype).view((summed.shape[0],) + tuple(like.shape))
+
+
 @dataclass
 class LlamaConfig:
     vocab_size: int = 128256
@@ -158,14 +179,10 @@ class LlamaTP:
             # included): rank r writes its tensor's BYTES as bf16 integers 0..255
             # into row r of a zero [tp, D] block; the sum over ranks is then the
             # gather, exactly (x + 0 in f32, integers < 256 exact in bf16)
-            nb = t.numel() * 4
-            D = -(-nb // 8) * 8
-            buf = torch.zeros((self.tp, D), device=t.device, dtype=xg.dtype)
-            buf[self.rank, :nb] = t.contiguous().view(-1).view(torch.uint8).to(xg.dtype)
+            buf = gather_rows_for_sum(t, self.rank, self.tp, xg.dtype)
             if self.pre_collective is not None:
                 self.pre_collective()
-            g = xg.all_reduce(buf)[:, :nb].to(torch.uint8).contiguous()
-            return g.view(t.dtype).view((self.tp,) + tuple(t.shape))
+            return gathered_from_sum(xg.all_reduce(buf), t)
         out = torch.empty((self.tp,) + tuple(t.shape), device=t.device, dtype=t.dtype)
         col.allgather_into(out.view(self.tp * t.shape[0], *t.shape[1:]) if t.dim() else out, t,
                            self.group or "default")
