@@ -3,7 +3,7 @@
 # captured in the bucket graphs, grid capped, no line-up barrier): world 2, then world 8, then the
 # line-up rehearsal (now on the xGMI all-reduce over the gloo host group).
 set -o pipefail
-O=gpurun_out/r6ac
+O=gpurun_out/r6ac2
 mkdir -p $O
 export PYTHONUNBUFFERED=1
 P="python -u -m pytest -x -v -s --timeout 300 --timeout-method thread -m gpu"
