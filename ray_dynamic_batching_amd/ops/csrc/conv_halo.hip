@@ -57,6 +57,17 @@ __device__ unsigned long long rdb_halo_stamps[4096][8];
   } while (0)
 #endif
 
+// Patch swizzle: 16-B chunk c of patch row r lives at slot c ^ (r & 7).  The GEMM tiles'
+// c ^ ((r >> 1) & 7) (swz_off) is conflict-free for 16 consecutive 16-aligned fragment
+// rows; the patch is read at rows prow + toff -- any offset, wrapping at the padded
+// image width, and 2 apart at stride 2 -- where that key costs 1.7-3.0x the LDS cycles
+// of a conflict-free ds_read_b128 and r & 7 1.1-2.0x (tools/lds_conflict_model_halo.py;
+// PMC: 0.39-0.41 of the halo kernels' LDS cycles were bank conflicts,
+// profiles/pmc_resnet50_forward_r6_cs1.json).  Weights keep swz_off.
+__device__ __forceinline__ int pswz_off(int row, int chunk) { return row * 128 + ((chunk ^ (row & 7)) << 4); }
+// the DMA side of it: lane slot (tid & 7) of patch row `row` loads chunk slot ^ (row & 7)
+__device__ __forceinline__ int pdma_chunk(int tid, int row) { return (tid & 7) ^ (row & 7); }
+
 template <int N>
 __device__ __forceinline__ void vm_wait() {
   static_assert(N >= 0 && N < 64, "vmcnt field is 6 bits");
@@ -126,7 +137,7 @@ conv3x3_halo_kernel(const f16* __restrict__ x, const f16* __restrict__ w, f16* _
     int ph = rem / g.Wp, pw = rem - ph * g.Wp;
 #pragma unroll
     for (int i = 0; i < LP; ++i) {
-      const int ch = dma_chunk(tid, row);
+      const int ch = pdma_chunk(tid, row);
       const int n = n_first + gi, h = g.S * p0 - 1 + ph, ww = pw - 1;
       const bool ok = row < g.PR && n < g.N && (unsigned)h < (unsigned)g.H && (unsigned)ww < (unsigned)g.W;
       poff[i] = ok ? (uint32_t)((((n * g.H + h) * g.W + ww) * g.C) * 2 + ch * 16) : kOOB;
@@ -244,7 +255,7 @@ conv3x3_halo_kernel(const f16* __restrict__ x, const f16* __restrict__ w, f16* _
         wf[ks][i] = *reinterpret_cast<const frag*>(pw + swz_off(wn * WN + i * 16 + fr, ks * 4 + fg));
 #pragma unroll
       for (int j = 0; j < TM; ++j)
-        af[ks][j] = *reinterpret_cast<const frag*>(pa + (swz_off(prow[j] + toff, fg) ^ (ks << 6)));
+        af[ks][j] = *reinterpret_cast<const frag*>(pa + (pswz_off(prow[j] + toff, fg) ^ (ks << 6)));
     }
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
@@ -404,7 +415,7 @@ conv3x3_halo_rw_kernel(const f16* __restrict__ x, const f16* __restrict__ w, f16
     int ph = rem / g.Wp, pw = rem - ph * g.Wp;
 #pragma unroll
     for (int i = 0; i < LP; ++i) {
-      const int ch = dma_chunk(tid, row);
+      const int ch = pdma_chunk(tid, row);
       prel[i] = ((gi * g.H + ph) * g.W + pw) * g.C * 2 + ch * 16;
       pph[i] = ph;
       pgi[i] = row < g.PR ? gi : 1 << 20;             // rows past the patch: never valid
@@ -456,7 +467,7 @@ conv3x3_halo_rw_kernel(const f16* __restrict__ x, const f16* __restrict__ w, f16
 #pragma unroll
   for (int tap = 0; tap < 9; ++tap)
 #pragma unroll
-    for (int j = 0; j < TM; ++j) aoff[tap][j] = swz_off(prow[j] + (tap / 3) * g.Wp + tap % 3, fg);
+    for (int j = 0; j < TM; ++j) aoff[tap][j] = pswz_off(prow[j] + (tap / 3) * g.Wp + tap % 3, fg);
   // epilogue addressing (tile-independent parts): output row offsets and column offsets
   int lrow[TM];
 #pragma unroll
