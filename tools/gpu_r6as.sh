@@ -2,7 +2,7 @@
 # Round 6: confirmation of the re-tuned ResNet-50 cs3 table (candidate, tools/gpu_r6ar.sh t2) vs the shipped one,
 # closed loop 128, interleaved x3 on a fresh box.
 set -o pipefail
-O=gpurun_out/r6as
+O=gpurun_out/${OUT:-r6as}
 mkdir -p $O
 export PYTHONUNBUFFERED=1
 S=$PWD/ray_dynamic_batching_amd/ops/tuned/mi355x_resnet50_B32_cs3_d6.json
