@@ -2,7 +2,7 @@
 # Round 6 closing run on the final tree (halo patch swizzle included): smoke + pytest -m gpu (the driver's
 # round-end tier), then the driver's bench command x5 and ResNet-50 closed loop 128 x2.
 set -o pipefail
-O=gpurun_out/r6aq
+O=gpurun_out/${OUT:-r6aq}
 mkdir -p $O
 export PYTHONUNBUFFERED=1
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail -20 $O/smoke.log; exit 1; }
